@@ -1,0 +1,69 @@
+// dmx_device.h -- device-side helpers shared by the deflate and inflate kernels (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dmx {
+
+// RFC 1951 length / distance tables; the same values as the reference's RangeLookup
+// (common.hpp:508-575).
+__constant__ const uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,
+                                            15, 17, 19, 23, 27, 31, 35, 43, 51,  59,
+                                            67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ const uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
+                                            2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ const uint16_t kDistBase[30] = {1,    2,    3,    4,     5,     7,    9,    13,
+                                             17,   25,   33,   49,    65,    97,   129,  193,
+                                             257,  385,  513,  769,   1025,  1537, 2049, 3073,
+                                             4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ const uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3,  3,  4,  4,  5,  5,  6,
+                                             6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+// code-length code order (RFC 1951 3.2.7; reference inflate.hpp:137-157)
+__constant__ const uint8_t kPerm[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5,
+                                        11, 4,  12, 3, 13, 2, 14, 1, 15};
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// length 3..258 -> lit/len symbol 257..285
+__device__ __forceinline__ uint32_t len_sym(uint32_t L) {
+    if (L <= 10) return 254 + L;
+    if (L == 258) return 285;
+    uint32_t x = L - 3;               // 8..254
+    uint32_t k = 31 - __clz(x);       // 3..7
+    return 257 + 4 * (k - 1) + ((x >> (k - 2)) & 3);
+}
+// distance 1..32768 -> distance symbol 0..29
+__device__ __forceinline__ uint32_t dist_sym(uint32_t d) {
+    if (d <= 4) return d - 1;
+    uint32_t x = d - 1;
+    uint32_t k = 31 - __clz(x);       // >= 2
+    return 2 * k + ((x >> (k - 1)) & 1);
+}
+
+__device__ __forceinline__ uint32_t bitrev(uint32_t v, uint32_t n) {
+    return n ? (__builtin_bitreverse32(v) >> (32 - n)) : 0;
+}
+
+// unaligned 32-bit read from an LDS byte image accessed as words (image padded by >= 8 B)
+__device__ __forceinline__ uint32_t ld32u(const uint32_t* w, uint32_t p) {
+    uint32_t i = p >> 2, sh = p & 3;
+    return __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+}
+
+// inclusive wave64 scan (sum)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, 64);
+        if (l >= d) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+}  // namespace dmx

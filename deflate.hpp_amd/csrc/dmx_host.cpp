@@ -1,0 +1,416 @@
+// dmx_host.cpp -- host runtime and C-ABI of libdmx (see include/dmx.h).
+//
+// A context owns one HIP device, one non-blocking stream and grow-only device scratch
+// (segment slots, size/offset arrays, candidate lists, look-back words).  Every entry point
+// locks the context, so a context may be shared between threads; the default context is
+// created once per process (std::call_once) on the caller's current device.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+
+#include "../../include/dmx.h"
+#include "dmx_internal.h"
+
+using namespace dmx;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool ensure(size_t bytes) {
+        if (bytes <= cap) return true;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 8 + 4096;
+        if (hipMalloc(&p, want) != hipSuccess) {
+            p = nullptr;
+            return false;
+        }
+        cap = want;
+        return true;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+constexpr uint32_t kSegCap = 32768;  // LDS window of k_inflate_segments
+
+}  // namespace
+
+struct dmx_ctx {
+    int device = 0;
+    uint32_t seg = 32768;
+    uint32_t flags = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    DevBuf in, out, slots, sizes, offs, scal, cands, tiles, tileoffs, recs, status;
+    bool timing = false;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    dmx_stats stats{};
+};
+
+namespace {
+
+#define HIPCHK(x)                                   \
+    do {                                            \
+        if ((x) != hipSuccess) return DMX_ERR_DEVICE; \
+    } while (0)
+
+struct Scal {  // small device-side scalars, one allocation
+    uint64_t total;
+    uint64_t nmarkers;
+    uint32_t ticket;
+    uint32_t pad;
+    InflateResult res;
+};
+
+void begin_timing(dmx_ctx* c, hipStream_t st) {
+    c->stats = dmx_stats{};
+    if (c->timing) (void)hipEventRecord(c->ev[0], st);
+}
+void end_timing(dmx_ctx* c, hipStream_t st) {
+    if (!c->timing) return;
+    (void)hipEventRecord(c->ev[3], st);
+    (void)hipEventSynchronize(c->ev[3]);
+    float a = 0, b = 0;
+    (void)hipEventElapsedTime(&a, c->ev[0], c->ev[3]);
+    (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
+    c->stats.ms_device_total = a;
+    c->stats.ms_main_kernel = b;
+}
+
+int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, uint32_t flags,
+                          uint8_t* d_out, size_t cap, size_t* out_len, hipStream_t st) {
+    if (level < 0 || level > 3) level = 1;  // reference switch has no default (deflate.hpp:699)
+    const bool final_last = (flags & DMX_DEFLATE_NOT_FINAL) == 0;
+    begin_timing(c, st);
+    if (n == 0) {
+        // empty input: one empty fixed-Huffman final block, as the reference's levels 1-3
+        static const uint8_t empty_final[2] = {0x03, 0x00};
+        *out_len = final_last ? 2 : 0;
+        if (!final_last) return DMX_OK;
+        if (cap < 2) return DMX_ERR_CAPACITY;
+        HIPCHK(hipMemcpyAsync(d_out, empty_final, 2, hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+        return DMX_OK;
+    }
+    const uint64_t nseg = (n + c->seg - 1) / c->seg;
+    const uint32_t slot_bytes = c->seg + 256;
+    if (!c->slots.ensure(nseg * (size_t)slot_bytes) || !c->sizes.ensure(nseg * 4) ||
+        !c->offs.ensure(nseg * 8) || !c->scal.ensure(sizeof(Scal)))
+        return DMX_ERR_NOMEM;
+    DeflateArgs A;
+    A.in = d_in;
+    A.n = n;
+    A.nseg = nseg;
+    A.level = level;
+    A.final_last = final_last ? 1 : 0;
+    A.slots = c->slots.as<uint8_t>();
+    A.slot_bytes = slot_bytes;
+    A.sizes = c->sizes.as<uint32_t>();
+    A.offsets = c->offs.as<uint64_t>();
+    A.total = &c->scal.as<Scal>()->total;
+    A.out = d_out;
+    A.cap = cap;
+    HIPCHK(launch_deflate(A, c->seg, st, c->timing ? c->ev[1] : nullptr, c->timing ? c->ev[2] : nullptr));
+    uint64_t total = 0;
+    HIPCHK(hipMemcpyAsync(&total, A.total, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    end_timing(c, st);
+    c->stats.segments = nseg;
+    c->stats.in_bytes = n;
+    c->stats.out_bytes = total;
+    *out_len = total;
+    return total > cap ? DMX_ERR_CAPACITY : DMX_OK;
+}
+
+// Shared inflate driver.  fixed_out != nullptr: decode into the caller's device buffer of
+// `cap` bytes.  Otherwise decode into c->out, grown as needed (*dev_out receives it).
+int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_out,
+                          size_t cap, size_t* total_out, uint8_t** dev_out, hipStream_t st) {
+    begin_timing(c, st);
+    *total_out = 0;
+    if (n == 0) return DMX_ERR_OVERREAD;  // the reference throws (or faults) on empty input
+    if (!c->scal.ensure(sizeof(Scal))) return DMX_ERR_NOMEM;
+    Scal* ds = c->scal.as<Scal>();
+    const uint64_t misalign = (uintptr_t)d_in & 3;
+    const uint32_t* words = reinterpret_cast<const uint32_t*>(d_in - misalign);
+
+    // candidate segment starts
+    const uint64_t ntiles = marker_tiles(n, misalign);
+    if (!c->tiles.ensure(ntiles * 4) || !c->tileoffs.ensure(ntiles * 8)) return DMX_ERR_NOMEM;
+    HIPCHK(launch_marker_count(words, misalign, n, c->tiles.as<uint32_t>(), ntiles, st));
+    HIPCHK(launch_scan_u32(c->tiles.as<uint32_t>(), c->tileoffs.as<uint64_t>(), ntiles, &ds->nmarkers, st));
+    uint64_t nmarkers = 0;
+    HIPCHK(hipMemcpyAsync(&nmarkers, &ds->nmarkers, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint64_t ncand = nmarkers + 1;
+    if (!c->cands.ensure(ncand * 8) || !c->recs.ensure(ncand * sizeof(SegRecord)) ||
+        !c->status.ensure(ncand * 8))
+        return DMX_ERR_NOMEM;
+    HIPCHK(launch_marker_write(words, misalign, n, c->tileoffs.as<uint64_t>(), ntiles,
+                               c->cands.as<uint64_t>(), nullptr, st));
+
+    uint8_t* out = fixed_out;
+    if (!out) {
+        if (!c->out.ensure(ncand * (size_t)kSegCap)) return DMX_ERR_NOMEM;
+        out = c->out.as<uint8_t>();
+        cap = c->out.cap;
+    }
+    InflateArgs A;
+    A.in_words = words;
+    A.misalign = misalign;
+    A.n = n;
+    A.cands = c->cands.as<uint64_t>();
+    A.ncand = ncand;
+    A.out = out;
+    A.cap = cap;
+    A.recs = c->recs.as<SegRecord>();
+    A.status = c->status.as<unsigned long long>();
+    A.ticket = &ds->ticket;
+    A.flags = c->flags;
+    HIPCHK(hipMemsetAsync(A.status, 0, ncand * 8, st));
+    HIPCHK(hipMemsetAsync(&ds->ticket, 0, 4, st));
+    HIPCHK(launch_inflate_segments(A, st, c->timing ? c->ev[1] : nullptr, c->timing ? c->ev[2] : nullptr));
+    HIPCHK(launch_inflate_validate(A, &ds->res, st));
+    InflateResult r{};
+    HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    c->stats.segments = ncand;
+    c->stats.in_bytes = n;
+    if (r.status == 0) {
+        end_timing(c, st);
+        c->stats.path = 0;
+        c->stats.out_bytes = r.total;
+        *total_out = r.total;
+        if (dev_out) *dev_out = out;
+        return r.total > cap ? DMX_ERR_CAPACITY : DMX_OK;
+    }
+
+    // serial path: size pass, then write pass
+    c->stats.path = 1;
+    HIPCHK(launch_inflate_serial(A, 1, &ds->res, st));
+    HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (r.status != 0) return r.status;
+    *total_out = r.total;
+    if (!fixed_out) {
+        if (!c->out.ensure(r.total ? r.total : 1)) return DMX_ERR_NOMEM;
+        A.out = c->out.as<uint8_t>();
+        A.cap = c->out.cap;
+    } else if (r.total > cap) {
+        return DMX_ERR_CAPACITY;
+    }
+    HIPCHK(launch_inflate_serial(A, 0, &ds->res, st));
+    HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    end_timing(c, st);
+    c->stats.out_bytes = r.total;
+    if (dev_out) *dev_out = A.out;
+    return r.status;
+}
+
+bool is_gfx950(int dev) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) != hipSuccess) return false;
+    return std::strncmp(p.gcnArchName, "gfx950", 6) == 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+void dmx_config_default(dmx_config* cfg) {
+    cfg->device = -1;
+    cfg->segment_bytes = 32768;
+    cfg->flags = 0;
+}
+
+int dmx_create(dmx_ctx** out, const dmx_config* cfg) {
+    if (!out) return DMX_ERR_ARG;
+    *out = nullptr;
+    dmx_config d;
+    dmx_config_default(&d);
+    if (!cfg) cfg = &d;
+    if (cfg->segment_bytes != 16384 && cfg->segment_bytes != 32768) return DMX_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return DMX_ERR_DEVICE;
+    int dev = cfg->device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return DMX_ERR_DEVICE;
+    if (dev >= ndev || !is_gfx950(dev)) return DMX_ERR_DEVICE;
+    if (hipSetDevice(dev) != hipSuccess) return DMX_ERR_DEVICE;
+    dmx_ctx* c = new (std::nothrow) dmx_ctx();
+    if (!c) return DMX_ERR_NOMEM;
+    c->device = dev;
+    c->seg = cfg->segment_bytes;
+    c->flags = cfg->flags;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return DMX_ERR_DEVICE;
+    }
+    for (auto& e : c->ev) (void)hipEventCreate(&e);
+    *out = c;
+    return DMX_OK;
+}
+
+void dmx_destroy(dmx_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (DevBuf* b : {&c->in, &c->out, &c->slots, &c->sizes, &c->offs, &c->scal, &c->cands,
+                      &c->tiles, &c->tileoffs, &c->recs, &c->status})
+        b->release();
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+dmx_ctx* dmx_default_ctx(void) {
+    static std::once_flag once;
+    static dmx_ctx* ctx = nullptr;
+    std::call_once(once, [] {
+        if (dmx_create(&ctx, nullptr) != DMX_OK) ctx = nullptr;
+    });
+    return ctx;
+}
+
+size_t dmx_deflate_bound(size_t n) { return n + 10 * ((n + 16383) / 16384) + 16; }
+
+int dmx_deflate_device(dmx_ctx* c, const void* d_in, size_t n, int level, uint32_t flags,
+                       void* d_out, size_t cap, size_t* out_len, void* stream) {
+    if (!c || (!d_in && n) || !d_out || !out_len) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (hipSetDevice(c->device) != hipSuccess) return DMX_ERR_DEVICE;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return deflate_device_locked(c, (const uint8_t*)d_in, n, level, flags, (uint8_t*)d_out, cap,
+                                 out_len, st);
+}
+
+int dmx_inflate_device(dmx_ctx* c, const void* d_in, size_t n, void* d_out, size_t cap,
+                       size_t* out_len, void* stream) {
+    if (!c || (!d_in && n) || !d_out || !out_len) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (hipSetDevice(c->device) != hipSuccess) return DMX_ERR_DEVICE;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return inflate_device_locked(c, (const uint8_t*)d_in, n, (uint8_t*)d_out, cap, out_len,
+                                 nullptr, st);
+}
+
+int dmx_deflate(dmx_ctx* c, const uint8_t* in, size_t n, int level, uint8_t* out, size_t cap,
+                size_t* out_len) {
+    if (!c) c = dmx_default_ctx();
+    if (!c) return DMX_ERR_DEVICE;
+    if ((!in && n) || !out_len || (!out && cap)) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (hipSetDevice(c->device) != hipSuccess) return DMX_ERR_DEVICE;
+    const size_t bound = dmx_deflate_bound(n);
+    if (!c->in.ensure(n + 16) || !c->out.ensure(bound)) return DMX_ERR_NOMEM;
+    if (n) HIPCHK(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
+    size_t total = 0;
+    int rc = deflate_device_locked(c, c->in.as<uint8_t>(), n, level, 0, c->out.as<uint8_t>(),
+                                   c->out.cap, &total, c->stream);
+    *out_len = total;
+    if (rc != DMX_OK) return rc;
+    if (total > cap) return DMX_ERR_CAPACITY;
+    if (total) HIPCHK(hipMemcpyAsync(out, c->out.p, total, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return DMX_OK;
+}
+
+static int inflate_host(dmx_ctx* c, const uint8_t* in, size_t n, uint8_t** dev, size_t* total) {
+    if (!c->in.ensure(n + 16)) return DMX_ERR_NOMEM;
+    if (n) HIPCHK(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
+    return inflate_device_locked(c, c->in.as<uint8_t>(), n, nullptr, 0, total, dev, c->stream);
+}
+
+int dmx_inflate(dmx_ctx* c, const uint8_t* in, size_t n, uint8_t* out, size_t cap,
+                size_t* written, size_t* total) {
+    if (!c) c = dmx_default_ctx();
+    if (!c) return DMX_ERR_DEVICE;
+    if ((!in && n) || (!out && cap) || !written) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (hipSetDevice(c->device) != hipSuccess) return DMX_ERR_DEVICE;
+    uint8_t* dev = nullptr;
+    size_t tot = 0;
+    *written = 0;
+    if (total) *total = 0;
+    int rc = inflate_host(c, in, n, &dev, &tot);
+    if (rc != DMX_OK) return rc;
+    const size_t w = tot < cap ? tot : cap;
+    if (w) HIPCHK(hipMemcpyAsync(out, dev, w, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *written = w;
+    if (total) *total = tot;
+    return DMX_OK;
+}
+
+int dmx_inflate_alloc(dmx_ctx* c, const uint8_t* in, size_t n, uint8_t** out, size_t* len) {
+    if (!c) c = dmx_default_ctx();
+    if (!c) return DMX_ERR_DEVICE;
+    if ((!in && n) || !out || !len) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (hipSetDevice(c->device) != hipSuccess) return DMX_ERR_DEVICE;
+    *out = nullptr;
+    *len = 0;
+    uint8_t* dev = nullptr;
+    size_t tot = 0;
+    int rc = inflate_host(c, in, n, &dev, &tot);
+    if (rc != DMX_OK) return rc;
+    uint8_t* h = static_cast<uint8_t*>(std::malloc(tot ? tot : 1));
+    if (!h) return DMX_ERR_NOMEM;
+    if (tot && hipMemcpyAsync(h, dev, tot, hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
+        std::free(h);
+        return DMX_ERR_DEVICE;
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess) {
+        std::free(h);
+        return DMX_ERR_DEVICE;
+    }
+    *out = h;
+    *len = tot;
+    return DMX_OK;
+}
+
+void dmx_free(void* p) { std::free(p); }
+
+const char* dmx_strerror(int code) {
+    switch (code) {
+        case DMX_OK: return "ok";
+        case DMX_ERR_ARG: return "invalid argument";
+        case DMX_ERR_NOMEM: return "out of memory";
+        case DMX_ERR_DEVICE: return "HIP device error (no usable gfx950 device?)";
+        case DMX_ERR_DATA: return "invalid deflate stream";
+        case DMX_ERR_OVERREAD: return "Reading bits beyond the alloted buffer size!";
+        case DMX_ERR_CAPACITY: return "output buffer too small";
+        case DMX_ERR_INTERNAL: return "internal error";
+        default: return "unknown error";
+    }
+}
+
+int dmx_set_timing(dmx_ctx* c, int enable) {
+    if (!c) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->timing = enable != 0;
+    return DMX_OK;
+}
+
+int dmx_last_stats(dmx_ctx* c, dmx_stats* st) {
+    if (!c || !st) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    *st = c->stats;
+    return DMX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,76 @@
+// dmx_internal.h -- kernel launch interfaces shared by the host runtime and the .hip files.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dmx {
+
+struct DeflateArgs {
+    const uint8_t* in;
+    uint64_t n;
+    uint64_t nseg;
+    int level;
+    int final_last;       // set BFINAL on the last segment
+    uint8_t* slots;       // nseg * slot_bytes scratch
+    uint32_t slot_bytes;
+    uint32_t* sizes;      // nseg
+    uint64_t* offsets;    // nseg
+    uint64_t* total;      // 1
+    uint8_t* out;
+    uint64_t cap;
+};
+
+hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t st, hipEvent_t ev0,
+                          hipEvent_t ev1);
+
+// per-candidate record of the segment-parallel inflate
+struct SegRecord {
+    uint64_t end_byte;  // byte offset (relative to the stream) just past the segment's marker
+    uint32_t out_size;
+    uint32_t flags;     // SEGF_*
+};
+enum : uint32_t {
+    SEGF_FINAL = 1u,      // the segment ended with a BFINAL block
+    SEGF_ERR_DATA = 2u,   // undecodable code / table
+    SEGF_OVERREAD = 4u,   // ran past the end of the input
+    SEGF_OVERFLOW = 8u,   // output exceeded the LDS window
+    SEGF_XREF = 16u,      // back-reference reaches before the segment start
+    SEGF_TIMEOUT = 32u,   // look-back spin bound hit
+};
+
+struct InflateArgs {
+    const uint32_t* in_words;  // 4-byte aligned base at or below the stream start
+    uint64_t misalign;         // stream start = in_words bytes + misalign
+    uint64_t n;                // stream bytes
+    const uint64_t* cands;     // candidate segment starts (bytes, relative to stream)
+    uint64_t ncand;
+    uint8_t* out;
+    uint64_t cap;
+    SegRecord* recs;
+    unsigned long long* status;  // ncand look-back words (zeroed)
+    unsigned int* ticket;        // zeroed
+    uint32_t flags;              // DMX_CFG_RFC_STRICT
+};
+
+// result of validation / serial decode, copied to the host
+struct InflateResult {
+    uint64_t total;   // decoded bytes
+    int32_t status;   // 0 ok, DMX_ERR_* for the serial path; 1 = fast path needs fallback
+    uint32_t fin_index;
+};
+
+hipError_t launch_marker_count(const uint32_t* in_words, uint64_t misalign, uint64_t n,
+                               uint32_t* tile_counts, uint64_t ntiles, hipStream_t st);
+hipError_t launch_marker_write(const uint32_t* in_words, uint64_t misalign, uint64_t n,
+                               const uint64_t* tile_offs, uint64_t ntiles, uint64_t* cands,
+                               uint64_t* ncand_out, hipStream_t st);
+uint64_t marker_tiles(uint64_t n, uint64_t misalign);
+hipError_t launch_scan_u32(const uint32_t* v, uint64_t* offs, uint64_t n, uint64_t* total,
+                           hipStream_t st);
+hipError_t launch_inflate_segments(const InflateArgs& A, hipStream_t st, hipEvent_t ev0,
+                                   hipEvent_t ev1);
+hipError_t launch_inflate_validate(const InflateArgs& A, InflateResult* res, hipStream_t st);
+hipError_t launch_inflate_serial(const InflateArgs& A, int count_only, InflateResult* res,
+                                 hipStream_t st);
+
+}  // namespace dmx

@@ -1,0 +1,220 @@
+"""Python binding of libdmx's C-ABI (include/dmx.h) via ctypes.
+
+Mirrors the reference's public API names (deflate::compress / inflate::decompress /
+inflate::decompressZlib, /root/reference/include/deflate.hpp:755-815, inflate.hpp:326-408)
+so tests read like the reference's own; errors raise ``DmxError`` (a ``RuntimeError``, as the
+reference throws ``std::runtime_error``).  The HIP library is mandatory: there is no CPU
+fallback, an import without ``lib/libdmx.so`` fails loudly.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libdmx.so")
+
+DMX_OK = 0
+DMX_ERR_ARG = -1
+DMX_ERR_NOMEM = -2
+DMX_ERR_DEVICE = -3
+DMX_ERR_DATA = -4
+DMX_ERR_OVERREAD = -5
+DMX_ERR_CAPACITY = -6
+DMX_CFG_RFC_STRICT = 1
+DMX_DEFLATE_NOT_FINAL = 1
+
+CORPUS = {"zeros": 0, "repeat": 1, "random": 2, "text": 3, "mixed": 4, "bmp": 5}
+
+# every symbol include/dmx.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "dmx_config_default", "dmx_create", "dmx_destroy", "dmx_default_ctx", "dmx_deflate_bound",
+    "dmx_deflate", "dmx_inflate", "dmx_inflate_alloc", "dmx_free", "dmx_strerror",
+    "dmx_deflate_device", "dmx_inflate_device", "dmx_set_timing", "dmx_last_stats",
+    "dmx_corpus_generate",
+]
+
+
+class DmxError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        super().__init__(f"{what}: {strerror(code)} ({code})" if what else f"{strerror(code)} ({code})")
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("segment_bytes", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("ms_main_kernel", ctypes.c_double), ("ms_device_total", ctypes.c_double),
+                ("segments", ctypes.c_uint64), ("in_bytes", ctypes.c_uint64),
+                ("out_bytes", ctypes.c_uint64), ("path", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libdmx.so (raises OSError when the HIP library has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"{LIB_PATH} missing: build it with `make -C deflate.hpp_amd` "
+                      "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    sz = ctypes.c_size_t
+    vp = ctypes.c_void_p
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    L.dmx_config_default.argtypes = [ctypes.POINTER(Config)]
+    L.dmx_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(Config)]
+    L.dmx_destroy.argtypes = [vp]
+    L.dmx_default_ctx.restype = vp
+    L.dmx_deflate_bound.argtypes = [sz]
+    L.dmx_deflate_bound.restype = sz
+    L.dmx_deflate.argtypes = [vp, vp, sz, ctypes.c_int, vp, sz, ctypes.POINTER(sz)]
+    L.dmx_inflate.argtypes = [vp, vp, sz, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
+    L.dmx_inflate_alloc.argtypes = [vp, vp, sz, ctypes.POINTER(u8p), ctypes.POINTER(sz)]
+    L.dmx_free.argtypes = [vp]
+    L.dmx_strerror.argtypes = [ctypes.c_int]
+    L.dmx_strerror.restype = ctypes.c_char_p
+    L.dmx_deflate_device.argtypes = [vp, vp, sz, ctypes.c_int, ctypes.c_uint32, vp, sz, ctypes.POINTER(sz), vp]
+    L.dmx_inflate_device.argtypes = [vp, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
+    L.dmx_set_timing.argtypes = [vp, ctypes.c_int]
+    L.dmx_last_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    L.dmx_corpus_generate.argtypes = [ctypes.c_int, ctypes.c_uint64, sz, vp]
+    _lib = L
+    return L
+
+
+def strerror(code):
+    try:
+        return lib().dmx_strerror(code).decode()
+    except OSError:
+        return f"error {code}"
+
+
+def _check(rc, what):
+    if rc != DMX_OK:
+        raise DmxError(rc, what)
+
+
+def deflate_bound(n):
+    return lib().dmx_deflate_bound(n)
+
+
+def corpus(kind, n, offset=0):
+    """Synthetic corpus bytes [offset, offset+n)."""
+    buf = ctypes.create_string_buffer(max(1, n))
+    _check(lib().dmx_corpus_generate(CORPUS[kind], offset, n, buf), "corpus")
+    return buf.raw[:n]
+
+
+def corpus_into(kind, n, ptr, offset=0):
+    _check(lib().dmx_corpus_generate(CORPUS[kind], offset, n, ctypes.c_void_p(ptr)), "corpus")
+
+
+class Context:
+    """A libdmx context bound to one HIP device (dmx_create / dmx_destroy)."""
+
+    def __init__(self, device=-1, segment_bytes=32768, rfc_strict=False):
+        cfg = Config()
+        lib().dmx_config_default(ctypes.byref(cfg))
+        cfg.device = device
+        cfg.segment_bytes = segment_bytes
+        cfg.flags = DMX_CFG_RFC_STRICT if rfc_strict else 0
+        h = ctypes.c_void_p()
+        _check(lib().dmx_create(ctypes.byref(h), ctypes.byref(cfg)), "dmx_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().dmx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- host-buffer API: the reference's signatures -------------------------------------
+    def compress(self, data, level=2):
+        """deflate::compress(char*, size_t, int) -> raw DEFLATE bytes."""
+        data = bytes(data)
+        cap = deflate_bound(len(data))
+        out = ctypes.create_string_buffer(max(1, cap))
+        n = ctypes.c_size_t()
+        _check(lib().dmx_deflate(self.h, data, len(data), level, out, cap, ctypes.byref(n)), "deflate")
+        return out.raw[: n.value]
+
+    def decompress(self, data, cap=None):
+        """inflate::decompress(void*, size_t) -> bytes; with cap: the (void*,size_t,void*,size_t)
+        overload (returns at most cap bytes)."""
+        data = bytes(data)
+        if cap is None:
+            p = ctypes.POINTER(ctypes.c_uint8)()
+            n = ctypes.c_size_t()
+            _check(lib().dmx_inflate_alloc(self.h, data, len(data), ctypes.byref(p), ctypes.byref(n)), "inflate")
+            try:
+                return ctypes.string_at(p, n.value)
+            finally:
+                lib().dmx_free(p)
+        out = ctypes.create_string_buffer(max(1, cap))
+        w = ctypes.c_size_t()
+        tot = ctypes.c_size_t()
+        _check(lib().dmx_inflate(self.h, data, len(data), out, cap, ctypes.byref(w), ctypes.byref(tot)), "inflate")
+        return out.raw[: w.value]
+
+    def decompress_zlib(self, data):
+        """inflate::decompressZlib(void*, size_t): skips the 2-byte zlib header (the reference's
+        FDICT test never fires, inflate.hpp:355, SURVEY A-9) and ignores the Adler-32."""
+        data = bytes(data)
+        if len(data) < 2:
+            raise DmxError(DMX_ERR_OVERREAD, "inflate_zlib")
+        return self.decompress(data[2:])
+
+    # ---- device-resident API --------------------------------------------------------------
+    def deflate_device(self, d_in, n, level, d_out, cap, stream=None, not_final=False):
+        out_len = ctypes.c_size_t()
+        rc = lib().dmx_deflate_device(self.h, ctypes.c_void_p(d_in), n, level,
+                                      DMX_DEFLATE_NOT_FINAL if not_final else 0,
+                                      ctypes.c_void_p(d_out), cap, ctypes.byref(out_len),
+                                      ctypes.c_void_p(stream) if stream else None)
+        _check(rc, "deflate_device")
+        return out_len.value
+
+    def inflate_device(self, d_in, n, d_out, cap, stream=None):
+        out_len = ctypes.c_size_t()
+        rc = lib().dmx_inflate_device(self.h, ctypes.c_void_p(d_in), n, ctypes.c_void_p(d_out), cap,
+                                      ctypes.byref(out_len), ctypes.c_void_p(stream) if stream else None)
+        _check(rc, "inflate_device")
+        return out_len.value
+
+    def set_timing(self, on=True):
+        _check(lib().dmx_set_timing(self.h, 1 if on else 0), "set_timing")
+
+    def stats(self):
+        s = Stats()
+        _check(lib().dmx_last_stats(self.h, ctypes.byref(s)), "stats")
+        return s
+
+
+_default = None
+
+
+def default_context():
+    global _default
+    if _default is None:
+        _default = Context()
+    return _default
+
+
+def compress(data, level=2):
+    return default_context().compress(data, level)
+
+
+def decompress(data, cap=None):
+    return default_context().decompress(data, cap)
+
+
+def decompress_zlib(data):
+    return default_context().decompress_zlib(data)

@@ -1,0 +1,129 @@
+/* dmx.h -- C-ABI of the MI355X-native DEFLATE/INFLATE engine (libdmx.so).
+ *
+ * This is the drop-in boundary for HyperBitGore/deflate.hpp's hot path.  The reference has no
+ * C ABI of its own (header-only static methods); each entry point below states the reference
+ * interface it replaces (file:line under the reference's include/).  include/deflate.hpp and
+ * include/inflate.hpp re-expose the reference's class API on top of these functions, and
+ * INTEGRATION.md shows the ctypes / C++ bindings a caller adds.
+ *
+ * Plain pointers and sizes only; no torch or HIP types in any signature (streams are passed as
+ * an opaque void* that is a hipStream_t).  All functions are thread-safe per context; the
+ * default context (dmx_default_ctx) is created lazily under a once-flag.
+ */
+#ifndef DMX_H
+#define DMX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------------------- */
+#define DMX_OK 0
+#define DMX_ERR_ARG (-1)      /* bad argument (null pointer, unsupported option)              */
+#define DMX_ERR_NOMEM (-2)    /* host or device allocation failed                               */
+#define DMX_ERR_DEVICE (-3)   /* HIP runtime error or no usable gfx950 device                   */
+#define DMX_ERR_DATA (-4)     /* stream cannot be decoded (no Huffman code matches, bad table) */
+#define DMX_ERR_OVERREAD (-5) /* stream ends before its final block: the reference throws
+                                 "Reading bits beyond the alloted buffer size!"
+                                 (inflate.hpp:81-82, 97-99, 106-108)                          */
+#define DMX_ERR_CAPACITY (-6) /* caller's output buffer too small (device API only)           */
+#define DMX_ERR_INTERNAL (-7)
+
+/* ---- context --------------------------------------------------------------------------- */
+typedef struct dmx_ctx dmx_ctx;
+
+typedef struct dmx_config {
+    int device;             /* HIP device ordinal, -1 = the calling thread's current device  */
+    uint32_t segment_bytes; /* independent deflate segment: 16384, 32768 (default) or 65536.
+                               32768 mirrors the reference's per-chunk LZ77 reset
+                               (deflate.hpp:689-697).                                          */
+    uint32_t flags;         /* DMX_CFG_*                                                        */
+} dmx_config;
+
+/* Inflate code-length RLE per RFC 1951 (repeat may span HLIT/HDIST, code 16 repeats the
+ * previous length) instead of the reference's behaviour (SURVEY A-11/A-12, inflate.hpp:166-224).
+ * Default off: output is bit-exact to the reference. */
+#define DMX_CFG_RFC_STRICT 1u
+
+void dmx_config_default(dmx_config* cfg);
+int dmx_create(dmx_ctx** ctx, const dmx_config* cfg);
+void dmx_destroy(dmx_ctx* ctx);
+/* process-wide context on the current device with the default config (never destroyed) */
+dmx_ctx* dmx_default_ctx(void);
+
+/* ---- host-buffer API (what include/deflate.hpp / inflate.hpp call) ---------------------- */
+
+/* Upper bound of dmx_deflate's output for n input bytes, any segment size / level. */
+size_t dmx_deflate_bound(size_t n);
+
+/* Replaces deflate::compress(char*, size_t, int)             deflate.hpp:779-796
+ *          deflate::compress(std::vector<uint8_t>&, int)      deflate.hpp:798-815
+ * Raw DEFLATE (RFC 1951, no zlib/gzip wrapper).  level 0 = stored, 1 = Huffman only,
+ * 2 = fast (greedy hash), 3 = slow (lazy, deeper search); any other value behaves like 1,
+ * as the reference's switch without default does (deflate.hpp:699-717).  Output is a valid
+ * stream the reference inflate::decompress round-trips exactly (the reference's own levels
+ * 2/3 are not; SURVEY A-1..A-3).  *out_len receives the stream length. */
+int dmx_deflate(dmx_ctx* ctx, const uint8_t* in, size_t n, int level, uint8_t* out, size_t cap,
+                size_t* out_len);
+
+/* Replaces inflate::decompress(void*, size_t, void*, size_t)   inflate.hpp:338-350
+ * Decodes the whole stream, copies min(total, cap) bytes to out.  *written = bytes copied
+ * (the reference's return value), *total = full decoded size (may be NULL). */
+int dmx_inflate(dmx_ctx* ctx, const uint8_t* in, size_t n, uint8_t* out, size_t cap,
+                size_t* written, size_t* total);
+
+/* Replaces inflate::decompress(void*, size_t)                  inflate.hpp:363-374
+ *          inflate::decompress(std::vector<uint8_t>)           inflate.hpp:376-387
+ * *out is allocated by the library; release it with dmx_free. */
+int dmx_inflate_alloc(dmx_ctx* ctx, const uint8_t* in, size_t n, uint8_t** out, size_t* len);
+
+void dmx_free(void* p);
+const char* dmx_strerror(int code);
+
+/* ---- device-resident API (HBM in, HBM out; used by bench.py and multi-GPU sharding) ------ */
+
+/* Do not set BFINAL on the last block: the output is one shard of a larger stream and ends
+ * byte-aligned on an empty stored block, so shards concatenate with plain byte copies. */
+#define DMX_DEFLATE_NOT_FINAL 1u
+
+/* d_in/d_out are device pointers on the context's device; stream is a hipStream_t or NULL for
+ * the context's own stream.  Returns DMX_ERR_CAPACITY if cap < the produced size. */
+int dmx_deflate_device(dmx_ctx* ctx, const void* d_in, size_t n, int level, uint32_t flags,
+                       void* d_out, size_t cap, size_t* out_len, void* stream);
+
+/* Device-resident inflate.  Returns DMX_ERR_CAPACITY (and the needed size in *out_len) when
+ * the decoded stream does not fit in cap. */
+int dmx_inflate_device(dmx_ctx* ctx, const void* d_in, size_t n, void* d_out, size_t cap,
+                       size_t* out_len, void* stream);
+
+/* ---- instrumentation -------------------------------------------------------------------- */
+typedef struct dmx_stats {
+    double ms_main_kernel;  /* HIP-event time of the dominant kernel of the last call       */
+    double ms_device_total; /* HIP-event time of all device work of the last call          */
+    uint64_t segments;      /* segments (deflate) / candidate segments (inflate)            */
+    uint64_t in_bytes;
+    uint64_t out_bytes;
+    uint32_t path;          /* inflate: 0 = segment-parallel fast path, 1 = serial path      */
+    uint32_t reserved;
+} dmx_stats;
+
+/* Enable (1) / disable (0) per-call HIP-event timing on a context (off by default). */
+int dmx_set_timing(dmx_ctx* ctx, int enable);
+int dmx_last_stats(dmx_ctx* ctx, dmx_stats* st);
+
+/* ---- synthetic corpora, bytes [offset, offset + n) --------------- */
+#define DMX_CORPUS_ZEROS 0
+#define DMX_CORPUS_REPEAT 1
+#define DMX_CORPUS_RANDOM 2
+#define DMX_CORPUS_TEXT 3
+#define DMX_CORPUS_MIXED 4
+#define DMX_CORPUS_BMP 5
+int dmx_corpus_generate(int kind, uint64_t offset, size_t n, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DMX_H */
