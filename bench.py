@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "deflate.hpp_amd"))
 
 import dmx  # noqa: E402
+import shard  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 GiB = 1 << 30
@@ -124,19 +125,8 @@ def main():
                                   not_final=not last)
         ks_d = ctx.stats()
         ev[1].record(stream)
-        if world > 1:  # RCCL gather of the compressed shards to rank 0
-            sz = torch.tensor([clen], dtype=torch.int64, device=dev)
-            sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-            dist.all_gather(sizes, sz)
-            sizes = [int(s.item()) for s in sizes]
-            if rank == 0:
-                offs = [sum(sizes[:r]) for r in range(world)]
-                gathered[: sizes[0]].copy_(d_comp[: sizes[0]])
-                ops = [dist.P2POp(dist.irecv, gathered[offs[r]: offs[r] + sizes[r]], r) for r in range(1, world)]
-            else:
-                ops = [dist.P2POp(dist.isend, d_comp[:clen], 0)]
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
+        if world > 1:  # RCCL gather of the compressed shards to rank 0 (xGMI P2P)
+            shard.gather_stream(d_comp, clen, gathered)
         ev[2].record(stream)
         ilen = clen
         if not last:  # make the shard a complete stream for the local round trip

@@ -5,14 +5,16 @@
 // (realCompress, /root/reference/include/deflate.hpp:680-752):
 //
 //   load (16 B/lane coalesced)  -> LDS byte image of the segment
-//   match candidates            -> LDS hash table (u32 head, atomicMax), rounds of 1024
-//                                  positions; cand[p] = distance to the latest earlier
-//                                  occurrence of the 4-byte prefix   (replaces LZ77::getMatches
+//   match candidates            -> two LDS hash tables, rounds of 1024 positions (one per
+//                                  thread): cand[p] = distance to the first occurrence of p's
+//                                  4-byte prefix earlier in the same round, else to the latest
+//                                  one in earlier rounds   (replaces LZ77::getMatches
 //                                  deflate.hpp:310-383 / getMatchesSlow :268-304)
-//   tokenize walk               -> 256-byte chunk per lane, greedy (level 2) or one-step lazy
-//                                  (level 3) parse; matches never cross a chunk edge, so chunks
-//                                  parse independently; LDS histogram   (constructDynamicHuffmanTree
-//                                  :402-418)
+//   parse walk                  -> 256-byte chunk per lane, greedy (level 2) or one-step lazy
+//                                  (level 3); matches never cross a chunk edge, so chunks parse
+//                                  independently; token starts -> LDS bitmap
+//   histogram                   -> one bitmap word (32 positions) per thread, LDS atomics
+//                                  (constructDynamicHuffmanTree :402-418)
 //   code lengths                -> block-parallel length-limited Huffman
 //                                  (FlatHuffmanTree::generateCodeLengths common.hpp:322-404)
 //   canonical codes             -> (FlatHuffmanTree::construct common.hpp:104-145)
@@ -31,32 +33,9 @@
 
 namespace dmx {
 
-constexpr int DF_NT = 256;     // threads per workgroup
-constexpr int DF_CHUNK = 256;  // bytes per tokenizer lane
-
-template <int SEG>
-struct DfSmem {
-    static constexpr int HB = (SEG >= 32768) ? 13 : 12;
-    static constexpr int NWALK = SEG / DF_CHUNK;
-    static constexpr int UW0 = 1 << HB;
-    static constexpr int UW1 = SEG / 4 + 64;
-    static constexpr int UW = UW0 > UW1 ? UW0 : UW1;
-    uint32_t data32[SEG / 4 + 16];
-    uint16_t cand[SEG + 8];
-    uint32_t U[UW];  // hash head during matching, output bit image afterwards
-    uint32_t litfreq[288];
-    uint32_t distfreq[32];
-    uint32_t prefreq[32];
-    uint32_t litcode[288];  // (len << 16) | bit-reversed code
-    uint32_t distcode[32];
-    uint32_t precode[32];
-    uint8_t litlen[288];
-    uint8_t distlen[32];
-    uint8_t prelen[32];
-    uint16_t order[320];
-    uint32_t scan[2 * DF_NT];
-    uint32_t sh[48];
-};
+constexpr int DF_NT = 1024;    // threads per workgroup (16 waves)
+constexpr int DF_CHUNK = 256;  // bytes per parse lane
+constexpr int DF_HB = 12;      // hash bits of each of the two match tables
 
 // ---------------------------------------------------------------------------------------
 // block primitives
@@ -65,13 +44,13 @@ struct DfSmem {
 // exclusive block scan of one value per thread; returns the prefix, *total gets the sum
 __device__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
     const int t = threadIdx.x, w = t >> 6;
-    uint32_t inc = wave_incl_scan(v);
+    const uint32_t inc = wave_incl_scan(v);
     if ((t & 63) == 63) scratch[w] = inc;
     __syncthreads();
     uint32_t base = 0, tot = 0;
 #pragma unroll
     for (int i = 0; i < DF_NT / 64; i++) {
-        uint32_t s = scratch[i];
+        const uint32_t s = scratch[i];
         if (i < w) base += s;
         tot += s;
     }
@@ -80,154 +59,155 @@ __device__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* tot
     return base + inc - v;
 }
 
-// Length-limited code lengths for freq[0..nsym), written to lens[].  Block-parallel:
-//  1. L = round(log2(F/f)) clamped to [1, maxbits]  (rank symbols by (f desc, sym asc))
-//  2. Kraft repair: while sum 2^-L > 1 lengthen the least frequent codes, longest class first
-//  3. slack fill: per class of equal length (shortest first) shorten the most frequent codes
+// Length-limited code lengths for freq[0..nsym) (nsym <= 512), written to lens[].  One
+// wavefront, registers only:
+//  1. keys (f << 9 | 511 - sym) sorted descending (register bitonic network) -> rank order
+//  2. L = round(log2(F/f)) clamped to [1, maxbits]
+//  3. Kraft repair: while sum 2^-L > 1 lengthen the least frequent codes, longest class first
+//  4. slack fill: per class of equal length (shortest first) shorten the most frequent codes
 //     while the Kraft budget allows; repeat until the code is complete.
 // Zero or one used symbol -> two codes of length 1 (complete code, as zlib emits).
-// Stands in for FlatHuffmanTree::generateCodeLengths (common.hpp:322-404), which is a serial
+// Stands in for FlatHuffmanTree::generateCodeLengths (common.hpp:322-404), a serial
 // priority-queue Huffman; this one stays within ~1% of optimal.
-__device__ void build_lengths(const uint32_t* freq, int nsym, int maxbits, uint8_t* lens,
-                              uint16_t* order, uint32_t* sh) {
-    const int t = threadIdx.x;
-    if (t == 0) { sh[0] = 0; sh[1] = 0; sh[2] = 0; }
-    __syncthreads();
-    for (int s = t; s < nsym; s += DF_NT) {
-        uint32_t f = freq[s];
-        if (f) { atomicAdd(&sh[0], f); atomicAdd(&sh[1], 1u); }
+__device__ void wave_build_lengths(const uint32_t* freq, int nsym, int maxbits, uint8_t* lens) {
+    const int lane = lane_id();
+    uint32_t key[8];
+    uint32_t fs = 0, nzs = 0, used = 0;
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const int s = lane * 8 + r;
+        const uint32_t f = s < nsym ? freq[s] : 0;
+        key[r] = f ? (f << 9) | (511 - s) : 0;
+        fs += f;
+        nzs += f ? 1 : 0;
+        if (f) used = s + 1;
+        if (s < nsym) lens[s] = 0;
     }
-    __syncthreads();
-    const uint32_t F = sh[0], nz = sh[1];
+    const uint32_t F = wave_sum(fs), nz = wave_sum(nzs);
     const uint32_t U = 1u << maxbits;
     if (nz <= 1) {
-        for (int s = t; s < nsym; s += DF_NT) lens[s] = 0;
-        __syncthreads();
-        if (t == 0) {
-            int used = -1;
-            for (int s = 0; s < nsym; s++)
-                if (freq[s]) { used = s; break; }
-            if (used < 0) { lens[0] = 1; lens[1] = 1; }
-            else { lens[used] = 1; lens[used == 0 ? 1 : 0] = 1; }
+        uint32_t u = used;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) u = max(u, __shfl_xor(u, d, 64));
+        if (lane == 0) {
+            if (u == 0) { lens[0] = 1; lens[1] = 1; }
+            else { lens[u - 1] = 1; lens[u - 1 == 0 ? 1 : 0] = 1; }
         }
-        __syncthreads();
         return;
     }
-    for (int s = t; s < nsym; s += DF_NT) {
-        uint32_t f = freq[s];
+    wave_sort512_desc(key);
+    uint32_t len[8];
+    bool val[8];
+    uint32_t ks = 0;
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const uint32_t f = key[r] >> 9;
+        val[r] = f != 0;
         uint32_t L = 0;
         if (f) {
-            uint32_t L0 = 31 - __clz(F / f);
-            uint64_t a = (uint64_t)f << (L0 + 1);
+            const uint32_t L0 = 31 - __clz(F / f);
+            const uint64_t a = (uint64_t)f << (L0 + 1);
             L = L0 + ((a * a <= 2ull * F * F) ? 1u : 0u);
             L = max(1u, min((uint32_t)maxbits, L));
-            atomicAdd(&sh[2], U >> L);
-            uint32_t rank = 0;
-            for (int s2 = 0; s2 < nsym; s2++) {
-                uint32_t f2 = freq[s2];
-                rank += (f2 > f) || (f2 == f && s2 < s);
-            }
-            order[rank] = (uint16_t)s;
+            ks += U >> L;
         }
-        lens[s] = (uint8_t)L;
+        len[r] = L;
     }
-    __syncthreads();
-    if (t < 64) {
-        const int lane = t;
-        const uint32_t S = (nz + 63) / 64;  // <= 5
-        uint32_t sym[5], len[5];
-        bool val[5];
+    uint32_t K = wave_sum(ks);
+    const uint64_t ltmask = (1ull << lane) - 1ull;
+    // class L members: ballots per register slot give the class size and each member's
+    // position in rank order (rank = lane * 8 + r)
+    auto class_scan = [&](uint32_t L, uint32_t (&pos)[8], uint32_t& total) {
+        uint64_t B[8];
+        total = 0;
+        uint32_t below = 0;
 #pragma unroll
-        for (int i = 0; i < 5; i++) {
-            uint32_t r = lane * S + i;
-            val[i] = (uint32_t)i < S && r < nz;
-            sym[i] = val[i] ? order[r] : 0;
-            len[i] = val[i] ? lens[sym[i]] : 0;
+        for (int r = 0; r < 8; r++) {
+            B[r] = __ballot(val[r] && len[r] == L);
+            total += __popcll(B[r]);
+            below += __popcll(B[r] & ltmask);
         }
-        uint32_t K = sh[2];
-        // Kraft repair (over-full after rounding / clamping)
-        while (K > U) {
-            for (int L = maxbits - 1; L >= 1 && K > U; L--) {
-                const uint32_t gain = U >> (L + 1);
-                const uint32_t need = (K - U + gain - 1) / gain;
-                uint32_t cnt = 0;
+        uint32_t run = below;
 #pragma unroll
-                for (int i = 0; i < 5; i++) cnt += (val[i] && len[i] == (uint32_t)L);
-                uint32_t inc = wave_incl_scan(cnt);
-                uint32_t total = __shfl(inc, 63, 64);
-                uint32_t after = total - inc;  // class members with a higher rank
-                uint32_t k = min(need, total);
-                uint32_t local = 0;
-#pragma unroll
-                for (int i = 4; i >= 0; i--) {
-                    if (val[i] && len[i] == (uint32_t)L) {
-                        if (after + local < k) len[i] = L + 1;
-                        local++;
-                    }
-                }
-                K -= k * gain;
-            }
+        for (int r = 0; r < 8; r++) {
+            pos[r] = run;
+            run += (uint32_t)((B[r] >> lane) & 1ull);
         }
-        // slack fill
-        uint32_t R = U - K;
-        for (int pass = 0; pass < 64 && R; pass++) {
-            bool changed = false;
-            for (int L = 2; L <= maxbits; L++) {
-                const uint32_t c = U >> L;
-                uint32_t cnt = 0;
+    };
+    // Kraft repair (over-full after rounding / clamping): lengthen lowest-frequency codes
+    while (K > U) {
+        for (int L = maxbits - 1; L >= 1 && K > U; L--) {
+            const uint32_t gain = U >> (L + 1);
+            const uint32_t need = (K - U + gain - 1) / gain;
+            uint32_t pos[8], total;
+            class_scan(L, pos, total);
+            const uint32_t k = min(need, total);
+            if (!k) continue;
 #pragma unroll
-                for (int i = 0; i < 5; i++) cnt += (val[i] && len[i] == (uint32_t)L);
-                uint32_t inc = wave_incl_scan(cnt);
-                uint32_t total = __shfl(inc, 63, 64);
-                uint32_t before = inc - cnt;
-                uint32_t k = min(total, R / c);
-                if (k) { changed = true; R -= k * c; }
-                uint32_t local = 0;
-#pragma unroll
-                for (int i = 0; i < 5; i++) {
-                    if (val[i] && len[i] == (uint32_t)L) {
-                        if (before + local < k) len[i] = L - 1;
-                        local++;
-                    }
-                }
-            }
-            if (!changed) break;
+            for (int r = 0; r < 8; r++)
+                if (val[r] && len[r] == (uint32_t)L && pos[r] >= total - k) len[r] = L + 1;
+            K -= k * gain;
         }
-#pragma unroll
-        for (int i = 0; i < 5; i++)
-            if (val[i]) lens[sym[i]] = (uint8_t)len[i];
     }
-    __syncthreads();
+    // slack fill: shorten the most frequent codes of each class while the budget allows
+    uint32_t R = U - K;
+    for (int pass = 0; pass < 64 && R; pass++) {
+        bool changed = false;
+        for (int L = 2; L <= maxbits && R; L++) {
+            const uint32_t c = U >> L;
+            if (c > R) continue;
+            uint32_t pos[8], total;
+            class_scan(L, pos, total);
+            const uint32_t k = min(total, R / c);
+            if (!k) continue;
+            changed = true;
+            R -= k * c;
+#pragma unroll
+            for (int r = 0; r < 8; r++)
+                if (val[r] && len[r] == (uint32_t)L && pos[r] < k) len[r] = L - 1;
+        }
+        if (!changed) break;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+        if (val[r]) lens[511 - (key[r] & 511)] = (uint8_t)len[r];
 }
 
 // Canonical codes (RFC 1951 3.2.2; reference FlatHuffmanTree::construct common.hpp:104-145),
 // stored bit-reversed for the LSB-first bit packer: codes[s] = (len << 16) | rev(code).
-__device__ void assign_codes(const uint8_t* lens, int nsym, uint32_t* codes, uint32_t* sh) {
-    const int t = threadIdx.x;
-    if (t < 32) sh[t] = 0;
-    __syncthreads();
-    for (int s = t; s < nsym; s += DF_NT)
-        if (lens[s]) atomicAdd(&sh[lens[s]], 1u);
-    __syncthreads();
-    if (t == 0) {
-        uint32_t code = 0;
-        for (int b = 1; b <= 15; b++) {
-            code = (code + (b > 1 ? sh[b - 1] : 0)) << 1;
-            sh[16 + b] = code;
-        }
+// One wavefront; per-length counts and ranks come from ballots over 64-symbol chunks.
+__device__ void wave_assign_codes(const uint8_t* lens, int nsym, uint32_t* codes) {
+    const int lane = lane_id();
+    const uint64_t ltmask = (1ull << lane) - 1ull;
+    uint32_t cnt[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) cnt[k] = 0;
+    for (int c = 0; c < nsym; c += 64) {
+        const int s = c + lane;
+        const uint32_t L = s < nsym ? lens[s] : 0;
+#pragma unroll
+        for (int k = 1; k < 16; k++) cnt[k] += __popcll(__ballot(L == (uint32_t)k));
     }
-    __syncthreads();
-    for (int s = t; s < nsym; s += DF_NT) {
-        uint32_t L = lens[s];
-        uint32_t v = 0;
-        if (L) {
-            uint32_t rank = 0;
-            for (int s2 = 0; s2 < s; s2++) rank += (lens[s2] == L);
-            v = (L << 16) | bitrev(sh[16 + L] + rank, L);
-        }
-        codes[s] = v;
+    uint32_t next[16];
+    uint32_t code = 0;
+    next[0] = 0;
+#pragma unroll
+    for (int k = 1; k < 16; k++) {
+        code = (code + (k > 1 ? cnt[k - 1] : 0)) << 1;
+        next[k] = code;
     }
-    __syncthreads();
+    for (int c = 0; c < nsym; c += 64) {
+        const int s = c + lane;
+        const uint32_t L = s < nsym ? lens[s] : 0;
+        uint32_t my = 0;
+#pragma unroll
+        for (int k = 1; k < 16; k++) {
+            const uint64_t b = __ballot(L == (uint32_t)k);
+            if (L == (uint32_t)k) my = next[k] + __popcll(b & ltmask);
+            next[k] += __popcll(b);
+        }
+        if (s < nsym) codes[s] = L ? (L << 16) | bitrev(my, L) : 0;
+    }
 }
 
 // LSB-first bit writer that ORs 32-bit words into an LDS image (image pre-zeroed).
@@ -309,8 +289,32 @@ __device__ __forceinline__ RunPlan plan_run(uint32_t v, uint32_t r) {
 }
 
 // ---------------------------------------------------------------------------------------
-// the segment kernel
+// the segment kernel: 1024 threads (16 waves) per segment, one workgroup per CU
 // ---------------------------------------------------------------------------------------
+template <int SEG>
+struct DfSmem {
+    static constexpr int NWALK = SEG / DF_CHUNK;
+    static constexpr int HT = 1 << DF_HB;  // entries per hash table
+    static constexpr int UW0 = 2 * HT;
+    static constexpr int UW1 = SEG / 4 + 64;
+    static constexpr int UW = UW0 > UW1 ? UW0 : UW1;
+    uint32_t data32[SEG / 4 + 16];
+    uint16_t cand[SEG + 8];
+    uint32_t U[UW];  // head[HT] | first[HT] while matching, the output bit image afterwards
+    uint32_t tokmap[SEG / 32];  // token-start bitmap
+    uint32_t litfreq[288];
+    uint32_t distfreq[32];
+    uint32_t prefreq[32];
+    uint32_t litcode[288];  // (len << 16) | bit-reversed code
+    uint32_t distcode[32];
+    uint32_t precode[32];
+    uint8_t litlen[288];
+    uint8_t distlen[32];
+    uint8_t prelen[32];
+    uint32_t scan[2 * DF_NT / 64];
+    uint64_t runmask[6];
+    uint32_t sh[48];
+};
 
 // stored block: [BFINAL|00][LEN][NLEN][data] (+ empty stored block unless final)
 template <int SEG>
@@ -350,92 +354,121 @@ __device__ void emit_stored(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t*
     if (t == 0) *size_out = total;
 }
 
+// bits of the tokens starting in bitmap word wi (token p: literal if cand[p] == 0, else a
+// match with distance cand[p] and length cand[p + 1])
+template <int SEG>
+__device__ __forceinline__ uint32_t word_bits(const DfSmem<SEG>& S, uint32_t wi) {
+    uint32_t w = S.tokmap[wi], bits = 0;
+    while (w) {
+        const uint32_t p = wi * 32 + __builtin_ctz(w);
+        w &= w - 1;
+        const uint32_t d = S.cand[p];
+        if (d) {
+            const uint32_t L = S.cand[p + 1];
+            const uint32_t ls = len_sym(L), ds = dist_sym(d);
+            bits += (S.litcode[ls] >> 16) + len_extra(ls) + (S.distcode[ds] >> 16) + dist_extra(ds);
+        } else {
+            bits += S.litcode[data_byte(S.data32, p)] >> 16;
+        }
+    }
+    return bits;
+}
+
 // Huffman (dynamic or fixed) block for the tokenized segment; returns false when a stored
 // block would be smaller (the caller then emits it), true after writing the slot.
 template <int SEG>
 __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t* slot,
-                             uint32_t* size_out) {
-    constexpr int NWALK = DfSmem<SEG>::NWALK;
+                             uint32_t* size_out, uint64_t* dbg, uint64_t seg) {
+    constexpr int NMAP = SEG / 32;
     const int t = threadIdx.x;
 
-    // ---- code lengths + canonical codes -------------------------------------------------
-    build_lengths(S.litfreq, 286, 15, S.litlen, S.order, S.sh);
-    build_lengths(S.distfreq, 30, 15, S.distlen, S.order, S.sh);
-    assign_codes(S.litlen, 286, S.litcode, S.sh);
-    assign_codes(S.distlen, 30, S.distcode, S.sh);
-
-    // ---- token cost under the dynamic and the fixed code; HLIT / HDIST ------------------
+    // ---- code lengths + canonical codes (wave 0: lit/len, wave 1: distance) -------------
+    if (t < 64) {
+        wave_build_lengths(S.litfreq, 286, 15, S.litlen);
+        DMX_PHASE(dbg, seg, 12);
+        wave_assign_codes(S.litlen, 286, S.litcode);
+        DMX_PHASE(dbg, seg, 13);
+    } else if (t < 128) {
+        wave_build_lengths(S.distfreq, 30, 15, S.distlen);
+        wave_assign_codes(S.distlen, 30, S.distcode);
+    }
     if (t < 8) S.sh[32 + t] = 0;
     __syncthreads();
-    {
-        uint32_t dyn = 0, fix = 0, ml = 0, md = 0;
-        for (int s = t; s < 286; s += DF_NT) {
-            if (S.litlen[s]) ml = max(ml, (uint32_t)s + 1);
-            const uint32_t f = S.litfreq[s];
-            if (!f) continue;
-            const uint32_t ex = s > 256 ? kLenExtra[s - 257] : 0;
-            dyn += f * (S.litlen[s] + ex);
-            fix += f * (fixed_lit_len(s) + ex);
-        }
+    DMX_PHASE(dbg, seg, 4);
+
+    // ---- token cost under the dynamic and the fixed code; HLIT / HDIST ------------------
+    if (t < 286) {
+        const uint32_t s = t;
+        const uint32_t f = S.litfreq[s];
+        const uint32_t ex = s > 256 ? len_extra(s) : 0;
+        uint32_t dyn = f * (S.litlen[s] + ex), fix = f * (fixed_lit_len(s) + ex);
         if (t < 30) {
-            const uint32_t f = S.distfreq[t];
-            dyn += f * (S.distlen[t] + kDistExtra[t]);
-            fix += f * (5 + kDistExtra[t]);
-            if (S.distlen[t]) md = t + 1;
+            const uint32_t g = S.distfreq[t];
+            dyn += g * (S.distlen[t] + dist_extra(t));
+            fix += g * (5 + dist_extra(t));
+            if (S.distlen[t]) atomicMax(&S.sh[35], (uint32_t)t + 1);
         }
-        atomicAdd(&S.sh[32], dyn);
-        atomicAdd(&S.sh[33], fix);
-        atomicMax(&S.sh[34], ml);
-        atomicMax(&S.sh[35], md);
+        if (dyn) atomicAdd(&S.sh[32], dyn);
+        if (fix) atomicAdd(&S.sh[33], fix);
+        if (S.litlen[s]) atomicMax(&S.sh[34], s + 1);
     }
     __syncthreads();
+    DMX_PHASE(dbg, seg, 5);
     const uint32_t dyn_tok = S.sh[32], fix_tok = S.sh[33];
     const uint32_t nlit = max(257u, S.sh[34]), ndist = max(1u, S.sh[35]);
     const uint32_t nall = nlit + ndist;
 
     // ---- dynamic header: RLE runs over (litlen[0..nlit), distlen[0..ndist)) -------------
-    RunPlan plan[2];
-    uint32_t runv[2] = {0, 0};
-    bool isrun[2] = {false, false};
-    for (int k = 0; k < 2; k++) {
-        const uint32_t i = t + k * DF_NT;
-        if (i >= nall) continue;
-        const uint32_t send = i < nlit ? nlit : nall;
-        const uint32_t v = i < nlit ? S.litlen[i] : S.distlen[i - nlit];
-        bool start = (i == 0 || i == nlit);
-        if (!start) {
-            const uint32_t pv = (i - 1) < nlit ? S.litlen[i - 1] : S.distlen[i - 1 - nlit];
-            start = pv != v;
+    // run starts as a bitmap (one ballot per wave), each run start finds the next start
+    RunPlan plan = {0, 0, 0, 0, 0, 0, 0};
+    uint32_t runv = 0;
+    bool isrun = false;
+    {
+        const uint32_t i = t;
+        bool start = false;
+        uint32_t v = 0;
+        if (i < nall) {
+            v = i < nlit ? S.litlen[i] : S.distlen[i - nlit];
+            start = (i == 0 || i == nlit);
+            if (!start) {
+                const uint32_t pv = (i - 1) < nlit ? S.litlen[i - 1] : S.distlen[i - 1 - nlit];
+                start = pv != v;
+            }
         }
-        if (!start) continue;
-        uint32_t j = i + 1;
-        while (j < send && (j < nlit ? S.litlen[j] : S.distlen[j - nlit]) == v) j++;
-        isrun[k] = true;
-        runv[k] = v;
-        plan[k] = plan_run(v, j - i);
-        const RunPlan& p = plan[k];
-        if (p.n18) atomicAdd(&S.prefreq[18], p.n18);
-        if (p.n17) atomicAdd(&S.prefreq[17], p.n17);
-        if (p.n16) atomicAdd(&S.prefreq[16], p.n16);
-        if (p.nlit) atomicAdd(&S.prefreq[v], p.nlit);
+        const uint64_t bm = __ballot(start);
+        if (t < 6 * 64 && (t & 63) == 0) S.runmask[t >> 6] = bm;
+        __syncthreads();
+        if (start) {
+            uint32_t wq = (i + 1) >> 6;
+            uint64_t m = wq < 6 ? S.runmask[wq] & (~0ull << ((i + 1) & 63)) : 0;
+            while (!m && ++wq < 6) m = S.runmask[wq];
+            const uint32_t j = min(m ? wq * 64 + (uint32_t)__builtin_ctzll(m) : nall, nall);
+            isrun = true;
+            runv = v;
+            plan = plan_run(v, j - i);
+            if (plan.n18) atomicAdd(&S.prefreq[18], plan.n18);
+            if (plan.n17) atomicAdd(&S.prefreq[17], plan.n17);
+            if (plan.n16) atomicAdd(&S.prefreq[16], plan.n16);
+            if (plan.nlit) atomicAdd(&S.prefreq[v], plan.nlit);
+        }
     }
     __syncthreads();
-    build_lengths(S.prefreq, 19, 7, S.prelen, S.order, S.sh);
-    assign_codes(S.prelen, 19, S.precode, S.sh);
+    if (t < 64) {
+        wave_build_lengths(S.prefreq, 19, 7, S.prelen);
+        wave_assign_codes(S.prelen, 19, S.precode);
+    }
+    __syncthreads();
+    DMX_PHASE(dbg, seg, 6);
     uint32_t hclen = 4;
     for (int i = 18; i >= 4; i--)
         if (S.prelen[kPerm[i]]) { hclen = i + 1; break; }
-    uint32_t runbits[2] = {0, 0};
-    for (int k = 0; k < 2; k++) {
-        if (!isrun[k]) continue;
-        const RunPlan& p = plan[k];
-        runbits[k] = p.n18 * (S.prelen[18] + 7) + p.n17 * (S.prelen[17] + 3) +
-                     p.n16 * (S.prelen[16] + 2) + p.nlit * S.prelen[runv[k]];
-    }
-    uint32_t rtot0, rtot1;
-    const uint32_t off0 = block_excl_scan(runbits[0], S.scan, &rtot0);
-    const uint32_t off1 = block_excl_scan(runbits[1], S.scan, &rtot1);
-    const uint32_t hdr_bits = 14 + 3 * hclen + rtot0 + rtot1;  // after the 3-bit block header
+    const uint32_t runbits = isrun ? plan.n18 * (S.prelen[18] + 7) + plan.n17 * (S.prelen[17] + 3) +
+                                         plan.n16 * (S.prelen[16] + 2) + plan.nlit * S.prelen[runv]
+                                   : 0;
+    uint32_t rtot;
+    const uint32_t roff = block_excl_scan(runbits, S.scan, &rtot);
+    const uint32_t hdr_bits = 14 + 3 * hclen + rtot;  // after the 3-bit block header
+    DMX_PHASE(dbg, seg, 7);
 
     // ---- choose the block type (reference deflate.hpp:739-746 picks the smallest too) ----
     const uint64_t dyn_bits = 3ull + hdr_bits + dyn_tok;
@@ -447,33 +480,17 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t
     if (hbytes >= stored_bytes) return false;
 
     if (!use_dyn) {
-        for (int s = t; s < 286; s += DF_NT) S.litcode[s] = (fixed_lit_len(s) << 16) | fixed_lit_code(s);
+        if (t < 286) S.litcode[t] = (fixed_lit_len(t) << 16) | fixed_lit_code(t);
         if (t < 30) S.distcode[t] = (5u << 16) | bitrev(t, 5);
         __syncthreads();
     }
 
-    // ---- per-lane token bit counts and block scan ---------------------------------------
-    uint32_t mybits = 0;
-    if (t < NWALK) {
-        const uint32_t lo = t * DF_CHUNK, hi = min(lo + DF_CHUNK, nb);
-        uint32_t p = lo;
-        while (p < hi) {
-            const uint32_t d = S.cand[p];
-            if (d) {
-                const uint32_t L = S.cand[p + 1];
-                const uint32_t ls = len_sym(L), ds = dist_sym(d);
-                mybits += (S.litcode[ls] >> 16) + kLenExtra[ls - 257] + (S.distcode[ds] >> 16) +
-                          kDistExtra[ds];
-                p += L;
-            } else {
-                mybits += S.litcode[data_byte(S.data32, p)] >> 16;
-                p++;
-            }
-        }
-    }
+    // ---- token bits per bitmap word, block scan ------------------------------------------
+    const uint32_t mybits = (t < NMAP) ? word_bits(S, t) : 0;
     uint32_t tok_total;
     const uint32_t tok_off = block_excl_scan(mybits, S.scan, &tok_total);
     const uint32_t hdr_end = 3 + (use_dyn ? hdr_bits : 0);
+    DMX_PHASE(dbg, seg, 8);
 
     // ---- emission into the zeroed LDS image ---------------------------------------------
     if (t == 0) {
@@ -488,63 +505,57 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t
         }
         bw.flush();
     }
-    if (use_dyn) {
-        const uint32_t rbase = 3 + 14 + 3 * hclen;
-        for (int k = 0; k < 2; k++) {
-            if (!isrun[k]) continue;
-            const RunPlan& p = plan[k];
-            BitOr bw;
-            bw.init(S.U, rbase + (k == 0 ? off0 : rtot0 + off1));
-            const uint32_t v = runv[k];
-            if (v == 0) {
-                const uint32_t c18 = S.precode[18] & 0xFFFF, l18 = S.precode[18] >> 16;
-                for (uint32_t q = 0; q < p.n18; q++) {
-                    const uint32_t rep = (q + 1 == p.n18) ? p.last18 : 138;
-                    bw.put(c18, l18);
-                    bw.put(rep - 11, 7);
-                }
-                if (p.n17) {
-                    bw.put(S.precode[17] & 0xFFFF, S.precode[17] >> 16);
-                    bw.put(p.r17 - 3, 3);
-                }
-                for (uint32_t q = 0; q < p.nlit; q++) bw.put(S.precode[0] & 0xFFFF, S.precode[0] >> 16);
-            } else {
-                const uint32_t cv = S.precode[v] & 0xFFFF, lv = S.precode[v] >> 16;
-                bw.put(cv, lv);
-                const uint32_t c16 = S.precode[16] & 0xFFFF, l16 = S.precode[16] >> 16;
-                for (uint32_t q = 0; q < p.n16; q++) {
-                    const uint32_t rep = (q + 1 == p.n16) ? p.last16 : 6;
-                    bw.put(c16, l16);
-                    bw.put(rep - 3, 2);
-                }
-                for (uint32_t q = 1; q < p.nlit; q++) bw.put(cv, lv);
+    if (use_dyn && isrun) {
+        BitOr bw;
+        bw.init(S.U, 3 + 14 + 3 * hclen + roff);
+        const uint32_t v = runv;
+        if (v == 0) {
+            const uint32_t c18 = S.precode[18] & 0xFFFF, l18 = S.precode[18] >> 16;
+            for (uint32_t q = 0; q < plan.n18; q++) {
+                const uint32_t rep = (q + 1 == plan.n18) ? plan.last18 : 138;
+                bw.put(c18, l18);
+                bw.put(rep - 11, 7);
             }
-            bw.flush();
+            if (plan.n17) {
+                bw.put(S.precode[17] & 0xFFFF, S.precode[17] >> 16);
+                bw.put(plan.r17 - 3, 3);
+            }
+            for (uint32_t q = 0; q < plan.nlit; q++) bw.put(S.precode[0] & 0xFFFF, S.precode[0] >> 16);
+        } else {
+            const uint32_t cv = S.precode[v] & 0xFFFF, lv = S.precode[v] >> 16;
+            bw.put(cv, lv);
+            const uint32_t c16 = S.precode[16] & 0xFFFF, l16 = S.precode[16] >> 16;
+            for (uint32_t q = 0; q < plan.n16; q++) {
+                const uint32_t rep = (q + 1 == plan.n16) ? plan.last16 : 6;
+                bw.put(c16, l16);
+                bw.put(rep - 3, 2);
+            }
+            for (uint32_t q = 1; q < plan.nlit; q++) bw.put(cv, lv);
         }
+        bw.flush();
     }
-    if (t < NWALK) {
+    if (t < NMAP && mybits) {
         BitOr bw;
         bw.init(S.U, hdr_end + tok_off);
-        const uint32_t lo = t * DF_CHUNK, hi = min(lo + DF_CHUNK, nb);
-        uint32_t p = lo;
-        while (p < hi) {
+        uint32_t w = S.tokmap[t];
+        while (w) {
+            const uint32_t p = t * 32 + __builtin_ctz(w);
+            w &= w - 1;
             const uint32_t d = S.cand[p];
             if (d) {
                 const uint32_t L = S.cand[p + 1];
                 const uint32_t ls = len_sym(L), ds = dist_sym(d);
                 const uint32_t lc = S.litcode[ls];
                 bw.put(lc & 0xFFFF, lc >> 16);
-                const uint32_t le = kLenExtra[ls - 257];
-                if (le) bw.put(L - kLenBase[ls - 257], le);
+                const uint32_t le = len_extra(ls);
+                if (le) bw.put(L - len_base(ls), le);
                 const uint32_t dc = S.distcode[ds];
                 bw.put(dc & 0xFFFF, dc >> 16);
-                const uint32_t de = kDistExtra[ds];
-                if (de) bw.put(d - kDistBase[ds], de);
-                p += L;
+                const uint32_t de = dist_extra(ds);
+                if (de) bw.put(d - dist_base(ds), de);
             } else {
                 const uint32_t lc = S.litcode[data_byte(S.data32, p)];
                 bw.put(lc & 0xFFFF, lc >> 16);
-                p++;
             }
         }
         bw.flush();
@@ -565,6 +576,7 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t
         }
     }
     __syncthreads();
+    DMX_PHASE(dbg, seg, 9);
     const uint32_t nv = (total + 15) / 16;
     const uint4* s4 = reinterpret_cast<const uint4*>(S.U);
     uint4* d4 = reinterpret_cast<uint4*>(slot);
@@ -576,8 +588,9 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t
 template <int SEG>
 __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
     __shared__ DfSmem<SEG> S;
-    constexpr int HB = DfSmem<SEG>::HB;
     constexpr int NWALK = DfSmem<SEG>::NWALK;
+    constexpr int HT = DfSmem<SEG>::HT;
+    constexpr int NMAP = SEG / 32;
     const int t = threadIdx.x;
     const uint64_t seg = blockIdx.x;
     const uint64_t base = seg * (uint64_t)SEG;
@@ -586,6 +599,9 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
     const int level = A.level;
     uint8_t* const slot = A.slots + seg * (uint64_t)A.slot_bytes;
     uint8_t* const dbytes = reinterpret_cast<uint8_t*>(S.data32);
+    uint32_t* const head = S.U;
+    uint32_t* const first = S.U + HT;
+    DMX_PHASE(A.dbg, seg, 0);
 
     // ---- load the segment into LDS (16 B per lane when aligned) ------------------------
     {
@@ -601,80 +617,172 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
         }
         // zero padding after the data (match compares read up to 8 bytes past)
         for (uint32_t i = nb + t; i < ((nb + 3) & ~3u) + 32; i += DF_NT) dbytes[i] = 0;
-        for (int i = t; i < 288; i += DF_NT) S.litfreq[i] = 0;
+        if (t < 288) S.litfreq[t] = 0;
         if (t < 32) { S.distfreq[t] = 0; S.prefreq[t] = 0; }
+        if (t < NMAP) S.tokmap[t] = 0;
         if (level >= 2)
-            for (int i = t; i < (1 << HB); i += DF_NT) S.U[i] = 0;
+            for (int i = t; i < 2 * HT; i += DF_NT) S.U[i] = 0;
     }
     __syncthreads();
+    DMX_PHASE(A.dbg, seg, 1);
 
     if (level != 0) {
-        // ---- match candidates: rounds of 1024 positions, 4 consecutive per thread ------
+        // ---- match candidates: rounds of 2*DF_NT positions, two per thread ---------------
         if (level >= 2) {
-            for (uint32_t r0 = 0; r0 < nb; r0 += 4 * DF_NT) {
-                const uint32_t p0 = r0 + 4 * t;
-                uint32_t h[4];
-                bool ok[4] = {false, false, false, false};
-                if (p0 < nb) {
-                    const uint32_t w0 = S.data32[p0 >> 2], w1 = S.data32[(p0 >> 2) + 1];
+            bool pok[2] = {false, false};
+            uint32_t ph[2] = {0, 0}, pp[2] = {0, 0};
+            for (uint32_t r0 = 0, rr = 0; r0 < nb; r0 += 2 * DF_NT, rr++) {
+                uint32_t h[2], p[2];
+                bool ok[2];
 #pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const uint32_t p = p0 + j;
-                        ok[j] = p + 4 <= nb;
-                        const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, j);
-                        h[j] = (v * 0x1E35A7BDu) >> (32 - HB);
-                        uint32_t c = 0;
-                        if (ok[j]) {
-                            const uint32_t q = S.U[h[j]];
-                            if (q) {
-                                c = p - (q - 1);
-                                if (c > 32768) c = 0;
-                            }
-                        }
-                        if (p < nb) S.cand[p] = (uint16_t)c;
-                    }
+                for (int k = 0; k < 2; k++) {
+                    p[k] = r0 + k * DF_NT + t;
+                    ok[k] = p[k] + 4 <= nb;
+                    h[k] = ok[k] ? (ld32u(S.data32, p[k]) * 0x1E35A7BDu) >> (32 - DF_HB) : 0;
+                    if (ok[k]) atomicMax(&first[h[k]], (rr << 16) | (0xFFFFu - p[k]));  // first in round
+                    if (pok[k]) atomicMax(&head[ph[k]], pp[k] + 1);                     // previous round
                 }
                 __syncthreads();
 #pragma unroll
-                for (int j = 0; j < 4; j++)
-                    if (ok[j]) atomicMax(&S.U[h[j]], p0 + j + 1);
+                for (int k = 0; k < 2; k++) {
+                    uint32_t c = 0;
+                    if (ok[k]) {
+                        const uint32_t f = first[h[k]];
+                        if ((f >> 16) == rr) {
+                            const uint32_t q = 0xFFFFu - (f & 0xFFFF);
+                            if (q < p[k]) c = p[k] - q;
+                        }
+                        if (!c) {
+                            const uint32_t q = head[h[k]];
+                            if (q) c = p[k] - (q - 1);
+                        }
+                        if (c > 32768) c = 0;
+                    }
+                    if (p[k] < nb) S.cand[p[k]] = (uint16_t)c;
+                    pok[k] = ok[k];
+                    ph[k] = h[k];
+                    pp[k] = p[k];
+                }
                 __syncthreads();
             }
+            DMX_PHASE(A.dbg, seg, 14);
+            // ---- match lengths capped at 16 (and at the chunk end), data-parallel; bit p of
+            //      tokmap = "a match of >= 3 starts at p" until the walk turns it into tokens
+            uint8_t* const L16 = reinterpret_cast<uint8_t*>(S.U);
+            const uint32_t wave = t >> 6, lane = t & 63;
+            for (uint32_t b = wave * 64; b < nb; b += DF_NT) {
+                const uint32_t q = b + lane;
+                uint32_t L = 0;
+                if (q < nb) {
+                    const uint32_t d = S.cand[q];
+                    if (d) {
+                        const uint32_t cap = min(16u, min(q / DF_CHUNK * DF_CHUNK + DF_CHUNK, nb) - q);
+                        L = matchlen(S.data32, q, q - d, cap);
+                        if (L < 3) {
+                            L = 0;
+                            S.cand[q] = 0;
+                        }
+                    }
+                    L16[q] = (uint8_t)L;
+                }
+                const uint64_t m = __ballot(L >= 3);
+                if (lane == 0) {
+                    S.tokmap[b >> 5] = (uint32_t)m;
+                    if ((b >> 5) + 1 < NMAP) S.tokmap[(b >> 5) + 1] = (uint32_t)(m >> 32);
+                }
+            }
+            __syncthreads();
         }
+        DMX_PHASE(A.dbg, seg, 2);
 
-        // ---- tokenize walk: one 256-byte chunk per lane ----------------------------------
-        if (t < NWALK) {
+        // ---- parse walk: one 256-byte chunk per lane; jumps over literal runs with the
+        //      match bitmap, turns it into the token-start bitmap in place ------------------
+        if (level >= 2 && t < NWALK) {
+            const uint8_t* const L16 = reinterpret_cast<const uint8_t*>(S.U);
             const uint32_t lo = t * DF_CHUNK;
             const uint32_t hi = min(lo + DF_CHUNK, nb);
-            uint32_t p = lo;
+            const uint32_t wlast = (hi - 1) >> 5;
+            auto bits_range = [](uint32_t a, uint32_t b, uint32_t w) -> uint32_t {  // [a, b) in word w
+                const uint32_t e = b - w * 32;
+                return (e >= 32 ? 0xFFFFFFFFu : ((1u << e) - 1u)) & (0xFFFFFFFFu << (a & 31));
+            };
+            auto full_len = [&](uint32_t q) -> uint32_t {
+                uint32_t L = L16[q];
+                if (L == 16 && hi - q > 16) {
+                    const uint32_t d = S.cand[q];
+                    L = 16 + matchlen(S.data32, q + 16, q + 16 - d, min(258u, hi - q) - 16);
+                }
+                return L;
+            };
+            uint32_t p = lo, w = lo >> 5, mw = S.tokmap[w], tok = 0;
             while (p < hi) {
-                const uint32_t d = (level >= 2) ? S.cand[p] : 0;
-                uint32_t L = 0;
-                if (d) L = matchlen(S.data32, p, p - d, min(258u, hi - p));
-                if (level == 3 && L >= 3 && L < 258 && p + 1 < hi) {
-                    const uint32_t d2 = S.cand[p + 1];
-                    if (d2) {
-                        const uint32_t L2 = matchlen(S.data32, p + 1, p + 1 - d2, min(258u, hi - p - 1));
-                        if (L2 > L) L = 0;  // literal here, the longer match starts next
+                const uint32_t wi = p >> 5;
+                if (wi != w) {
+                    S.tokmap[w] = tok;
+                    for (uint32_t x = w + 1; x < wi; x++) S.tokmap[x] = 0;
+                    w = wi;
+                    mw = S.tokmap[w];
+                    tok = 0;
+                }
+                const uint32_t m = mw & (0xFFFFFFFFu << (p & 31));
+                const uint32_t q = m ? w * 32 + __builtin_ctz(m) : 0xFFFFFFFFu;
+                if (q >= hi || !m) {  // literals to the end of the word (or chunk)
+                    const uint32_t e = min((w + 1) * 32, hi);
+                    tok |= bits_range(p, e, w);
+                    p = e;
+                    continue;
+                }
+                tok |= bits_range(p, q, w);  // literals before the match
+                p = q;
+                uint32_t L = full_len(p);
+                const uint32_t l1 = (level == 3 && L < 258 && p + 1 < hi) ? L16[p + 1] : 0;
+                if (l1 > L || (l1 == 16 && L >= 16)) {
+                    if (full_len(p + 1) > L) {  // lazy: literal here, the longer match next
+                        tok |= 1u << (p & 31);
+                        S.cand[p] = 0;
+                        p++;
+                        continue;
                     }
                 }
-                if (L >= 3) {
-                    atomicAdd(&S.litfreq[len_sym(L)], 1u);
+                tok |= 1u << (p & 31);
+                S.cand[p + 1] = (uint16_t)L;
+                p += L;
+            }
+            S.tokmap[w] = tok;
+            for (uint32_t x = w + 1; x <= wlast; x++) S.tokmap[x] = 0;
+        }
+        if (level < 2) {  // Huffman only: every position is a literal token
+            for (uint32_t i = t; i < nb; i += DF_NT) S.cand[i] = 0;
+            if (t < NMAP) {
+                const uint32_t b0 = t * 32;
+                S.tokmap[t] = b0 >= nb ? 0u : (nb - b0 >= 32 ? 0xFFFFFFFFu : ((1u << (nb - b0)) - 1u));
+            }
+        }
+        __syncthreads();
+        DMX_PHASE(A.dbg, seg, 3);
+
+        // ---- histogram over token starts; the output image is zeroed meanwhile ------------
+        if (t < NMAP) {
+            uint32_t w = S.tokmap[t];
+            while (w) {
+                const uint32_t p = t * 32 + __builtin_ctz(w);
+                w &= w - 1;
+                const uint32_t d = S.cand[p];
+                if (d) {
+                    atomicAdd(&S.litfreq[len_sym(S.cand[p + 1])], 1u);
                     atomicAdd(&S.distfreq[dist_sym(d)], 1u);
-                    S.cand[p + 1] = (uint16_t)L;
-                    p += L;
                 } else {
-                    S.cand[p] = 0;
-                    atomicAdd(&S.litfreq[dbytes[p]], 1u);
-                    p++;
+                    atomicAdd(&S.litfreq[data_byte(S.data32, p)], 1u);
                 }
             }
         }
-        if (t == 0) S.litfreq[256] = 1;  // end-of-block
-        __syncthreads();
         for (int i = t; i < DfSmem<SEG>::UW; i += DF_NT) S.U[i] = 0;
-        // emit_huffman's first barrier orders the zeroing before any emission
-        if (emit_huffman<SEG>(S, nb, is_final, slot, &A.sizes[seg])) return;
+        if (t == 0) atomicAdd(&S.litfreq[256], 1u);  // end-of-block
+        __syncthreads();
+        if (emit_huffman<SEG>(S, nb, is_final, slot, &A.sizes[seg], A.dbg, seg)) {
+            DMX_PHASE(A.dbg, seg, 10);
+            return;
+        }
     }
     emit_stored<SEG>(S, nb, is_final, slot, &A.sizes[seg]);
 }

@@ -40,6 +40,22 @@ __device__ __forceinline__ uint32_t dist_sym(uint32_t d) {
     return 2 * k + ((x >> (k - 1)) & 1);
 }
 
+// RFC 1951 3.2.5 length / distance code parameters by arithmetic (no table loads in hot loops)
+__device__ __forceinline__ uint32_t len_extra(uint32_t s) {  // s in 257..285
+    return (s >= 265 && s < 285) ? (s - 261) >> 2 : 0;
+}
+__device__ __forceinline__ uint32_t len_base(uint32_t s) {
+    if (s < 265) return s - 254;
+    if (s >= 285) return 258;
+    return ((4 + ((s - 265) & 3)) << ((s - 261) >> 2)) + 3;
+}
+__device__ __forceinline__ uint32_t dist_extra(uint32_t d) {  // d in 0..29
+    return d < 4 ? 0 : (d >> 1) - 1;
+}
+__device__ __forceinline__ uint32_t dist_base(uint32_t d) {
+    return d < 4 ? d + 1 : ((2 + (d & 1)) << ((d >> 1) - 1)) + 1;
+}
+
 __device__ __forceinline__ uint32_t bitrev(uint32_t v, uint32_t n) {
     return n ? (__builtin_bitreverse32(v) >> (32 - n)) : 0;
 }
@@ -64,6 +80,39 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
+}
+
+// Sorts 512 keys held as k[8] per lane (element index = lane * 8 + r) into descending order
+// with a register bitonic network (45 stages; cross-lane stages use ds_bpermute shuffles).
+__device__ __forceinline__ void wave_sort512_desc(uint32_t (&k)[8]) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int size = 2; size <= 512; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 8) {
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    const int i = lane * 8 + r;
+                    const uint32_t o = __shfl_xor(k[r], stride >> 3, 64);
+                    const bool lower = (i & stride) == 0;
+                    const bool desc = (i & size) == 0;
+                    k[r] = (lower == desc) ? max(k[r], o) : min(k[r], o);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    const int p = r ^ stride;
+                    if (p > r) {
+                        const bool desc = ((lane * 8 + r) & size) == 0;
+                        const uint32_t a = k[r], b = k[p];
+                        k[r] = desc ? max(a, b) : min(a, b);
+                        k[p] = desc ? min(a, b) : max(a, b);
+                    }
+                }
+            }
+        }
+    }
 }
 
 }  // namespace dmx

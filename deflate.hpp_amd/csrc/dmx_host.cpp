@@ -7,10 +7,13 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <string>
 
 #include "../../include/dmx.h"
 #include "dmx_internal.h"
@@ -54,7 +57,7 @@ struct dmx_ctx {
     uint32_t flags = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
-    DevBuf in, out, slots, sizes, offs, scal, cands, tiles, tileoffs, recs, status;
+    DevBuf in, out, slots, sizes, offs, scal, cands, tiles, tileoffs, recs, status, dbg;
     bool timing = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     dmx_stats stats{};
@@ -74,6 +77,48 @@ struct Scal {  // small device-side scalars, one allocation
     uint32_t pad;
     InflateResult res;
 };
+
+// DMX_PHASES=<file>: kernels record s_memtime per phase and segment; the host appends one line
+// "<kernel> <nsegs> <mean cycles of phase k - phase k-1 ...>" per call (developer profiling).
+uint64_t* phase_buf(dmx_ctx* c, uint64_t nidx) {
+    if (!std::getenv("DMX_PHASES")) return nullptr;
+    if (!c->dbg.ensure(nidx * kPhaseSlots * 8)) return nullptr;
+    (void)hipMemset(c->dbg.p, 0, nidx * kPhaseSlots * 8);
+    return c->dbg.as<uint64_t>();
+}
+void phase_dump(dmx_ctx* c, const char* kernel, uint64_t nidx, hipStream_t st) {
+    const char* path = std::getenv("DMX_PHASES");
+    if (!path || !c->dbg.p) return;
+    std::vector<uint64_t> h(nidx * kPhaseSlots);
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpy(h.data(), c->dbg.p, h.size() * 8, hipMemcpyDeviceToHost);
+    double sum[kPhaseSlots] = {0};
+    uint64_t cnt[kPhaseSlots] = {0};
+    const bool inf = std::string(kernel) == "inflate";
+    for (uint64_t i = 0; i < nidx; i++) {
+        const uint64_t* r = &h[i * kPhaseSlots];
+        uint64_t prev = r[0];
+        for (int k = 1; k < (inf ? 8 : 12); k++) {
+            if (!inf && k == 12) break;
+            if (!r[k]) continue;
+            sum[k] += (double)(r[k] - prev);
+            cnt[k]++;
+            prev = r[k];
+        }
+        if (inf) { sum[15] += (double)r[8]; cnt[15]++; }
+        if (!inf && r[12] && r[13] && r[3] && r[14]) {  // Huffman build sub-phases, match rounds
+            sum[12] += (double)(r[12] - r[3]); cnt[12]++;
+            sum[13] += (double)(r[13] - r[12]); cnt[13]++;
+            sum[14] += (double)(r[14] - r[1]); cnt[14]++;
+        }
+    }
+    FILE* f = std::fopen(path, "a");
+    if (!f) return;
+    std::fprintf(f, "%s %llu", kernel, (unsigned long long)nidx);
+    for (int k = 1; k < kPhaseSlots; k++) std::fprintf(f, " p%d=%.0f", k, cnt[k] ? sum[k] / cnt[k] : 0.0);
+    std::fprintf(f, "\n");
+    std::fclose(f);
+}
 
 void begin_timing(dmx_ctx* c, hipStream_t st) {
     c->stats = dmx_stats{};
@@ -123,7 +168,9 @@ int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, 
     A.total = &c->scal.as<Scal>()->total;
     A.out = d_out;
     A.cap = cap;
+    A.dbg = phase_buf(c, nseg);
     HIPCHK(launch_deflate(A, c->seg, st, c->timing ? c->ev[1] : nullptr, c->timing ? c->ev[2] : nullptr));
+    if (A.dbg) phase_dump(c, "deflate", nseg, st);
     uint64_t total = 0;
     HIPCHK(hipMemcpyAsync(&total, A.total, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -180,18 +227,24 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     A.status = c->status.as<unsigned long long>();
     A.ticket = &ds->ticket;
     A.flags = c->flags;
-    HIPCHK(hipMemsetAsync(A.status, 0, ncand * 8, st));
-    HIPCHK(hipMemsetAsync(&ds->ticket, 0, 4, st));
-    HIPCHK(launch_inflate_segments(A, st, c->timing ? c->ev[1] : nullptr, c->timing ? c->ev[2] : nullptr));
-    HIPCHK(launch_inflate_validate(A, &ds->res, st));
+    A.dbg = phase_buf(c, ncand);
     InflateResult r{};
-    HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    for (uint32_t mode = 0; mode < 2; mode++) {
+        A.mode = mode;
+        HIPCHK(hipMemsetAsync(A.status, 0, ncand * 8, st));
+        HIPCHK(hipMemsetAsync(&ds->ticket, 0, 4, st));
+        HIPCHK(launch_inflate_segments(A, st, c->timing ? c->ev[1] : nullptr, c->timing ? c->ev[2] : nullptr));
+        HIPCHK(launch_inflate_validate(A, &ds->res, st));
+        if (A.dbg) phase_dump(c, "inflate", ncand, st);
+        HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (r.status != 1) break;  // 1: sizes not uniform, place outputs by look-back
+    }
     c->stats.segments = ncand;
     c->stats.in_bytes = n;
     if (r.status == 0) {
         end_timing(c, st);
-        c->stats.path = 0;
+        c->stats.path = A.mode;
         c->stats.out_bytes = r.total;
         *total_out = r.total;
         if (dev_out) *dev_out = out;
@@ -199,7 +252,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     }
 
     // serial path: size pass, then write pass
-    c->stats.path = 1;
+    c->stats.path = 2;
     HIPCHK(launch_inflate_serial(A, 1, &ds->res, st));
     HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -269,7 +322,7 @@ void dmx_destroy(dmx_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->in, &c->out, &c->slots, &c->sizes, &c->offs, &c->scal, &c->cands,
-                      &c->tiles, &c->tileoffs, &c->recs, &c->status})
+                      &c->tiles, &c->tileoffs, &c->recs, &c->status, &c->dbg})
         b->release();
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);

@@ -18,6 +18,7 @@ struct DeflateArgs {
     uint64_t* total;      // 1
     uint8_t* out;
     uint64_t cap;
+    uint64_t* dbg;        // optional per-block phase timestamps (DMX_PHASES), else nullptr
 };
 
 hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t st, hipEvent_t ev0,
@@ -26,6 +27,7 @@ hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t 
 // per-candidate record of the segment-parallel inflate
 struct SegRecord {
     uint64_t end_byte;  // byte offset (relative to the stream) just past the segment's marker
+    uint64_t offset;    // output offset the segment was written at
     uint32_t out_size;
     uint32_t flags;     // SEGF_*
 };
@@ -50,12 +52,20 @@ struct InflateArgs {
     unsigned long long* status;  // ncand look-back words (zeroed)
     unsigned int* ticket;        // zeroed
     uint32_t flags;              // DMX_CFG_RFC_STRICT
+    uint32_t mode;               // 0 = speculative uniform segment sizes, 1 = decoupled look-back
+    uint64_t* dbg;               // optional per-segment phase timestamps (DMX_PHASES)
 };
+
+constexpr int kPhaseSlots = 16;
+#define DMX_PHASE(dbg, idx, slot)                                                   \
+    do {                                                                            \
+        if ((dbg) && threadIdx.x == 0) (dbg)[(idx) * kPhaseSlots + (slot)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 
 // result of validation / serial decode, copied to the host
 struct InflateResult {
     uint64_t total;   // decoded bytes
-    int32_t status;   // 0 ok, DMX_ERR_* for the serial path; 1 = fast path needs fallback
+    int32_t status;   // fast path: 0 ok, 1 re-run with look-back, 2 serial; serial: 0 / DMX_ERR_*
     uint32_t fin_index;
 };
 

@@ -56,9 +56,10 @@ struct BitIn {
     const uint32_t* w;
     uint64_t nwords, end_bytes, end_bits;
     uint64_t pos;  // bits consumed, relative to the aligned base
-    uint64_t buf;
-    uint32_t cnt;
-    uint64_t wi;
+    uint64_t buf;  // LSB = next bit
+    uint32_t cnt;  // valid bits in buf
+    uint64_t wi;   // index of the word held in q0
+    uint32_t q0, q1;  // raw words wi, wi + 1 (loaded two refills ahead of use)
 
     __device__ void init(const uint32_t* words, uint64_t misalign, uint64_t n) {
         w = words;
@@ -66,26 +67,37 @@ struct BitIn {
         end_bits = end_bytes * 8;
         nwords = (end_bytes + 3) / 4;
     }
-    __device__ uint32_t load(uint64_t i) const {
-        if (i >= nwords) return 0;
-        uint32_t v = w[i];
+    // Unconditional load with a clamped index (no branch, so the wait lands at first use).
+    // The decoder state is wave-uniform, so the input is read through the scalar cache
+    // (s_load, constant address space): a vector load would be waited on immediately to move
+    // its value into an SGPR, defeating the two-word prefetch.
+    __device__ uint32_t raw(uint64_t i) const {
+        const __attribute__((address_space(4))) uint32_t* cw =
+            (const __attribute__((address_space(4))) uint32_t*)w;
+        return cw[i < nwords ? i : nwords - 1];
+    }
+    __device__ uint32_t mask(uint64_t i) const {  // bytes of word i inside the stream
+        if (i >= nwords) return 0u;
         const uint64_t lim = end_bytes - 4 * i;
-        if (lim < 4) v &= (1u << (8 * lim)) - 1u;
-        return v;
+        return lim >= 4 ? 0xFFFFFFFFu : ((1u << (8 * lim)) - 1u);
     }
     __device__ void refill() {
         if (cnt <= 32) {
-            buf |= (uint64_t)load(wi) << cnt;
-            wi++;
+            buf |= (uint64_t)(q0 & mask(wi)) << cnt;
             cnt += 32;
+            wi++;
+            q0 = q1;
+            q1 = raw(wi + 1);
         }
     }
     __device__ void seek(uint64_t bitpos) {
         pos = bitpos;
-        wi = bitpos >> 5;
-        buf = (uint64_t)(load(wi) >> (bitpos & 31));
+        const uint64_t i = bitpos >> 5;
+        buf = (uint64_t)((raw(i) & mask(i)) >> (bitpos & 31));
         cnt = 32 - (uint32_t)(bitpos & 31);
-        wi++;
+        wi = i + 1;
+        q0 = raw(wi);
+        q1 = raw(wi + 1);
         refill();
     }
     __device__ void ensure(uint32_t k) {  // k <= 33
@@ -181,17 +193,29 @@ __device__ __forceinline__ bool key_hit(const TreeMeta& m, uint32_t k, uint32_t 
 // primary LUT over PB bits: entry = sym | (len << 9), 0 = no code of length <= PB matches
 template <int PB>
 __device__ void fill_lut(uint16_t* lut, const TreeMeta& m, const uint16_t* sorted) {
+    uint32_t lo[PB + 1], hi[PB + 1], cn[PB + 1], of[PB + 1];
+#pragma unroll
+    for (int k = 1; k <= PB; k++) {
+        lo[k] = m.lo[k];
+        hi[k] = m.hi[k];
+        cn[k] = m.cnt[k];
+        of[k] = m.offs[k];
+    }
     for (int wv = lane_id(); wv < (1 << PB); wv += 64) {
         const uint32_t v = bitrev(wv, PB);
-        uint16_t e = 0;
+        uint32_t idx = 0, len = 0;
+#pragma unroll
         for (int k = 1; k <= PB; k++) {
-            uint32_t c;
-            if (key_hit(m, k, v >> (PB - k), &c)) {
-                e = (uint16_t)(sorted[m.offs[k] + c - m.lo[k]] | (k << 9));
-                break;
+            const uint32_t x = v >> (PB - k);
+            if (!len && cn[k] && x <= hi[k]) {
+                const uint32_t cm = x + (((hi[k] - x) >> k) << k);
+                if (cm >= lo[k]) {
+                    idx = of[k] + cm - lo[k];
+                    len = k;
+                }
             }
         }
-        lut[wv] = e;
+        lut[wv] = len ? (uint16_t)(sorted[idx] | (len << 9)) : (uint16_t)0;
     }
 }
 
@@ -456,8 +480,8 @@ __device__ uint32_t decode_huffman(BitIn& br, const Tables& T, Sink& sk) {
         if (sym == 256) return br.over() ? SEGF_OVERREAD : 0;
         uint32_t L = 0;
         if (sym <= 285) {
-            const uint32_t ex = kLenExtra[sym - 257];
-            L = kLenBase[sym - 257] + (ex ? br.bits(ex) : 0);
+            const uint32_t ex = len_extra(sym);
+            L = len_base(sym) + (ex ? br.bits(ex) : 0);
         }
         br.ensure(28);
         v = br.peek(15);
@@ -472,8 +496,8 @@ __device__ uint32_t decode_huffman(BitIn& br, const Tables& T, Sink& sk) {
         br.consume(dl);
         uint32_t dist = 0;
         if (ds < 30) {
-            const uint32_t ex = kDistExtra[ds];
-            dist = kDistBase[ds] + (ex ? br.bits(ex) : 0);
+            const uint32_t ex = dist_extra(ds);
+            dist = dist_base(ds) + (ex ? br.bits(ex) : 0);
         }
         if (br.over()) return SEGF_OVERREAD;
         if (!sk.copy(L, dist)) return sk.err;
@@ -484,7 +508,7 @@ __device__ uint32_t decode_huffman(BitIn& br, const Tables& T, Sink& sk) {
 // non-final stored block whose NLEN is FFFF (the "00 00 FF FF" the scanner keyed on).
 template <class Sink>
 __device__ uint32_t inflate_blocks(BitIn& br, Tables& T, Sink& sk, bool rfc, bool stop_at_marker,
-                                   uint64_t* end_byte, bool* fin) {
+                                   uint64_t* end_byte, bool* fin, uint64_t* hdr_cycles = nullptr) {
     *fin = false;
     for (;;) {
         br.ensure(3);
@@ -515,7 +539,9 @@ __device__ uint32_t inflate_blocks(BitIn& br, Tables& T, Sink& sk, bool rfc, boo
             if (err) return err;
         } else if (btype == 2) {
             T.fixed_loaded = 0;
+            const uint64_t h0 = hdr_cycles ? __builtin_amdgcn_s_memtime() : 0;
             uint32_t err = read_dynamic_header(br, T, rfc);
+            if (hdr_cycles) *hdr_cycles += __builtin_amdgcn_s_memtime() - h0;
             if (err) return err;
             err = decode_huffman(br, T, sk);
             if (err) return err;
@@ -625,7 +651,9 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
     __syncthreads();
     const uint64_t j = s_j;
     if (j >= A.ncand) return;
+    DMX_PHASE(A.dbg, j, 0);
     const uint64_t start = A.cands[j];
+    uint64_t hdr_cycles = 0;
 
     BitIn br;
     br.init(A.in_words, A.misalign, A.n);
@@ -633,14 +661,35 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
     SegSink sk{win, 0, j == 0, 0};
     uint64_t end_byte = 0;
     bool fin = false;
-    uint32_t err = inflate_blocks(br, T, sk, (A.flags & DMX_CFG_RFC_STRICT) != 0, true, &end_byte, &fin);
+    uint32_t err = inflate_blocks(br, T, sk, (A.flags & DMX_CFG_RFC_STRICT) != 0, true, &end_byte, &fin,
+                                  A.dbg ? &hdr_cycles : nullptr);
     const uint32_t size = err ? 0 : sk.pos;
+    DMX_PHASE(A.dbg, j, 1);
+    if (A.dbg && lane_id() == 0) A.dbg[j * kPhaseSlots + 8] = hdr_cycles;
 
     if (lane == 0) {
         uint64_t excl = 0;
-        if (j == 0) {
+        if (A.mode == 0) {
+            // speculative: every segment before the final one has this segment's size (what
+            // libdmx's deflate emits); the final one takes segment 0's size.  Checked after
+            // the kernel by k_inflate_validate; a miss re-runs in look-back mode.
+            if (j == 0) {
+                __hip_atomic_store(&A.status[0], LB_P | size, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (!fin) {
+                excl = j * (uint64_t)size;
+            } else {
+                uint32_t spins = 0;
+                unsigned long long v;
+                while (((v = __hip_atomic_load(&A.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0) {
+                    if (++spins > (1u << 24)) { err |= SEGF_TIMEOUT; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                excl = j * (v & LB_V);
+            }
+        } else if (j == 0) {
             __hip_atomic_store(&A.status[0], LB_P | size, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
+            // decoupled look-back over the candidates before this one
             __hip_atomic_store(&A.status[j], LB_A | size, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             uint64_t k = j - 1;
             uint32_t spins = 0;
@@ -664,9 +713,11 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         s_excl = excl;
+        DMX_PHASE(A.dbg, j, 2);
         A.recs[j].end_byte = end_byte - A.misalign;
         A.recs[j].out_size = size;
         A.recs[j].flags = err | (fin ? SEGF_FINAL : 0u);
+        A.recs[j].offset = excl;
     }
     __syncthreads();
     if (err) return;
@@ -683,13 +734,18 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
     } else {
         for (uint32_t i = lane; i < nb; i += 64) dst[i] = win[i];
     }
+    DMX_PHASE(A.dbg, j, 3);
 }
 
+// Candidate chain check.  Valid iff, up to the first BFINAL segment k, every segment decoded
+// without error and ended exactly at the next candidate.  Speculative mode additionally needs
+// every segment before k to have segment 0's size (else status 1: re-run with look-back).
 __global__ __launch_bounds__(1024) void k_inflate_validate(InflateArgs A, InflateResult* res) {
-    __shared__ unsigned long long kmin, bmin;
+    __shared__ unsigned long long kmin, bmin, umin;
     const int t = threadIdx.x;
-    if (t == 0) { kmin = ~0ull; bmin = ~0ull; }
+    if (t == 0) { kmin = ~0ull; bmin = ~0ull; umin = ~0ull; }
     __syncthreads();
+    const uint32_t size0 = A.recs[0].out_size;
     for (uint64_t j = t; j < A.ncand; j += 1024) {
         const SegRecord r = A.recs[j];
         const bool fin = (r.flags & SEGF_FINAL) != 0;
@@ -697,18 +753,23 @@ __global__ __launch_bounds__(1024) void k_inflate_validate(InflateArgs A, Inflat
         const bool chain = (j + 1 < A.ncand) && r.end_byte == A.cands[j + 1];
         if (fin) atomicMin(&kmin, (unsigned long long)j);
         if (err || (!fin && !chain)) atomicMin(&bmin, (unsigned long long)j);
+        if (!fin && r.out_size != size0) atomicMin(&umin, (unsigned long long)j);
     }
     __syncthreads();
     if (t == 0) {
         const uint64_t k = kmin;
+        res->fin_index = (uint32_t)k;
         if (k < A.ncand && bmin > k) {
-            res->total = A.status[k] & LB_V;
-            res->status = 0;
-            res->fin_index = (uint32_t)k;
+            if (A.mode == 0 && umin < k) {
+                res->status = 1;
+                res->total = 0;
+            } else {
+                res->status = 0;
+                res->total = A.recs[k].offset + A.recs[k].out_size;
+            }
         } else {
             res->total = 0;
-            res->status = 1;
-            res->fin_index = 0;
+            res->status = 2;
         }
     }
 }

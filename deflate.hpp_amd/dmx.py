@@ -57,6 +57,10 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    try:  # share torch's HIP runtime (same SONAME libamdhip64.so.7) instead of loading a second
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise OSError(f"{LIB_PATH} missing: build it with `make -C deflate.hpp_amd` "
                       "(or __graft_entry__.build()); there is no CPU fallback")

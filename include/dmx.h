@@ -37,7 +37,7 @@ typedef struct dmx_ctx dmx_ctx;
 
 typedef struct dmx_config {
     int device;             /* HIP device ordinal, -1 = the calling thread's current device  */
-    uint32_t segment_bytes; /* independent deflate segment: 16384, 32768 (default) or 65536.
+    uint32_t segment_bytes; /* independent deflate segment: 16384 or 32768 (default).
                                32768 mirrors the reference's per-chunk LZ77 reset
                                (deflate.hpp:689-697).                                          */
     uint32_t flags;         /* DMX_CFG_*                                                        */
@@ -106,7 +106,8 @@ typedef struct dmx_stats {
     uint64_t segments;      /* segments (deflate) / candidate segments (inflate)            */
     uint64_t in_bytes;
     uint64_t out_bytes;
-    uint32_t path;          /* inflate: 0 = segment-parallel fast path, 1 = serial path      */
+    uint32_t path;          /* inflate: 0 = segment-parallel (speculative offsets),
+                               1 = segment-parallel (look-back offsets), 2 = serial path     */
     uint32_t reserved;
 } dmx_stats;
 

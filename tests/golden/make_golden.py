@@ -1,0 +1,147 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/ fixtures from the REAL reference (oracle/_ref/libdeflate_ref.so,
+compiled in place from /root/reference/include by oracle/Makefile) and zlib 1.2.11.
+
+Run in the build container (where /root/reference exists):
+    make -C oracle all ref && python tests/golden/make_golden.py
+
+Outputs (all data, no reference source):
+  streams/*.deflate   raw DEFLATE inputs
+  expect/*.bin        expected inflate outputs kept in full (small / lossy cases)
+  manifest.json       per stream: input file, expected output sha256 + size or the
+                      reference's error, and how the vector was produced
+"""
+import hashlib
+import json
+import os
+import sys
+import zlib
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "deflate.hpp_amd"))
+from oracle_bind import Reference, CheckerError  # noqa: E402
+
+import ctypes  # noqa: E402
+
+# the corpus generator lives in libdmx (host-only entry point, no GPU needed)
+import dmx  # noqa: E402
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def raw(d, level, strategy):
+    z = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strategy)
+    return z.compress(d) + z.flush()
+
+
+def main():
+    ref = Reference()
+    sdir = os.path.join(HERE, "streams")
+    edir = os.path.join(HERE, "expect")
+    os.makedirs(sdir, exist_ok=True)
+    os.makedirs(edir, exist_ok=True)
+    man = {"generator": "tests/golden/make_golden.py", "reference": "oracle/_ref (HyperBitGore/deflate.hpp headers, g++ -O2)",
+           "zlib": zlib.ZLIB_RUNTIME_VERSION, "vectors": []}
+
+    def add(name, stream, how, keep_output=False, original=None):
+        path = os.path.join(sdir, name + ".deflate")
+        with open(path, "wb") as f:
+            f.write(stream)
+        ent = {"name": name, "stream": "streams/" + name + ".deflate", "how": how}
+        try:
+            out = ref.decompress(stream)
+            ent.update(ref_ok=True, out_sha256=sha(out), out_len=len(out))
+            if original is not None:
+                ent["equals_original"] = out == original
+            if keep_output:
+                with open(os.path.join(edir, name + ".bin"), "wb") as f:
+                    f.write(out)
+                ent["expect"] = "expect/" + name + ".bin"
+        except CheckerError:
+            ent.update(ref_ok=False, ref_error="Reading bits beyond the alloted buffer size!")
+        man["vectors"].append(ent)
+
+    inputs = {
+        "empty": b"",
+        "one": b"\x41",
+        "tiny.bmp": open(os.path.join(HERE, "tiny.bmp"), "rb").read(),
+        "test.bmp": open(os.path.join(HERE, "test.bmp"), "rb").read(),
+    }
+    for k in ("zeros", "repeat", "random", "text", "mixed", "bmp"):
+        inputs[k + "16k"] = dmx.corpus(k, 16384, offset=65536 * 3 + 123)
+
+    # 1. reference deflate streams (levels 0-3) of tiny.bmp / test.bmp and what the reference
+    #    inflate makes of them (levels 2/3 can be lossy: SURVEY A-1, A-2)
+    for nm in ("tiny.bmp", "test.bmp", "empty"):
+        for lvl in range(4):
+            s = ref.compress(inputs[nm], lvl)
+            add(f"ref_L{lvl}_{nm}", s, f"reference deflate::compress level {lvl}", keep_output=True,
+                original=inputs[nm])
+
+    # 2. zlib raw streams, levels x strategies
+    strategies = {"default": zlib.Z_DEFAULT_STRATEGY, "filtered": zlib.Z_FILTERED,
+                  "huffman": zlib.Z_HUFFMAN_ONLY, "rle": zlib.Z_RLE, "fixed": zlib.Z_FIXED}
+    for nm, d in inputs.items():
+        for lvl in (0, 1, 6, 9):
+            for sn, st in strategies.items():
+                if nm.startswith("random") and (lvl, sn) not in ((1, "default"), (9, "default"), (6, "fixed")):
+                    continue
+                if lvl == 0 and sn != "default":
+                    continue
+                add(f"zlib_{nm}_l{lvl}_{sn}", raw(d, lvl, st), f"zlib {zlib.ZLIB_RUNTIME_VERSION} raw level {lvl} {sn}",
+                    keep_output=len(d) <= 300, original=d)
+
+    # 3. crafted RFC-edge vectors
+    crafted = {"B_control": "0d83050100000040b6f27f040237",
+               "A_cross_boundary": "0d83050100000040b6f27f84c40d",
+               "C_16_after_17": "0d89250100000080b6c2ff1140100027"}
+    for nm, h in crafted.items():
+        add("crafted_" + nm, bytes.fromhex(h), "SURVEY Appendix C", keep_output=True)
+
+    # 4. lenient-reference cases (SURVEY A-10)
+    bad_nlen = bytes([1]) + (100 | (27 << 16)).to_bytes(4, "little") + bytes(range(100))  # test/example.cpp:12-19
+    add("lenient_bad_nlen", bad_nlen, "stored block with NLEN != ~LEN (example.cpp)", keep_output=True)
+    add("lenient_btype3_final", bytes([0x07, 0x00]), "BTYPE 3 final block", keep_output=True)
+    tg = raw(inputs["tiny.bmp"], 6, 0) + b"\xde\xad\xbe\xef" * 4
+    add("lenient_trailing_garbage", tg, "zlib stream + 16 trailing bytes", keep_output=True)
+    # distance larger than the output so far: fixed block, literal 'a', then length 3 dist 4
+    # (copies nothing in the reference, inflate.hpp:268)
+    add("lenient_far_distance", bytes.fromhex("4b046200"), "fixed block: 'a', <3, dist 4>, EOB", keep_output=True)
+    add("fixed_overlap_copy", bytes.fromhex("4b4c024200"), "fixed block: 'ab', <3, dist 2>, EOB", keep_output=True)
+    # truncated streams
+    full = raw(inputs["test.bmp"], 6, 0)
+    add("trunc_test.bmp_half", full[: len(full) // 2], "zlib stream cut in half")
+    add("trunc_tiny_minus1", raw(inputs["tiny.bmp"], 6, 0)[:-1], "zlib stream minus its last byte")
+    # the reference reads data[n] (one byte past the buffer, A-9) before it throws, so on a
+    # stream cut inside its last byte its result depends on memory it does not own: such
+    # vectors are excluded from parity (ours reports DMX_ERR_OVERREAD)
+    for v in man["vectors"]:
+        if v["name"].startswith("trunc_"):
+            v["reference_reads_past_buffer"] = True
+
+    # 5. the reference's own zlib fixtures via decompressZlib (inflate.hpp:352)
+    for nm in ("weird.dat", "zlib.dat"):
+        d = open(os.path.join(HERE, nm), "rb").read()
+        out = ref.decompress_zlib(d)
+        man["vectors"].append({"name": "refzlib_" + nm, "zlib_file": nm, "how": "reference inflate::decompressZlib",
+                               "ref_ok": True, "out_sha256": sha(out), "out_len": len(out),
+                               "equals_zlib": out == zlib.decompress(d)})
+    # 6. the pointer API with a capacity (inflate.hpp:338): cap 1000 on test.bmp
+    s = raw(inputs["test.bmp"], 1, 0)
+    outc = ref.decompress_cap(s, 1000)
+    man["cap_case"] = {"stream": "streams/zlib_test.bmp_l1_default.deflate", "cap": 1000,
+                       "written": len(outc), "sha256": sha(outc)}
+    # 7. corpus checksums for the generator
+    man["corpus_sha256_1MiB"] = {k: sha(dmx.corpus(k, 1 << 20)) for k in ("zeros", "repeat", "random", "text", "mixed")}
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(man, f, indent=1)
+    tot = sum(os.path.getsize(os.path.join(dp, fn)) for dp, _, fns in os.walk(HERE) for fn in fns)
+    print(f"{len(man['vectors'])} vectors, {tot / 1e6:.2f} MB under tests/golden")
+
+
+if __name__ == "__main__":
+    main()
