@@ -24,6 +24,14 @@ __constant__ const uint8_t kPerm[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5,
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// LDS hand-off between the lanes of ONE wavefront (DS instructions of a wave execute in order;
+// this only keeps the compiler from moving LDS accesses across it)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // length 3..258 -> lit/len symbol 257..285
 __device__ __forceinline__ uint32_t len_sym(uint32_t L) {
     if (L <= 10) return 254 + L;

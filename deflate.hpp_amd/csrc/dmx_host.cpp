@@ -229,22 +229,52 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     A.flags = c->flags;
     A.dbg = phase_buf(c, ncand);
     InflateResult r{};
-    for (uint32_t mode = 0; mode < 2; mode++) {
+    // workgroup-per-segment decoder first (segment j lands at j * 32768); if the stream's
+    // segments are not all 32 KiB or one is outside its layout, the wave-per-segment decoder
+    // redoes the stream and places segments by look-back
+    static const int path_env = [] {
+        const char* e = std::getenv("DMX_INFLATE_PATH");
+        return e ? std::atoi(e) : -1;
+    }();
+    uint32_t first = 2;
+    if (path_env == 0 || path_env == 1) first = (uint32_t)path_env;
+    for (uint32_t mode = first; mode < 3; mode = (mode == 2 ? 1 : mode + 1)) {
         A.mode = mode;
-        HIPCHK(hipMemsetAsync(A.status, 0, ncand * 8, st));
-        HIPCHK(hipMemsetAsync(&ds->ticket, 0, 4, st));
-        HIPCHK(launch_inflate_segments(A, st, c->timing ? c->ev[1] : nullptr, c->timing ? c->ev[2] : nullptr));
+        hipEvent_t e0 = c->timing ? c->ev[1] : nullptr, e1 = c->timing ? c->ev[2] : nullptr;
+        if (mode == 2) {
+            HIPCHK(launch_inflate_pj(A, st, e0, e1));
+        } else {
+            HIPCHK(hipMemsetAsync(A.status, 0, ncand * 8, st));
+            HIPCHK(hipMemsetAsync(&ds->ticket, 0, 4, st));
+            HIPCHK(launch_inflate_segments(A, st, e0, e1));
+        }
         HIPCHK(launch_inflate_validate(A, &ds->res, st));
         if (A.dbg) phase_dump(c, "inflate", ncand, st);
         HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        if (r.status != 1) break;  // 1: sizes not uniform, place outputs by look-back
+        if (std::getenv("DMX_RECS")) {  // developer aid: per-candidate outcome of this pass
+            std::vector<SegRecord> h(ncand);
+            (void)hipMemcpy(h.data(), A.recs, ncand * sizeof(SegRecord), hipMemcpyDeviceToHost);
+            uint64_t fl[8] = {0}, shown = 0;
+            for (uint64_t i = 0; i < ncand; i++) {
+                for (int b = 0; b < 8; b++) fl[b] += (h[i].flags >> b) & 1;
+                if ((h[i].flags & ~1u) && shown++ < 8)
+                    std::fprintf(stderr, "dmx: mode %u cand %llu flags %u size %u end %llu next %llu\n", mode,
+                                 (unsigned long long)i, h[i].flags, h[i].out_size,
+                                 (unsigned long long)h[i].end_byte, (unsigned long long)(i + 1 < ncand ? 0 : 0));
+            }
+            std::fprintf(stderr, "dmx: mode %u ncand %llu status %u flags fin %llu data %llu over %llu ovf %llu xref %llu tmo %llu exo %llu\n",
+                         mode, (unsigned long long)ncand, r.status, (unsigned long long)fl[0], (unsigned long long)fl[1],
+                         (unsigned long long)fl[2], (unsigned long long)fl[3], (unsigned long long)fl[4],
+                         (unsigned long long)fl[5], (unsigned long long)fl[6]);
+        }
+        if (r.status != 1 || mode == 1) break;  // 1: sizes not uniform
     }
     c->stats.segments = ncand;
     c->stats.in_bytes = n;
     if (r.status == 0) {
         end_timing(c, st);
-        c->stats.path = A.mode;
+        c->stats.path = A.mode == 2 ? 3 : A.mode;
         c->stats.out_bytes = r.total;
         *total_out = r.total;
         if (dev_out) *dev_out = out;

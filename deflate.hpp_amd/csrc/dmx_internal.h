@@ -38,6 +38,8 @@ enum : uint32_t {
     SEGF_OVERFLOW = 8u,   // output exceeded the LDS window
     SEGF_XREF = 16u,      // back-reference reaches before the segment start
     SEGF_TIMEOUT = 32u,   // look-back spin bound hit
+    SEGF_EXOTIC = 64u,    // layout the workgroup decoder does not take (several blocks, > 32 KiB,
+                          // unsettled split): the wave-per-segment decoder redoes the stream
 };
 
 struct InflateArgs {
@@ -52,7 +54,8 @@ struct InflateArgs {
     unsigned long long* status;  // ncand look-back words (zeroed)
     unsigned int* ticket;        // zeroed
     uint32_t flags;              // DMX_CFG_RFC_STRICT
-    uint32_t mode;               // 0 = speculative uniform segment sizes, 1 = decoupled look-back
+    uint32_t mode;               // 0 = speculative uniform segment sizes, 1 = decoupled look-back,
+                                 // 2 = k_inflate_pj (segment j at j * 32768)
     uint64_t* dbg;               // optional per-segment phase timestamps (DMX_PHASES)
 };
 
@@ -79,6 +82,9 @@ hipError_t launch_scan_u32(const uint32_t* v, uint64_t* offs, uint64_t n, uint64
                            hipStream_t st);
 hipError_t launch_inflate_segments(const InflateArgs& A, hipStream_t st, hipEvent_t ev0,
                                    hipEvent_t ev1);
+// workgroup-per-segment decoder (lane-parallel Huffman decode + pointer-jumping LZ77);
+// segment j lands at j * 32768 (mode 2)
+hipError_t launch_inflate_pj(const InflateArgs& A, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_inflate_validate(const InflateArgs& A, InflateResult* res, hipStream_t st);
 hipError_t launch_inflate_serial(const InflateArgs& A, int count_only, InflateResult* res,
                                  hipStream_t st);

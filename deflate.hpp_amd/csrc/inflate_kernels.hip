@@ -177,7 +177,7 @@ __device__ void build_tree(const uint8_t* lens, int nsym, uint16_t* sorted, Tree
         m.hi[lane] = vlo + vc - 1;
         m.offs[lane] = vo;
     }
-    __syncthreads();
+    wave_sync();
 }
 
 // the reference's lookup rule for key (k, x): the last-inserted code c in [lo_k, hi_k] with
@@ -256,12 +256,12 @@ __device__ void load_fixed(Tables& T) {
     const int lane = lane_id();
     for (int s = lane; s < 288; s += 64) T.llen[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
     if (lane < 32) T.dlen[lane] = 5;
-    __syncthreads();
+    wave_sync();
     build_tree(T.llen, 288, T.lsorted, T.lm);
     build_tree(T.dlen, 32, T.dsorted, T.dm);
     fill_lut<LUT_L>(T.llut, T.lm, T.lsorted);
     fill_lut<LUT_D>(T.dlut, T.dm, T.dsorted);
-    __syncthreads();
+    wave_sync();
 }
 
 // code-length sequence(s) (inflate.hpp:166-206).  Reference mode: called once per sequence,
@@ -310,7 +310,7 @@ __device__ uint32_t read_code_lengths(BitIn& br, const Tables& T, uint8_t* a, ui
         }
         i += rep;
     }
-    __syncthreads();
+    wave_sync();
     if (!rfc) {
         *outa = min(i, 300u);
         *outb = 0;
@@ -326,16 +326,16 @@ __device__ uint32_t read_dynamic_header(BitIn& br, Tables& T, bool rfc) {
     br.ensure(14);
     const uint32_t hlit = br.bits(5), hdist = br.bits(5), hclen = br.bits(4);
     if (lane < 32) T.plen[lane] = 0;
-    __syncthreads();
+    wave_sync();
     for (uint32_t i = 0; i < hclen + 4; i++) {
         const uint32_t v = br.bits(3);
         if (lane == 0) T.plen[kPerm[i]] = (uint8_t)v;
     }
     if (br.over()) return SEGF_OVERREAD;
-    __syncthreads();
+    wave_sync();
     build_tree(T.plen, 19, T.psorted, T.pm);
     fill_prelut(T.plut, T.pm, T.psorted);
-    __syncthreads();
+    wave_sync();
     uint32_t nl, nd, err;
     if (!rfc) {
         uint32_t dummy;
@@ -351,7 +351,7 @@ __device__ uint32_t read_dynamic_header(BitIn& br, Tables& T, bool rfc) {
     build_tree(T.dlen, nd, T.dsorted, T.dm);
     fill_lut<LUT_L>(T.llut, T.lm, T.lsorted);
     fill_lut<LUT_D>(T.dlut, T.dm, T.dsorted);
-    __syncthreads();
+    wave_sync();
     return 0;
 }
 
@@ -529,7 +529,7 @@ __device__ uint32_t inflate_blocks(BitIn& br, Tables& T, Sink& sk, bool rfc, boo
             if (b0 + len > br.end_bytes) return SEGF_OVERREAD;
             if (!sk.stored(br, b0, len)) return sk.err;
             br.seek(br.pos + 8ull * len);
-            __syncthreads();
+            wave_sync();
         } else if (btype == 1) {
             if (!T.fixed_loaded) {
                 load_fixed(T);
@@ -737,17 +737,496 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
     DMX_PHASE(A.dbg, j, 3);
 }
 
+// ---------------------------------------------------------------------------------------
+// k_inflate_pj: one workgroup of PJ_NT lanes per candidate segment.
+//   1. wave 0 reads the block header (wave-uniform, as above) into shared tables;
+//   2. the segment's Huffman bits are split into PJ_NT equal ranges; lane t decodes tokens
+//      from the start of its range (an arbitrary bit: Huffman decoding self-synchronises
+//      within a few tokens) until its path crosses into the next range, keeping the first
+//      PJ_K token boundaries it passed;
+//   3. settle: lane t restarts where lane t-1's path left its range and decodes until it
+//      reaches a boundary of its own first path (merged: the rest of its count is known) --
+//      repeated until every range starts where the previous one ended (normally one round);
+//   4. exclusive scan of the per-lane output counts, then every lane re-decodes its range and
+//      writes P[x] for each output byte x: 0x8000 | byte for a literal, or the position the
+//      byte is copied from (LZ77 copy out[o + i] = out[o - d + (i mod d)], always < x);
+//   5. pointer jumping P[x] = P[P[x]] until every entry is a literal (chains halve per round);
+//   6. the low bytes of P go to HBM with 16-byte stores at the segment's slot j * 32768.
+// Everything else -- several blocks in one segment, stored + Huffman mixes, an output above
+// 32 KiB, a split that does not settle -- is flagged SEGF_EXOTIC and the whole stream is
+// redone by k_inflate_segments, so results never depend on this path's coverage.
+// ---------------------------------------------------------------------------------------
+constexpr int PJ_NT = 256;
+constexpr int PJ_K = 8;
+constexpr uint32_t PJ_LIT = 0x8000u;
+constexpr uint32_t PJ_MAXBITS = 1u << 20;  // Huffman bits of one segment (32 KiB * 15 < 2^19)
+constexpr int PJ_ROUNDS = 16;
+constexpr uint32_t PJ_MINBITS = 256;
+
+// LSB-first bit reader whose position differs per lane: plain (vector) loads
+struct LBits {
+    const uint32_t* w;
+    uint64_t nwords, end_bytes;
+    uint64_t pos;
+    uint64_t buf;
+    uint32_t cnt;
+    uint64_t wi;
+    uint32_t q0, q1;
+
+    __device__ void init(const uint32_t* words, uint64_t misalign, uint64_t n) {
+        w = words;
+        end_bytes = misalign + n;
+        nwords = (end_bytes + 3) / 4;
+    }
+    __device__ uint32_t raw(uint64_t i) const { return w[i < nwords ? i : nwords - 1]; }
+    __device__ uint32_t mask(uint64_t i) const {
+        if (i >= nwords) return 0u;
+        const uint64_t lim = end_bytes - 4 * i;
+        return lim >= 4 ? 0xFFFFFFFFu : ((1u << (8 * lim)) - 1u);
+    }
+    __device__ void refill() {
+        if (cnt <= 32) {
+            buf |= (uint64_t)(q0 & mask(wi)) << cnt;
+            cnt += 32;
+            wi++;
+            q0 = q1;
+            q1 = raw(wi + 1);
+        }
+    }
+    __device__ void seek(uint64_t bitpos) {
+        pos = bitpos;
+        const uint64_t i = bitpos >> 5;
+        buf = (uint64_t)((raw(i) & mask(i)) >> (bitpos & 31));
+        cnt = 32 - (uint32_t)(bitpos & 31);
+        wi = i + 1;
+        q0 = raw(wi);
+        q1 = raw(wi + 1);
+        refill();
+    }
+    __device__ void ensure(uint32_t k) {
+        if (cnt < k) refill();
+    }
+    __device__ uint32_t peek(uint32_t k) const { return (uint32_t)buf & ((1u << k) - 1u); }
+    __device__ void consume(uint32_t k) {
+        buf >>= k;
+        cnt -= k;
+        pos += k;
+    }
+    __device__ uint32_t bits(uint32_t k) {
+        ensure(k);
+        const uint32_t v = peek(k);
+        consume(k);
+        return v;
+    }
+};
+
+enum : uint32_t { TK_LIT = 0, TK_MATCH = 1, TK_EOB = 2, TK_BAD = 3 };
+
+// one token of decompressHuffmanBlock (inflate.hpp:226-275): a literal (*a = byte), a match
+// (*a = length, *d = distance; 0 for symbols 286+ / 30+), the end of block, or no code
+__device__ __forceinline__ uint32_t pj_token(LBits& br, const Tables& T, uint32_t* a, uint32_t* d) {
+    br.ensure(20);
+    uint32_t v = br.peek(15);
+    uint32_t e = T.llut[v & ((1u << LUT_L) - 1)];
+    uint32_t sym, len;
+    if (e) {
+        sym = e & 511;
+        len = e >> 9;
+    } else if (!slow_decode(T.lm, T.lsorted, v, LUT_L + 1, &sym, &len)) {
+        return TK_BAD;
+    }
+    br.consume(len);
+    if (sym < 256) {
+        *a = sym;
+        return TK_LIT;
+    }
+    if (sym == 256) return TK_EOB;
+    uint32_t L = 0;
+    if (sym <= 285) {
+        const uint32_t ex = len_extra(sym);
+        L = len_base(sym) + (ex ? br.bits(ex) : 0);
+    }
+    br.ensure(28);
+    v = br.peek(15);
+    e = T.dlut[v & ((1u << LUT_D) - 1)];
+    uint32_t ds, dl;
+    if (e) {
+        ds = e & 511;
+        dl = e >> 9;
+    } else if (!slow_decode(T.dm, T.dsorted, v, LUT_D + 1, &ds, &dl)) {
+        return TK_BAD;
+    }
+    br.consume(dl);
+    uint32_t dist = 0;
+    if (ds < 30) {
+        const uint32_t ex = dist_extra(ds);
+        dist = dist_base(ds) + (ex ? br.bits(ex) : 0);
+    }
+    *a = L;
+    *d = dist;
+    return TK_MATCH;
+}
+
+__device__ __forceinline__ uint32_t tok_bytes(uint32_t k, uint32_t a, uint32_t d) {
+    return k == TK_LIT ? 1u : (k == TK_MATCH && a && d) ? a : 0u;
+}
+
+struct PjSmem {
+    uint16_t P[SEG_CAP];
+    Tables T;
+    uint32_t endp[PJ_NT];   // where lane t's current path crossed into range t+1 (relative)
+    uint32_t part[PJ_NT / 64];
+    uint64_t hs;            // absolute bit of the first Huffman token
+    uint32_t hlen;          // bits split among the lanes
+    uint32_t kind;          // 0 Huffman, 1 stored, 2 done (empty segment / error)
+    uint32_t bfinal;
+    uint32_t err;
+    uint32_t slen;
+    uint64_t sb0;
+    uint32_t tew[PJ_NT / 64];  // per wave: first lane whose path ends (EOB / no code)
+    uint32_t total;
+    uint64_t end_byte;
+};
+
+__global__ __launch_bounds__(PJ_NT) void k_inflate_pj(InflateArgs A) {
+    __shared__ __attribute__((aligned(16))) PjSmem S;
+    const int t = threadIdx.x;
+    const int wave = t >> 6;
+    const uint64_t j = blockIdx.x;
+    const bool rfc = (A.flags & DMX_CFG_RFC_STRICT) != 0;
+    const uint64_t obase = j * (uint64_t)SEG_CAP;
+    DMX_PHASE(A.dbg, j, 0);
+
+    // ---- 1. block header (wave 0) ----
+    if (wave == 0) {
+        BitIn br;
+        br.init(A.in_words, A.misalign, A.n);
+        br.seek((A.misalign + A.cands[j]) * 8);
+        br.ensure(3);
+        const uint32_t bfinal = br.bits(1);
+        const uint32_t btype = br.bits(2);
+        uint32_t kind = 2, err = 0;
+        uint64_t end_byte = 0, sb0 = 0;
+        uint32_t slen = 0, hlen = 0;
+        if (br.over()) {
+            err = SEGF_OVERREAD;
+        } else if (btype == 0) {
+            br.align();
+            br.ensure(32);
+            const uint32_t len = br.bits(16);
+            const uint32_t nlen = br.bits(16);
+            sb0 = br.pos >> 3;
+            if (br.over()) {
+                err = SEGF_OVERREAD;
+            } else if (!bfinal && len == 0 && nlen == 0xFFFF) {
+                end_byte = sb0;  // the segment is just the marker
+            } else if (sb0 + len > br.end_bytes) {
+                err = SEGF_OVERREAD;
+            } else if (bfinal) {
+                kind = 1;
+                slen = len;
+                end_byte = sb0 + len;
+            } else {
+                // the next block must be the marker: 000 + 5 pad bits, 00 00 FF FF
+                const uint64_t m = sb0 + len;
+                if (m + 5 <= br.end_bytes && (br.byte_at(m) & 7) == 0 && br.byte_at(m + 1) == 0 &&
+                    br.byte_at(m + 2) == 0 && br.byte_at(m + 3) == 0xFF && br.byte_at(m + 4) == 0xFF) {
+                    kind = 1;
+                    slen = len;
+                    end_byte = m + 5;
+                } else {
+                    err = SEGF_EXOTIC;
+                }
+            }
+        } else if (btype == 3) {
+            err = SEGF_EXOTIC;
+        } else {
+            if (btype == 1) {
+                load_fixed(S.T);
+            } else {
+                err = read_dynamic_header(br, S.T, rfc);
+            }
+            if (!err) {
+                const uint64_t hs = br.pos;
+                const uint64_t he = j + 1 < A.ncand ? (A.misalign + A.cands[j + 1] - 4) * 8 - 3
+                                                    : (A.misalign + A.n) * 8;
+                if (he <= hs || he - hs > PJ_MAXBITS) {
+                    err = SEGF_EXOTIC;
+                } else {
+                    kind = 0;
+                    hlen = (uint32_t)(he - hs);
+                }
+                if (lane_id() == 0) S.hs = hs;
+            }
+        }
+        if (lane_id() == 0) {
+            S.kind = err ? 2 : kind;
+            S.err = err;
+            S.bfinal = bfinal;
+            S.end_byte = end_byte;
+            S.slen = slen;
+            S.sb0 = sb0;
+            S.hlen = hlen;
+            S.total = kind == 1 ? slen : 0;
+        }
+    }
+    __syncthreads();
+    DMX_PHASE(A.dbg, j, 1);
+    const uint32_t kind = S.kind;
+
+    if (kind == 1) {
+        // ---- stored segment: bytes straight to the slot ----
+        const uint32_t len = S.slen;
+        if (len > SEG_CAP) {
+            if (t == 0) S.err = SEGF_OVERFLOW;
+        } else {
+            const uint64_t b0 = S.sb0;
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(A.in_words);
+            for (uint32_t i = t; i < len; i += PJ_NT)
+                if (obase + i < A.cap) A.out[obase + i] = src[b0 + i];
+        }
+    } else if (kind == 0) {
+        // ---- 2. first pass over the lane ranges ----
+        const uint64_t hs = S.hs;
+        const uint32_t hlen = S.hlen;
+        // ranges of at least PJ_MINBITS (a few dozen tokens) so that a path started at an
+        // arbitrary bit re-synchronises inside its own range; surplus lanes stay empty
+        const uint32_t nl = max(1u, min((uint32_t)PJ_NT, hlen / PJ_MINBITS));
+        const uint32_t sp = t < (int)nl ? (uint32_t)(((uint64_t)hlen * t) / nl) : hlen;
+        const uint32_t sp1 = t + 1 < (int)nl ? (uint32_t)(((uint64_t)hlen * (t + 1)) / nl) : hlen;
+        LBits br;
+        br.init(A.in_words, A.misalign, A.n);
+        uint32_t q[PJ_K], c[PJ_K];
+#pragma unroll
+        for (int k = 0; k < PJ_K; k++) q[k] = c[k] = 0xFFFFFFFFu;
+        uint32_t e1, cnt1 = 0, st1 = 0, nb = 0;
+        {
+            br.seek(hs + sp);
+            uint32_t p = sp;
+            while (p < sp1) {
+                uint32_t a, d;
+                const uint32_t k = pj_token(br, S.T, &a, &d);
+                if (k == TK_BAD) { st1 = 2; break; }
+                p = (uint32_t)(br.pos - hs);
+                if (k == TK_EOB) { st1 = 1; break; }
+                cnt1 += tok_bytes(k, a, d);
+                if (nb < PJ_K) {
+#pragma unroll
+                    for (int m = 0; m < PJ_K; m++)
+                        if (m == (int)nb) { q[m] = p; c[m] = cnt1; }
+                    nb++;
+                }
+            }
+            e1 = p;
+        }
+        // ---- 3. settle the range starts ----
+        // per round: [publish end, first-ending lane per wave] | read: te, want | or-barrier |
+        // redo | barrier.  Every shared word is written and read on opposite sides of a barrier.
+        uint32_t s = sp, e = e1, cnt = cnt1, st = st1;
+        uint32_t te = PJ_NT;
+        bool settled = false;
+        for (int round = 0; round <= PJ_ROUNDS; round++) {
+            S.endp[t] = e;
+            {
+                const uint64_t bm = __ballot(st != 0);
+                if ((t & 63) == 0) S.tew[wave] = bm ? (uint32_t)(wave * 64 + __ffsll((long long)bm) - 1) : PJ_NT;
+            }
+            __syncthreads();
+            te = min(min(S.tew[0], S.tew[1]), min(S.tew[2], S.tew[3]));
+            const uint32_t want = t == 0 ? 0 : S.endp[t - 1];
+            const bool redo = t > 0 && t <= (int)te && want != s;
+            if (!__syncthreads_or(redo)) {
+                settled = true;
+                break;
+            }
+            if (round == PJ_ROUNDS) break;
+            if (redo) {
+                // decode from the true start until the path meets a boundary of the first pass
+                s = want;
+                uint32_t p = want, acc = 0, stn = 0;
+                bool merged = false;
+                br.seek(hs + p);
+                for (;;) {
+                    if (p == sp) {
+                        merged = true;
+                        cnt = acc + cnt1;
+                    }
+#pragma unroll
+                    for (int m = 0; m < PJ_K; m++)
+                        if (!merged && p == q[m]) {
+                            merged = true;
+                            cnt = acc + cnt1 - c[m];
+                        }
+                    if (merged || p >= sp1) break;
+                    uint32_t a, d;
+                    const uint32_t k = pj_token(br, S.T, &a, &d);
+                    if (k == TK_BAD) { stn = 2; break; }
+                    p = (uint32_t)(br.pos - hs);
+                    if (k == TK_EOB) { stn = 1; break; }
+                    acc += tok_bytes(k, a, d);
+                }
+                if (merged) {
+                    e = e1;
+                    st = st1;
+                } else {
+                    e = p;
+                    cnt = acc;
+                    st = stn;
+                }
+            }
+            __syncthreads();
+        }
+        if (t == 0 && !settled) S.err |= SEGF_EXOTIC;
+        if (t == (int)te) {
+            if (st == 2) {
+                S.err |= SEGF_ERR_DATA;
+            } else {
+                // end of block: BFINAL ends the stream, else the marker block must follow
+                const uint64_t pe = hs + e;
+                if (S.bfinal) {
+                    S.end_byte = (pe + 7) >> 3;
+                } else {
+                    br.seek(pe);
+                    const uint32_t h3 = br.bits(3);
+                    const uint64_t m = (pe + 3 + 7) >> 3;
+                    const uint8_t* src = reinterpret_cast<const uint8_t*>(A.in_words);
+                    if (h3 == 0 && m + 4 <= A.misalign + A.n && src[m] == 0 && src[m + 1] == 0 &&
+                        src[m + 2] == 0xFF && src[m + 3] == 0xFF)
+                        S.end_byte = m + 4;
+                    else
+                        S.err |= SEGF_EXOTIC;
+                }
+            }
+        }
+        // no end of block before the split end: several blocks, or the next candidate is not
+        // this segment's end
+        if (te >= PJ_NT && t == 0) S.err |= SEGF_EXOTIC;
+        const uint32_t mycnt = t <= (int)te ? cnt : 0u;
+        // ---- 4. scan + emit ----
+        const uint32_t inc = wave_incl_scan(mycnt);
+        if ((t & 63) == 63) S.part[wave] = inc;
+        __syncthreads();
+        uint32_t base = 0;
+        for (int w = 0; w < wave; w++) base += S.part[w];
+        const uint32_t total = S.part[0] + S.part[1] + S.part[2] + S.part[3];
+        if (t == 0) {
+            S.total = total;
+            if (total > SEG_CAP) S.err |= SEGF_OVERFLOW;
+        }
+        __syncthreads();
+        if (!S.err && t <= (int)te && mycnt) {
+            uint32_t o = base + inc - mycnt;
+            br.seek(hs + s);
+            uint32_t p = s;
+            uint32_t bad = 0;
+            while (p < sp1) {
+                uint32_t a, d;
+                const uint32_t k = pj_token(br, S.T, &a, &d);
+                p = (uint32_t)(br.pos - hs);
+                if (k == TK_LIT) {
+                    S.P[o++] = (uint16_t)(PJ_LIT | a);
+                } else if (k == TK_MATCH) {
+                    if (!a || !d) continue;
+                    if (d > o) {  // before the segment: cross-segment or stream-start reference
+                        bad = j == 0 ? SEGF_EXOTIC : SEGF_XREF;
+                        break;
+                    }
+                    uint32_t src = o - d, r = 0;
+                    for (uint32_t i = 0; i < a; i++) {
+                        S.P[o + i] = (uint16_t)(src + r);
+                        if (++r == d) r = 0;
+                    }
+                    o += a;
+                } else {
+                    break;
+                }
+            }
+            if (bad) atomicOr(&S.err, bad);
+        }
+        __syncthreads();
+        DMX_PHASE(A.dbg, j, 2);
+        // ---- 5. pointer jumping ----
+        if (!S.err) {
+            uint32_t* P2 = reinterpret_cast<uint32_t*>(S.P);
+            const uint32_t npair = (total + 1) / 2;
+            bool open = true;
+            for (int round = 0; round < 24 && open; round++) {
+                uint32_t any = 0;
+                for (uint32_t i = t; i < npair; i += PJ_NT) {
+                    const uint32_t v = P2[i];
+                    uint32_t lo = v & 0xFFFF, hi = v >> 16;
+                    const bool plo = !(lo & PJ_LIT), phi = !(hi & PJ_LIT) && 2 * i + 1 < total;
+                    if (plo | phi) {
+                        if (plo) lo = S.P[lo];
+                        if (phi) hi = S.P[hi];
+                        if (phi) S.P[2 * i + 1] = (uint16_t)hi;
+                        if (plo) S.P[2 * i] = (uint16_t)lo;
+                        any |= (plo && !(lo & PJ_LIT)) || (phi && !(hi & PJ_LIT));
+                    }
+                }
+                open = __syncthreads_or(any) != 0;
+            }
+            if (open && t == 0) S.err |= SEGF_EXOTIC;
+            __syncthreads();
+        }
+        DMX_PHASE(A.dbg, j, 3);
+        // ---- 6. low bytes of P to the slot ----
+        if (!S.err) {
+            const uint32_t nb16 = total / 16;
+            uint8_t* dst = A.out + obase;
+            const bool vec = (((uintptr_t)dst) & 15) == 0 && obase + total <= A.cap;
+            const uint4* P4 = reinterpret_cast<const uint4*>(S.P);
+            if (vec) {
+                for (uint32_t i = t; i < nb16; i += PJ_NT) {
+                    const uint4 a = P4[2 * i], b = P4[2 * i + 1];
+                    uint4 o;
+                    o.x = __builtin_amdgcn_perm(a.y, a.x, 0x06040200u);
+                    o.y = __builtin_amdgcn_perm(a.w, a.z, 0x06040200u);
+                    o.z = __builtin_amdgcn_perm(b.y, b.x, 0x06040200u);
+                    o.w = __builtin_amdgcn_perm(b.w, b.z, 0x06040200u);
+                    reinterpret_cast<uint4*>(dst)[i] = o;
+                }
+                for (uint32_t i = nb16 * 16 + t; i < total; i += PJ_NT) dst[i] = (uint8_t)S.P[i];
+            } else {
+                for (uint32_t i = t; i < total; i += PJ_NT)
+                    if (obase + i < A.cap) dst[i] = (uint8_t)S.P[i];
+            }
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        const uint32_t err = S.err;
+        A.recs[j].end_byte = S.end_byte - A.misalign;
+        A.recs[j].out_size = err ? 0 : S.total;
+        A.recs[j].flags = err | (S.bfinal && !err ? SEGF_FINAL : 0u);
+        A.recs[j].offset = obase;
+    }
+    DMX_PHASE(A.dbg, j, 4);
+}
+
+hipError_t launch_inflate_pj(const InflateArgs& A, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+    if (ev0) (void)hipEventRecord(ev0, st);
+    hipLaunchKernelGGL(k_inflate_pj, dim3((uint32_t)A.ncand), dim3(PJ_NT), 0, st, A);
+    if (ev1) (void)hipEventRecord(ev1, st);
+    return hipGetLastError();
+}
+
 // Candidate chain check.  Valid iff, up to the first BFINAL segment k, every segment decoded
 // without error and ended exactly at the next candidate.  Speculative mode additionally needs
 // every segment before k to have segment 0's size (else status 1: re-run with look-back).
 __global__ __launch_bounds__(1024) void k_inflate_validate(InflateArgs A, InflateResult* res) {
-    __shared__ unsigned long long kmin, bmin, umin;
+    __shared__ unsigned long long kmin, bmin, umin, xmin;
     const int t = threadIdx.x;
-    if (t == 0) { kmin = ~0ull; bmin = ~0ull; umin = ~0ull; }
+    if (t == 0) { kmin = ~0ull; bmin = ~0ull; umin = ~0ull; xmin = ~0ull; }
     __syncthreads();
-    const uint32_t size0 = A.recs[0].out_size;
+    // mode 2 (k_inflate_lanes) placed segment j at j * 32768
+    const uint32_t size0 = A.mode == 2 ? 32768u : A.recs[0].out_size;
     for (uint64_t j = t; j < A.ncand; j += 1024) {
         const SegRecord r = A.recs[j];
+        if (r.flags & SEGF_EXOTIC) {  // k_inflate_pj declined this candidate
+            atomicMin(&xmin, (unsigned long long)j);
+            continue;
+        }
         const bool fin = (r.flags & SEGF_FINAL) != 0;
         const bool err = (r.flags & ~SEGF_FINAL) != 0;
         const bool chain = (j + 1 < A.ncand) && r.end_byte == A.cands[j + 1];
@@ -759,8 +1238,11 @@ __global__ __launch_bounds__(1024) void k_inflate_validate(InflateArgs A, Inflat
     if (t == 0) {
         const uint64_t k = kmin;
         res->fin_index = (uint32_t)k;
-        if (k < A.ncand && bmin > k) {
-            if (A.mode == 0 && umin < k) {
+        if (xmin < A.ncand) {
+            res->status = 1;
+            res->total = 0;
+        } else if (k < A.ncand && bmin > k) {
+            if (A.mode != 1 && umin < k) {
                 res->status = 1;
                 res->total = 0;
             } else {

@@ -107,7 +107,8 @@ typedef struct dmx_stats {
     uint64_t in_bytes;
     uint64_t out_bytes;
     uint32_t path;          /* inflate: 0 = segment-parallel (speculative offsets),
-                               1 = segment-parallel (look-back offsets), 2 = serial path     */
+                               1 = segment-parallel (look-back offsets), 2 = serial path,
+                               3 = workgroup-per-segment decoder (32 KiB slots)             */
     uint32_t reserved;
 } dmx_stats;
 
