@@ -92,7 +92,8 @@ void phase_dump(dmx_ctx* c, const char* kernel, uint64_t nidx, hipStream_t st) {
     std::vector<uint64_t> h(nidx * kPhaseSlots);
     (void)hipStreamSynchronize(st);
     (void)hipMemcpy(h.data(), c->dbg.p, h.size() * 8, hipMemcpyDeviceToHost);
-    double sum[kPhaseSlots] = {0};
+    double sum[kPhaseSlots] = {0}, xsum[kPhaseSlots] = {0};
+    uint64_t xcnt[kPhaseSlots] = {0};
     uint64_t cnt[kPhaseSlots] = {0};
     const bool inf = std::string(kernel) == "inflate";
     for (uint64_t i = 0; i < nidx; i++) {
@@ -105,7 +106,9 @@ void phase_dump(dmx_ctx* c, const char* kernel, uint64_t nidx, hipStream_t st) {
             cnt[k]++;
             prev = r[k];
         }
-        if (inf) { sum[15] += (double)r[8]; cnt[15]++; }
+        if (inf) {  // slots 8..10: raw per-segment values (header cycles / settle and jump rounds)
+            for (int k = 8; k < 16; k++) { xsum[k] += (double)r[k]; xcnt[k]++; }
+        }
         if (!inf && r[12] && r[13] && r[3] && r[14]) {  // Huffman build sub-phases, match rounds
             sum[12] += (double)(r[12] - r[3]); cnt[12]++;
             sum[13] += (double)(r[13] - r[12]); cnt[13]++;
@@ -116,6 +119,8 @@ void phase_dump(dmx_ctx* c, const char* kernel, uint64_t nidx, hipStream_t st) {
     if (!f) return;
     std::fprintf(f, "%s %llu", kernel, (unsigned long long)nidx);
     for (int k = 1; k < kPhaseSlots; k++) std::fprintf(f, " p%d=%.0f", k, cnt[k] ? sum[k] / cnt[k] : 0.0);
+    if (inf)
+        for (int k = 8; k < kPhaseSlots; k++) std::fprintf(f, " x%d=%.1f", k, xcnt[k] ? xsum[k] / xcnt[k] : 0.0);
     std::fprintf(f, "\n");
     std::fclose(f);
 }
@@ -229,20 +234,38 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     A.flags = c->flags;
     A.dbg = phase_buf(c, ncand);
     InflateResult r{};
-    // workgroup-per-segment decoder first (segment j lands at j * 32768); if the stream's
-    // segments are not all 32 KiB or one is outside its layout, the wave-per-segment decoder
-    // redoes the stream and places segments by look-back
+    // Plan: the workgroup-per-segment decoder with the context's segment size (segment j
+    // lands at j * seg), then with the other size, then the wave-per-segment decoder, which
+    // places segments of any size <= 32 KiB by look-back; each pass runs only if the previous
+    // one reported status 1 (a segment outside its layout or sizes not uniform).
     static const int path_env = [] {
         const char* e = std::getenv("DMX_INFLATE_PATH");
         return e ? std::atoi(e) : -1;
     }();
-    uint32_t first = 2;
-    if (path_env == 0 || path_env == 1) first = (uint32_t)path_env;
-    for (uint32_t mode = first; mode < 3; mode = (mode == 2 ? 1 : mode + 1)) {
+    // High-ratio streams (few compressed bytes per candidate: long matches, few tokens) go to
+    // the wave decoder first; the others to the workgroup decoder.
+    const bool few_bits = n / ncand < 4096;
+    uint32_t plan[6][2];
+    int np = 0;
+    if (path_env == 0 || path_env == 1) {
+        plan[np][0] = (uint32_t)path_env, plan[np][1] = 0, np++;
+    } else if (few_bits && path_env != 2) {
+        plan[np][0] = 0, plan[np][1] = 0, np++;
+    } else {
+        plan[np][0] = 2, plan[np][1] = c->seg, np++;
+        plan[np][0] = 3, plan[np][1] = c->seg, np++;  // patch the declined candidates
+        plan[np][0] = 2, plan[np][1] = c->seg == 32768 ? 16384u : 32768u, np++;
+        plan[np][0] = 3, plan[np][1] = c->seg == 32768 ? 16384u : 32768u, np++;
+    }
+    if (path_env != 1) plan[np][0] = 1, plan[np][1] = 0, np++;
+    for (int pi = 0; pi < np; pi++) {
+        const uint32_t mode = plan[pi][0];
+        if (mode == 3 && (r.exotic == 0 || r.exotic > ncand / 8)) continue;  // nothing / too many
         A.mode = mode;
+        A.slot = plan[pi][1];
         hipEvent_t e0 = c->timing ? c->ev[1] : nullptr, e1 = c->timing ? c->ev[2] : nullptr;
         if (mode == 2) {
-            HIPCHK(launch_inflate_pj(A, st, e0, e1));
+            HIPCHK(launch_inflate_pj(A, A.slot, st, e0, e1));
         } else {
             HIPCHK(hipMemsetAsync(A.status, 0, ncand * 8, st));
             HIPCHK(hipMemsetAsync(&ds->ticket, 0, 4, st));
@@ -268,13 +291,13 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
                          (unsigned long long)fl[2], (unsigned long long)fl[3], (unsigned long long)fl[4],
                          (unsigned long long)fl[5], (unsigned long long)fl[6]);
         }
-        if (r.status != 1 || mode == 1) break;  // 1: sizes not uniform
+        if (r.status != 1) break;  // 1: not this layout
     }
     c->stats.segments = ncand;
     c->stats.in_bytes = n;
     if (r.status == 0) {
         end_timing(c, st);
-        c->stats.path = A.mode == 2 ? 3 : A.mode;
+        c->stats.path = A.mode >= 2 ? 3 : A.mode;
         c->stats.out_bytes = r.total;
         *total_out = r.total;
         if (dev_out) *dev_out = out;

@@ -55,7 +55,10 @@ struct InflateArgs {
     unsigned int* ticket;        // zeroed
     uint32_t flags;              // DMX_CFG_RFC_STRICT
     uint32_t mode;               // 0 = speculative uniform segment sizes, 1 = decoupled look-back,
-                                 // 2 = k_inflate_pj (segment j at j * 32768)
+                                 // 2 = k_inflate_pj (segment j at j * slot),
+                                 // 3 = k_inflate_segments redoing only SEGF_EXOTIC candidates
+                                 //     of a mode-2 pass, at the same slots
+    uint32_t slot;               // mode 2: segment bytes (16384 or 32768)
     uint64_t* dbg;               // optional per-segment phase timestamps (DMX_PHASES)
 };
 
@@ -70,6 +73,7 @@ struct InflateResult {
     uint64_t total;   // decoded bytes
     int32_t status;   // fast path: 0 ok, 1 re-run with look-back, 2 serial; serial: 0 / DMX_ERR_*
     uint32_t fin_index;
+    uint64_t exotic;  // candidates flagged SEGF_EXOTIC by the pass
 };
 
 hipError_t launch_marker_count(const uint32_t* in_words, uint64_t misalign, uint64_t n,
@@ -84,7 +88,8 @@ hipError_t launch_inflate_segments(const InflateArgs& A, hipStream_t st, hipEven
                                    hipEvent_t ev1);
 // workgroup-per-segment decoder (lane-parallel Huffman decode + pointer-jumping LZ77);
 // segment j lands at j * 32768 (mode 2)
-hipError_t launch_inflate_pj(const InflateArgs& A, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_inflate_pj(const InflateArgs& A, uint32_t seg, hipStream_t st, hipEvent_t ev0,
+                             hipEvent_t ev1);
 hipError_t launch_inflate_validate(const InflateArgs& A, InflateResult* res, hipStream_t st);
 hipError_t launch_inflate_serial(const InflateArgs& A, int count_only, InflateResult* res,
                                  hipStream_t st);

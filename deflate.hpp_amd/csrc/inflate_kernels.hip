@@ -268,7 +268,8 @@ __device__ void load_fixed(Tables& T) {
 // last literal length starts at 0, a repeat may overshoot (entries keep their index as the
 // symbol value).  RFC mode: one call over both sequences (nb > 0).  Returns SEGF_* or 0 and
 // the number of entries written to a (and b).
-__device__ uint32_t read_code_lengths(BitIn& br, const Tables& T, uint8_t* a, uint32_t na,
+template <class BR>
+__device__ uint32_t read_code_lengths(BR& br, const Tables& T, uint8_t* a, uint32_t na,
                                       uint8_t* b, uint32_t nb, bool rfc, uint32_t* outa,
                                       uint32_t* outb) {
     const int lane = lane_id();
@@ -321,7 +322,8 @@ __device__ uint32_t read_code_lengths(BitIn& br, const Tables& T, uint8_t* a, ui
     return 0;
 }
 
-__device__ uint32_t read_dynamic_header(BitIn& br, Tables& T, bool rfc) {
+template <class BR>
+__device__ uint32_t read_dynamic_header(BR& br, Tables& T, bool rfc, bool fill = true) {
     const int lane = lane_id();
     br.ensure(14);
     const uint32_t hlit = br.bits(5), hdist = br.bits(5), hclen = br.bits(4);
@@ -349,9 +351,201 @@ __device__ uint32_t read_dynamic_header(BitIn& br, Tables& T, bool rfc) {
     }
     build_tree(T.llen, nl, T.lsorted, T.lm);
     build_tree(T.dlen, nd, T.dsorted, T.dm);
-    fill_lut<LUT_L>(T.llut, T.lm, T.lsorted);
-    fill_lut<LUT_D>(T.dlut, T.dm, T.dsorted);
+    if (fill) {
+        fill_lut<LUT_L>(T.llut, T.lm, T.lsorted);
+        fill_lut<LUT_D>(T.dlut, T.dm, T.dsorted);
+    }
     wave_sync();
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Wave-level dynamic header reader (inflate.hpp:136-224 semantics, as read_code_lengths
+// above).  The 64 lanes hold a 2048-bit window of the stream, one word each; every step
+// decodes the precode symbol (and its repeat bits) at 64 consecutive bit offsets at once, and
+// the true symbol chain is then walked with v_readlane -- a few scalar instructions per code
+// length instead of a dependent bit-reader refill + table lookup.
+// ---------------------------------------------------------------------------------------
+struct GlobalWords {  // stream words in HBM, masked at the stream end
+    const uint32_t* w;
+    uint64_t nwords, end_bytes;
+    __device__ uint32_t word(uint64_t i) const {
+        if (i >= nwords) return 0u;
+        const uint64_t lim = end_bytes - 4 * i;
+        const uint32_t v = w[i];
+        return lim >= 4 ? v : v & ((1u << (8 * lim)) - 1u);
+    }
+};
+struct StagedWords {  // words [ws, ws + nw) staged in LDS (already masked)
+    const uint32_t* w;
+    uint64_t ws, nw;
+    __device__ uint32_t word(uint64_t i) const { return (i >= ws && i < ws + nw) ? w[i - ws] : 0u; }
+};
+
+// 32 bits at window bit b; every lane passes its own b (all lanes must be active)
+__device__ __forceinline__ uint32_t win_bits(uint32_t win, uint32_t b) {
+    const int i = (int)(b >> 5);
+    const uint32_t lo = __shfl(win, i), hi = __shfl(win, i + 1);
+    return __builtin_amdgcn_alignbit(hi, lo, b & 31);
+}
+__device__ __forceinline__ uint32_t win_bits_u(uint32_t win, uint32_t b) {  // b wave-uniform
+    const int i = (int)(b >> 5);
+    const uint32_t lo = __builtin_amdgcn_readlane(win, i), hi = __builtin_amdgcn_readlane(win, i + 1);
+    return __builtin_amdgcn_alignbit(hi, lo, b & 31);
+}
+
+template <class Src>
+__device__ uint32_t fast_header(const Src& src, uint64_t* pos_io, uint64_t end_bits, Tables& T,
+                                bool rfc, bool fill, uint64_t* stamps = nullptr) {
+    const int lane = lane_id();
+    uint64_t t0 = stamps ? __builtin_amdgcn_s_memtime() : 0;
+#define FH_STAMP(k)                                              \
+    if (stamps) {                                                \
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();        \
+        stamps[k] += t1 - t0;                                    \
+        t0 = t1;                                                 \
+    }
+    uint64_t w0 = *pos_io >> 5;
+    uint32_t rp = (uint32_t)(*pos_io & 31);
+    uint32_t win = src.word(w0 + lane);
+    const uint32_t h = win_bits_u(win, rp);
+    const uint32_t hlit = h & 31, hdist = (h >> 5) & 31, hclen = (h >> 10) & 15;
+    rp += 14;
+    const uint32_t pv = win_bits(win, rp + 3 * (uint32_t)(lane < 19 ? lane : 0)) & 7;
+    if (lane < 32) T.plen[lane] = 0;
+    wave_sync();
+    if (lane < (int)hclen + 4) T.plen[kPerm[lane]] = (uint8_t)pv;
+    rp += 3 * (hclen + 4);
+    if (w0 * 32 + rp > end_bits) return SEGF_OVERREAD;
+    wave_sync();
+    build_tree(T.plen, 19, T.psorted, T.pm);
+    fill_prelut(T.plut, T.pm, T.psorted);
+    wave_sync();
+    FH_STAMP(0);
+    const uint32_t na = 257 + hlit, nd = 1 + hdist;
+    const uint32_t cap = rfc ? na + nd : 300;
+    uint32_t target = rfc ? na + nd : na;
+    uint32_t seq = 0, i = 0, last = 0, nl = 0, ndd = 0;
+    for (;;) {
+        if (rp + 64 + 46 > 2048) {  // keep 64 offsets + 46 bits of lookahead in the window
+            w0 += rp >> 5;
+            rp &= 31;
+            win = src.word(w0 + lane);
+        }
+        const uint32_t v = win_bits(win, rp + lane);
+        const uint32_t e = T.plut[v & 127];
+        const uint32_t sym = e & 511, len = e >> 9;
+        const uint32_t ex = sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u;
+        const uint32_t xv = (v >> len) & ((1u << ex) - 1u);
+        const uint32_t rep_l = sym < 16 ? 1u : sym == 18 ? 11u + xv : 3u + xv;
+        const uint32_t pack = e ? (sym | (rep_l << 8) | ((len + ex) << 16)) : 0xFFFFFFFFu;
+        // serial part: the chain of true symbol starts, their first index and value;
+        // the code lengths themselves are written afterwards by the lanes in parallel
+        const uint64_t end_rel64 = end_bits > w0 * 32 ? end_bits - w0 * 32 : 0;
+        const uint32_t end_rel = end_rel64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)end_rel64;
+        uint32_t widx = 0xFFFFFFFFu, wval = 0;  // per lane: (seq << 16 | index), value
+        uint32_t p = 0, err = 0;
+        bool done = false;
+        while (p < 64) {
+            const uint32_t pk = __builtin_amdgcn_readlane(pack, p);
+            if (pk == 0xFFFFFFFFu) {
+                err = SEGF_ERR_DATA;
+                break;
+            }
+            const uint32_t s = pk & 0xFF, rep = (pk >> 8) & 0xFF;
+            const uint32_t at = p;
+            p += pk >> 16;
+            if (s == 16 && rfc && i == 0) {
+                err = SEGF_ERR_DATA;
+                break;
+            }
+            const uint32_t val = s < 16 ? s : s == 16 ? last : 0u;
+            if (rfc || s < 16) last = val;
+            if (rp + p > end_rel) {
+                err = SEGF_OVERREAD;
+                break;
+            }
+            if (i + rep > cap && (rfc || val != 0)) {  // reference: value >= 300 is UB
+                err = SEGF_ERR_DATA;
+                break;
+            }
+            widx = lane == (int)at ? (i | (seq << 16)) : widx;
+            wval = lane == (int)at ? val : wval;
+            i += rep;
+            if (i >= target) {
+                if (rfc) {
+                    done = true;
+                    break;
+                }
+                if (seq == 0) {  // reference mode: the distance lengths are a second sequence
+                    nl = min(i, 300u);
+                    seq = 1;
+                    target = nd;
+                    i = 0;
+                    last = 0;
+                } else {
+                    ndd = min(i, 300u);
+                    done = true;
+                    break;
+                }
+            }
+        }
+        // parallel writes: entries idx < cap keep the value (reference: overshoot entries
+        // keep their index as the symbol value); long runs are written by the whole wave
+        {
+            const bool mine = widx != 0xFFFFFFFFu;
+            const uint32_t i0 = widx & 0xFFFF, sq = widx >> 16;
+            const bool longr = mine && rep_l > 8;
+            if (mine && !longr) {
+                for (uint32_t jj = 0; jj < rep_l; jj++) {
+                    const uint32_t idx = i0 + jj;
+                    if (idx < cap) {
+                        if (!rfc) (sq ? T.dlen : T.llen)[idx] = (uint8_t)wval;
+                        else if (idx < na) T.llen[idx] = (uint8_t)wval;
+                        else T.dlen[idx - na] = (uint8_t)wval;
+                    }
+                }
+            }
+            uint64_t lm = __ballot(longr);
+            while (lm) {
+                const int l = __builtin_ctzll(lm);
+                lm &= lm - 1;
+                const uint32_t wl = __builtin_amdgcn_readlane(widx, l);
+                const uint32_t vl = __builtin_amdgcn_readlane(wval, l);
+                const uint32_t rl = __builtin_amdgcn_readlane(rep_l, l);
+                const uint32_t b0 = wl & 0xFFFF;
+                for (uint32_t jj = lane; jj < rl; jj += 64) {
+                    const uint32_t idx = b0 + jj;
+                    if (idx < cap) {
+                        if (!rfc) ((wl >> 16) ? T.dlen : T.llen)[idx] = (uint8_t)vl;
+                        else if (idx < na) T.llen[idx] = (uint8_t)vl;
+                        else T.dlen[idx - na] = (uint8_t)vl;
+                    }
+                }
+            }
+        }
+        rp += p;
+        if (err) return err;
+        if (done) break;
+    }
+    if (rfc) {
+        nl = na;
+        ndd = nd;
+    }
+    *pos_io = w0 * 32 + rp;
+    wave_sync();
+    FH_STAMP(1);
+    build_tree(T.llen, nl, T.lsorted, T.lm);
+    build_tree(T.dlen, ndd, T.dsorted, T.dm);
+    wave_sync();
+    FH_STAMP(2);
+    if (fill) {
+        fill_lut<LUT_L>(T.llut, T.lm, T.lsorted);
+        fill_lut<LUT_D>(T.dlut, T.dm, T.dsorted);
+    }
+    wave_sync();
+    FH_STAMP(3);
+#undef FH_STAMP
     return 0;
 }
 
@@ -540,9 +734,12 @@ __device__ uint32_t inflate_blocks(BitIn& br, Tables& T, Sink& sk, bool rfc, boo
         } else if (btype == 2) {
             T.fixed_loaded = 0;
             const uint64_t h0 = hdr_cycles ? __builtin_amdgcn_s_memtime() : 0;
-            uint32_t err = read_dynamic_header(br, T, rfc);
+            uint64_t hp = br.pos;
+            const GlobalWords src{br.w, br.nwords, br.end_bytes};
+            uint32_t err = fast_header(src, &hp, br.end_bits, T, rfc, true, hdr_cycles ? hdr_cycles + 1 : nullptr);
             if (hdr_cycles) *hdr_cycles += __builtin_amdgcn_s_memtime() - h0;
             if (err) return err;
+            br.seek(hp);
             err = decode_huffman(br, T, sk);
             if (err) return err;
         }  // btype 3: no-op block (inflate.hpp:292 has no case 3)
@@ -651,9 +848,10 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
     __syncthreads();
     const uint64_t j = s_j;
     if (j >= A.ncand) return;
+    if (A.mode == 3 && !(A.recs[j].flags & SEGF_EXOTIC)) return;  // patch pass: declined ones only
     DMX_PHASE(A.dbg, j, 0);
     const uint64_t start = A.cands[j];
-    uint64_t hdr_cycles = 0;
+    uint64_t hdr_cycles[5] = {0, 0, 0, 0, 0};
 
     BitIn br;
     br.init(A.in_words, A.misalign, A.n);
@@ -662,14 +860,17 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
     uint64_t end_byte = 0;
     bool fin = false;
     uint32_t err = inflate_blocks(br, T, sk, (A.flags & DMX_CFG_RFC_STRICT) != 0, true, &end_byte, &fin,
-                                  A.dbg ? &hdr_cycles : nullptr);
+                                  A.dbg ? hdr_cycles : nullptr);
     const uint32_t size = err ? 0 : sk.pos;
     DMX_PHASE(A.dbg, j, 1);
-    if (A.dbg && lane_id() == 0) A.dbg[j * kPhaseSlots + 8] = hdr_cycles;
+    if (A.dbg && lane_id() == 0)
+        for (int k = 0; k < 5; k++) A.dbg[j * kPhaseSlots + 8 + k] = hdr_cycles[k];
 
     if (lane == 0) {
         uint64_t excl = 0;
-        if (A.mode == 0) {
+        if (A.mode == 3) {
+            excl = j * (uint64_t)A.slot;  // the workgroup decoder's slot
+        } else if (A.mode == 0) {
             // speculative: every segment before the final one has this segment's size (what
             // libdmx's deflate emits); the final one takes segment 0's size.  Checked after
             // the kernel by k_inflate_validate; a miss re-runs in look-back mode.
@@ -738,12 +939,14 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------
-// k_inflate_pj: one workgroup of PJ_NT lanes per candidate segment.
-//   1. wave 0 reads the block header (wave-uniform, as above) into shared tables;
-//   2. the segment's Huffman bits are split into PJ_NT equal ranges; lane t decodes tokens
-//      from the start of its range (an arbitrary bit: Huffman decoding self-synchronises
-//      within a few tokens) until its path crosses into the next range, keeping the first
-//      PJ_K token boundaries it passed;
+// k_inflate_pj<SEG, NT>: one workgroup of NT lanes per candidate segment of up to SEG bytes.
+//   1. wave 0 reads BTYPE; a stored segment is copied HBM -> HBM; a Huffman segment's
+//      compressed words are staged in LDS (every later bit read is an LDS read), then wave 0
+//      reads the block header and the workgroup fills the lookup tables;
+//   2. the segment's Huffman bits are split into nl equal ranges; lane t decodes tokens from
+//      the start of its range (an arbitrary bit: Huffman decoding self-synchronises within a
+//      few tokens) until its path crosses into the next range, keeping the first PJ_K token
+//      boundaries it passed;
 //   3. settle: lane t restarts where lane t-1's path left its range and decodes until it
 //      reaches a boundary of its own first path (merged: the rest of its count is known) --
 //      repeated until every range starts where the previous one ended (normally one round);
@@ -751,56 +954,78 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
 //      writes P[x] for each output byte x: 0x8000 | byte for a literal, or the position the
 //      byte is copied from (LZ77 copy out[o + i] = out[o - d + (i mod d)], always < x);
 //   5. pointer jumping P[x] = P[P[x]] until every entry is a literal (chains halve per round);
-//   6. the low bytes of P go to HBM with 16-byte stores at the segment's slot j * 32768.
-// Everything else -- several blocks in one segment, stored + Huffman mixes, an output above
-// 32 KiB, a split that does not settle -- is flagged SEGF_EXOTIC and the whole stream is
-// redone by k_inflate_segments, so results never depend on this path's coverage.
+//   6. the low bytes of P go to HBM with 16-byte stores at the segment's slot j * SEG.
+// Everything else -- several blocks in one segment, an output above SEG, compressed data
+// above the staging buffer, a split that does not settle -- is flagged SEGF_EXOTIC and the
+// stream is redone by k_inflate_segments, so results never depend on this path's coverage.
 // ---------------------------------------------------------------------------------------
-constexpr int PJ_NT = 256;
 constexpr int PJ_K = 8;
 constexpr uint32_t PJ_LIT = 0x8000u;
-constexpr uint32_t PJ_MAXBITS = 1u << 20;  // Huffman bits of one segment (32 KiB * 15 < 2^19)
-constexpr int PJ_ROUNDS = 16;
+constexpr int PJ_ROUNDS = 64;
 constexpr uint32_t PJ_MINBITS = 256;
+constexpr int PJ_LL = 12;  // lit/len lookup bits
+constexpr int PJ_LD = 10;  // distance lookup bits
 
-// LSB-first bit reader whose position differs per lane: plain (vector) loads
-struct LBits {
+template <int SEG, int NT>
+struct PjSmem {
+    static constexpr int IN_WORDS = (SEG + 2048) / 4 + 8;
+    uint16_t P[SEG];
+    uint32_t in[IN_WORDS];  // the candidate's compressed words, in[0] = stream word ws
+    uint16_t llut[1 << PJ_LL];
+    uint16_t dlut[1 << PJ_LD];
+    Tables T;
+    uint32_t endp[NT];      // where range r's current path crossed into range r+1; later the
+                            // exclusive output offset of range r
+    uint32_t cntr[NT];      // output bytes of range r
+    uint32_t part[NT / 64];
+    uint32_t te2[2];        // first range whose path ends (EOB / no code), alternating words
+    uint32_t dcount[4];     // developer counters (DMX_PHASES)
+    uint64_t ws;            // first staged stream word
+    uint32_t nst;           // staged words
+    uint32_t hs;            // first Huffman bit, relative to ws * 32
+    uint32_t hlen;          // bits split among the lanes
+    uint32_t kind;          // 0 Huffman, 1 stored, 2 done (empty segment / error)
+    uint32_t btype;
+    uint32_t bfinal;
+    uint32_t err;
+    uint32_t slen;
+    uint64_t sb0;
+    uint32_t total;
+    uint64_t end_byte;
+};
+
+// wave-uniform bit reader over the staged words (same contract as BitIn)
+struct LdsBitIn {
     const uint32_t* w;
-    uint64_t nwords, end_bytes;
+    uint64_t ws, nw;
+    uint64_t nwords, end_bytes, end_bits;
     uint64_t pos;
     uint64_t buf;
     uint32_t cnt;
     uint64_t wi;
-    uint32_t q0, q1;
 
-    __device__ void init(const uint32_t* words, uint64_t misalign, uint64_t n) {
-        w = words;
+    __device__ void init(const uint32_t* lds, uint64_t first, uint64_t count, uint64_t misalign, uint64_t n) {
+        w = lds;
+        ws = first;
+        nw = count;
         end_bytes = misalign + n;
+        end_bits = end_bytes * 8;
         nwords = (end_bytes + 3) / 4;
     }
-    __device__ uint32_t raw(uint64_t i) const { return w[i < nwords ? i : nwords - 1]; }
-    __device__ uint32_t mask(uint64_t i) const {
-        if (i >= nwords) return 0u;
-        const uint64_t lim = end_bytes - 4 * i;
-        return lim >= 4 ? 0xFFFFFFFFu : ((1u << (8 * lim)) - 1u);
-    }
+    __device__ uint32_t raw(uint64_t i) const { return (i >= ws && i < ws + nw) ? w[i - ws] : 0u; }
     __device__ void refill() {
         if (cnt <= 32) {
-            buf |= (uint64_t)(q0 & mask(wi)) << cnt;
+            buf |= (uint64_t)raw(wi) << cnt;  // staged words are already masked at the stream end
             cnt += 32;
             wi++;
-            q0 = q1;
-            q1 = raw(wi + 1);
         }
     }
     __device__ void seek(uint64_t bitpos) {
         pos = bitpos;
         const uint64_t i = bitpos >> 5;
-        buf = (uint64_t)((raw(i) & mask(i)) >> (bitpos & 31));
+        buf = (uint64_t)(raw(i) >> (bitpos & 31));
         cnt = 32 - (uint32_t)(bitpos & 31);
         wi = i + 1;
-        q0 = raw(wi);
-        q1 = raw(wi + 1);
         refill();
     }
     __device__ void ensure(uint32_t k) {
@@ -818,50 +1043,91 @@ struct LBits {
         consume(k);
         return v;
     }
+    __device__ bool over() const { return pos > end_bits; }
 };
+
+// 32 bits at bit p of the staged words (LSB = bit p)
+__device__ __forceinline__ uint32_t lds_peek32(const uint32_t* w, uint32_t p) {
+    const uint32_t i = p >> 5;
+    return __builtin_amdgcn_alignbit(w[i + 1], w[i], p & 31);
+}
+
+// primary lookup table over PB bits filled by the whole workgroup (same entries as fill_lut)
+template <int PB>
+__device__ void fill_lut_wg(uint16_t* lut, const TreeMeta& m, const uint16_t* sorted, int tid, int nthr) {
+    uint32_t lo[16], hi[16], cn[16], of[16];
+#pragma unroll
+    for (int k = 1; k < 16; k++) {
+        lo[k] = m.lo[k];
+        hi[k] = m.hi[k];
+        cn[k] = m.cnt[k];
+        of[k] = m.offs[k];
+    }
+    for (int wv = tid; wv < (1 << PB); wv += nthr) {
+        const uint32_t v = bitrev(wv, PB);
+        uint32_t idx = 0, len = 0;
+#pragma unroll
+        for (int k = 1; k <= PB && k < 16; k++) {
+            const uint32_t x = v >> (PB - k);
+            if (!len && cn[k] && x <= hi[k]) {
+                const uint32_t cm = x + (((hi[k] - x) >> k) << k);
+                if (cm >= lo[k]) {
+                    idx = of[k] + cm - lo[k];
+                    len = k;
+                }
+            }
+        }
+        lut[wv] = len ? (uint16_t)(sorted[idx] | (len << 9)) : (uint16_t)0;
+    }
+}
 
 enum : uint32_t { TK_LIT = 0, TK_MATCH = 1, TK_EOB = 2, TK_BAD = 3 };
 
-// one token of decompressHuffmanBlock (inflate.hpp:226-275): a literal (*a = byte), a match
-// (*a = length, *d = distance; 0 for symbols 286+ / 30+), the end of block, or no code
-__device__ __forceinline__ uint32_t pj_token(LBits& br, const Tables& T, uint32_t* a, uint32_t* d) {
-    br.ensure(20);
-    uint32_t v = br.peek(15);
-    uint32_t e = T.llut[v & ((1u << LUT_L) - 1)];
+// one token of decompressHuffmanBlock (inflate.hpp:226-275) at bit *p of the staged words:
+// a literal (*a = byte), a match (*a = length, *d = distance; 0 for symbols 286+ / 30+), the
+// end of block, or no code.  A literal reads one 32-bit window, a match two.
+__device__ __forceinline__ uint32_t pj_token(const uint32_t* w, uint32_t* p, const uint16_t* llut,
+                                             const uint16_t* dlut, const Tables& T, uint32_t* a,
+                                             uint32_t* d) {
+    uint32_t v = lds_peek32(w, *p);
+    uint32_t e = llut[v & ((1u << PJ_LL) - 1)];
     uint32_t sym, len;
     if (e) {
         sym = e & 511;
         len = e >> 9;
-    } else if (!slow_decode(T.lm, T.lsorted, v, LUT_L + 1, &sym, &len)) {
+    } else if (!slow_decode(T.lm, T.lsorted, v & 0x7FFF, PJ_LL + 1, &sym, &len)) {
         return TK_BAD;
     }
-    br.consume(len);
     if (sym < 256) {
+        *p += len;
         *a = sym;
         return TK_LIT;
     }
-    if (sym == 256) return TK_EOB;
-    uint32_t L = 0;
-    if (sym <= 285) {
-        const uint32_t ex = len_extra(sym);
-        L = len_base(sym) + (ex ? br.bits(ex) : 0);
+    if (sym == 256) {
+        *p += len;
+        return TK_EOB;
     }
-    br.ensure(28);
-    v = br.peek(15);
-    e = T.dlut[v & ((1u << LUT_D) - 1)];
+    uint32_t L = 0, ex = 0;
+    if (sym <= 285) {
+        ex = len_extra(sym);
+        L = len_base(sym) + ((v >> len) & ((1u << ex) - 1u));
+    }
+    *p += len + ex;
+    v = lds_peek32(w, *p);
+    e = dlut[v & ((1u << PJ_LD) - 1)];
     uint32_t ds, dl;
     if (e) {
         ds = e & 511;
         dl = e >> 9;
-    } else if (!slow_decode(T.dm, T.dsorted, v, LUT_D + 1, &ds, &dl)) {
+    } else if (!slow_decode(T.dm, T.dsorted, v & 0x7FFF, PJ_LD + 1, &ds, &dl)) {
         return TK_BAD;
     }
-    br.consume(dl);
-    uint32_t dist = 0;
+    uint32_t dist = 0, dx = 0;
     if (ds < 30) {
-        const uint32_t ex = dist_extra(ds);
-        dist = dist_base(ds) + (ex ? br.bits(ex) : 0);
+        dx = dist_extra(ds);
+        dist = dist_base(ds) + ((v >> dl) & ((1u << dx) - 1u));
     }
+    *p += dl + dx;
     *a = L;
     *d = dist;
     return TK_MATCH;
@@ -871,33 +1137,20 @@ __device__ __forceinline__ uint32_t tok_bytes(uint32_t k, uint32_t a, uint32_t d
     return k == TK_LIT ? 1u : (k == TK_MATCH && a && d) ? a : 0u;
 }
 
-struct PjSmem {
-    uint16_t P[SEG_CAP];
-    Tables T;
-    uint32_t endp[PJ_NT];   // where lane t's current path crossed into range t+1 (relative)
-    uint32_t part[PJ_NT / 64];
-    uint64_t hs;            // absolute bit of the first Huffman token
-    uint32_t hlen;          // bits split among the lanes
-    uint32_t kind;          // 0 Huffman, 1 stored, 2 done (empty segment / error)
-    uint32_t bfinal;
-    uint32_t err;
-    uint32_t slen;
-    uint64_t sb0;
-    uint32_t tew[PJ_NT / 64];  // per wave: first lane whose path ends (EOB / no code)
-    uint32_t total;
-    uint64_t end_byte;
-};
-
-__global__ __launch_bounds__(PJ_NT) void k_inflate_pj(InflateArgs A) {
-    __shared__ __attribute__((aligned(16))) PjSmem S;
+template <int SEG, int NT>
+__global__ __launch_bounds__(NT) void k_inflate_pj(InflateArgs A) {
+    using Smem = PjSmem<SEG, NT>;
+    __shared__ __attribute__((aligned(16))) Smem S;
+    constexpr int NW = NT / 64;
     const int t = threadIdx.x;
     const int wave = t >> 6;
     const uint64_t j = blockIdx.x;
     const bool rfc = (A.flags & DMX_CFG_RFC_STRICT) != 0;
-    const uint64_t obase = j * (uint64_t)SEG_CAP;
+    const uint64_t obase = j * (uint64_t)SEG;
+    const uint64_t end_bytes = A.misalign + A.n;
     DMX_PHASE(A.dbg, j, 0);
 
-    // ---- 1. block header (wave 0) ----
+    // ---- 1. block type (wave 0), stored segments ----
     if (wave == 0) {
         BitIn br;
         br.init(A.in_words, A.misalign, A.n);
@@ -906,8 +1159,8 @@ __global__ __launch_bounds__(PJ_NT) void k_inflate_pj(InflateArgs A) {
         const uint32_t bfinal = br.bits(1);
         const uint32_t btype = br.bits(2);
         uint32_t kind = 2, err = 0;
-        uint64_t end_byte = 0, sb0 = 0;
-        uint32_t slen = 0, hlen = 0;
+        uint64_t end_byte = 0, sb0 = 0, ws = 0;
+        uint32_t slen = 0, nst = 0;
         if (br.over()) {
             err = SEGF_OVERREAD;
         } else if (btype == 0) {
@@ -922,6 +1175,8 @@ __global__ __launch_bounds__(PJ_NT) void k_inflate_pj(InflateArgs A) {
                 end_byte = sb0;  // the segment is just the marker
             } else if (sb0 + len > br.end_bytes) {
                 err = SEGF_OVERREAD;
+            } else if (len > (uint32_t)SEG) {
+                err = SEGF_EXOTIC;
             } else if (bfinal) {
                 kind = 1;
                 slen = len;
@@ -941,73 +1196,112 @@ __global__ __launch_bounds__(PJ_NT) void k_inflate_pj(InflateArgs A) {
         } else if (btype == 3) {
             err = SEGF_EXOTIC;
         } else {
-            if (btype == 1) {
-                load_fixed(S.T);
+            // stage words [ws, we): the candidate through the word after the next candidate
+            ws = (A.misalign + A.cands[j]) >> 2;
+            const uint64_t next = j + 1 < A.ncand ? A.cands[j + 1] : A.n;
+            const uint64_t we = min((A.misalign + next + 3) / 4 + 1, br.nwords);
+            if (we - ws + 4 > (uint64_t)Smem::IN_WORDS) {
+                err = SEGF_EXOTIC;
             } else {
-                err = read_dynamic_header(br, S.T, rfc);
-            }
-            if (!err) {
-                const uint64_t hs = br.pos;
-                const uint64_t he = j + 1 < A.ncand ? (A.misalign + A.cands[j + 1] - 4) * 8 - 3
-                                                    : (A.misalign + A.n) * 8;
-                if (he <= hs || he - hs > PJ_MAXBITS) {
-                    err = SEGF_EXOTIC;
-                } else {
-                    kind = 0;
-                    hlen = (uint32_t)(he - hs);
-                }
-                if (lane_id() == 0) S.hs = hs;
+                kind = 0;
+                nst = (uint32_t)(we - ws);
             }
         }
         if (lane_id() == 0) {
             S.kind = err ? 2 : kind;
             S.err = err;
+            S.btype = btype;
             S.bfinal = bfinal;
             S.end_byte = end_byte;
             S.slen = slen;
             S.sb0 = sb0;
-            S.hlen = hlen;
+            S.ws = ws;
+            S.nst = nst;
             S.total = kind == 1 ? slen : 0;
+            S.dcount[0] = S.dcount[1] = S.dcount[2] = S.dcount[3] = 0;
         }
     }
     __syncthreads();
-    DMX_PHASE(A.dbg, j, 1);
     const uint32_t kind = S.kind;
 
     if (kind == 1) {
-        // ---- stored segment: bytes straight to the slot ----
         const uint32_t len = S.slen;
-        if (len > SEG_CAP) {
-            if (t == 0) S.err = SEGF_OVERFLOW;
-        } else {
-            const uint64_t b0 = S.sb0;
-            const uint8_t* src = reinterpret_cast<const uint8_t*>(A.in_words);
-            for (uint32_t i = t; i < len; i += PJ_NT)
-                if (obase + i < A.cap) A.out[obase + i] = src[b0 + i];
-        }
+        const uint64_t b0 = S.sb0;
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(A.in_words);
+        for (uint32_t i = t; i < len; i += NT)
+            if (obase + i < A.cap) A.out[obase + i] = src[b0 + i];
     } else if (kind == 0) {
-        // ---- 2. first pass over the lane ranges ----
-        const uint64_t hs = S.hs;
+        // ---- stage the compressed words (masked at the stream end), 4 words of zeros after ----
+        const uint64_t ws = S.ws;
+        const uint32_t nst = S.nst;
+        for (uint32_t i = t; i < nst + 4; i += NT) {
+            uint32_t v = 0;
+            if (i < nst) {
+                const uint64_t wi = ws + i;
+                v = A.in_words[wi];
+                const uint64_t lim = end_bytes - 4 * wi;
+                if (lim < 4) v &= (1u << (8 * lim)) - 1u;
+            }
+            S.in[i] = v;
+        }
+        __syncthreads();
+        // ---- block header (wave 0) ----
+        if (wave == 0) {
+            uint64_t hp = (A.misalign + A.cands[j]) * 8 + 3;
+            uint32_t err = 0;
+            if (S.btype == 1) {
+                load_fixed(S.T);
+            } else {
+                const StagedWords src{S.in, ws, nst};
+                err = fast_header(src, &hp, end_bytes * 8, S.T, rfc, false);
+            }
+            if (lane_id() == 0) {
+                const uint64_t hs = hp - ws * 32;
+                const uint64_t he = j + 1 < A.ncand ? (A.misalign + A.cands[j + 1] - 4) * 8 - 3 - ws * 32
+                                                    : (uint64_t)nst * 32;
+                if (!err && (he <= hs || he > (uint64_t)nst * 32)) err = SEGF_EXOTIC;
+                S.err = err;
+                S.hs = (uint32_t)hs;
+                S.hlen = err ? 0 : (uint32_t)(he - hs);
+            }
+        }
+        __syncthreads();
+        DMX_PHASE(A.dbg, j, 1);
+        if (!S.err) {
+            fill_lut_wg<PJ_LL>(S.llut, S.T.lm, S.T.lsorted, t, NT);
+            fill_lut_wg<PJ_LD>(S.dlut, S.T.dm, S.T.dsorted, t, NT);
+        }
+        __syncthreads();
+    }
+    if (kind == 0 && !S.err) {
+        const uint32_t* win = S.in;
+        const uint32_t hs = S.hs;
         const uint32_t hlen = S.hlen;
         // ranges of at least PJ_MINBITS (a few dozen tokens) so that a path started at an
-        // arbitrary bit re-synchronises inside its own range; surplus lanes stay empty
-        const uint32_t nl = max(1u, min((uint32_t)PJ_NT, hlen / PJ_MINBITS));
-        const uint32_t sp = t < (int)nl ? (uint32_t)(((uint64_t)hlen * t) / nl) : hlen;
-        const uint32_t sp1 = t + 1 < (int)nl ? (uint32_t)(((uint64_t)hlen * (t + 1)) / nl) : hlen;
-        LBits br;
-        br.init(A.in_words, A.misalign, A.n);
+        // arbitrary bit re-synchronises inside its own range; range r belongs to thread
+        // (r % NW) * 64 + r / NW so that a short segment's ranges spread over every wave
+        const uint32_t nl = max(1u, min((uint32_t)NT, hlen / PJ_MINBITS));
+        const uint32_t r = (uint32_t)((t & 63) * NW + wave);
+        const uint32_t sp = r < nl ? (uint32_t)(((uint64_t)hlen * r) / nl) : hlen;
+        const uint32_t sp1 = r + 1 < nl ? (uint32_t)(((uint64_t)hlen * (r + 1)) / nl) : hlen;
+        // P is free until the emit pass: it holds the first pass's token-start bitmap
+        uint32_t* bmap = reinterpret_cast<uint32_t*>(S.P);
+        for (uint32_t i = t; i < hlen / 32 + 2; i += NT) bmap[i] = 0;
+        if (t < 2) S.te2[t] = NT;
+        __syncthreads();
+        // ---- 2. first pass over the ranges (positions relative to hs) ----
         uint32_t q[PJ_K], c[PJ_K];
 #pragma unroll
         for (int k = 0; k < PJ_K; k++) q[k] = c[k] = 0xFFFFFFFFu;
         uint32_t e1, cnt1 = 0, st1 = 0, nb = 0;
         {
-            br.seek(hs + sp);
-            uint32_t p = sp;
+            uint32_t p = sp, pa = hs + sp;
             while (p < sp1) {
+                atomicOr(&bmap[p >> 5], 1u << (p & 31));
                 uint32_t a, d;
-                const uint32_t k = pj_token(br, S.T, &a, &d);
+                const uint32_t k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
                 if (k == TK_BAD) { st1 = 2; break; }
-                p = (uint32_t)(br.pos - hs);
+                p = pa - hs;
                 if (k == TK_EOB) { st1 = 1; break; }
                 cnt1 += tok_bytes(k, a, d);
                 if (nb < PJ_K) {
@@ -1019,53 +1313,78 @@ __global__ __launch_bounds__(PJ_NT) void k_inflate_pj(InflateArgs A) {
             }
             e1 = p;
         }
+        DMX_PHASE(A.dbg, j, 2);
         // ---- 3. settle the range starts ----
-        // per round: [publish end, first-ending lane per wave] | read: te, want | or-barrier |
-        // redo | barrier.  Every shared word is written and read on opposite sides of a barrier.
+        // per round: [publish end, first ending range] | read te, want | or-barrier | redo |
+        // barrier.  Every shared word is written and read on opposite sides of a barrier; the
+        // first-ending-range minimum alternates between two words (one reset per round).
         uint32_t s = sp, e = e1, cnt = cnt1, st = st1;
-        uint32_t te = PJ_NT;
+        uint32_t te = NT;
         bool settled = false;
+        uint32_t settle_rounds = 0;
         for (int round = 0; round <= PJ_ROUNDS; round++) {
-            S.endp[t] = e;
-            {
-                const uint64_t bm = __ballot(st != 0);
-                if ((t & 63) == 0) S.tew[wave] = bm ? (uint32_t)(wave * 64 + __ffsll((long long)bm) - 1) : PJ_NT;
-            }
+            S.endp[r] = e;
+            if (st) atomicMin(&S.te2[round & 1], r);
+            if (t == 0) S.te2[(round + 1) & 1] = NT;
             __syncthreads();
-            te = min(min(S.tew[0], S.tew[1]), min(S.tew[2], S.tew[3]));
-            const uint32_t want = t == 0 ? 0 : S.endp[t - 1];
-            const bool redo = t > 0 && t <= (int)te && want != s;
+            te = S.te2[round & 1];
+            const uint32_t want = r == 0 ? 0 : S.endp[r - 1];
+            const bool redo = r > 0 && r <= te && want != s;
+            settle_rounds = round;
             if (!__syncthreads_or(redo)) {
                 settled = true;
                 break;
             }
             if (round == PJ_ROUNDS) break;
             if (redo) {
-                // decode from the true start until the path meets a boundary of the first pass
+                // decode from the true start until the path meets a token start of this
+                // range's first pass (from there on both paths are the same)
                 s = want;
-                uint32_t p = want, acc = 0, stn = 0;
+                uint32_t p = want, pa = hs + want, acc = 0, stn = 0, dbg_tok = 0;
                 bool merged = false;
-                br.seek(hs + p);
                 for (;;) {
-                    if (p == sp) {
+                    if (p >= sp1) break;
+                    if (p >= sp && ((bmap[p >> 5] >> (p & 31)) & 1u)) {
                         merged = true;
-                        cnt = acc + cnt1;
+                        break;
                     }
-#pragma unroll
-                    for (int m = 0; m < PJ_K; m++)
-                        if (!merged && p == q[m]) {
-                            merged = true;
-                            cnt = acc + cnt1 - c[m];
-                        }
-                    if (merged || p >= sp1) break;
                     uint32_t a, d;
-                    const uint32_t k = pj_token(br, S.T, &a, &d);
+                    dbg_tok++;
+                    const uint32_t k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
                     if (k == TK_BAD) { stn = 2; break; }
-                    p = (uint32_t)(br.pos - hs);
+                    p = pa - hs;
                     if (k == TK_EOB) { stn = 1; break; }
                     acc += tok_bytes(k, a, d);
                 }
                 if (merged) {
+                    // first-pass bytes of the tokens before p: kept boundaries, else re-walk
+                    uint32_t before = 0, from = sp, cum = 0;
+                    bool found = p == sp;
+#pragma unroll
+                    for (int m = 0; m < PJ_K; m++) {
+                        if (!found && q[m] == p) {
+                            before = c[m];
+                            found = true;
+                        }
+                        if (!found && q[m] < p) {
+                            from = q[m];
+                            cum = c[m];
+                        }
+                    }
+                    if (!found) {
+                        uint32_t pw = from, pwa = hs + from;
+                        while (pw < p) {
+                            uint32_t a, d;
+                            dbg_tok++;
+                            const uint32_t k = pj_token(win, &pwa, S.llut, S.dlut, S.T, &a, &d);
+                            pw = pwa - hs;
+                            cum += tok_bytes(k, a, d);
+                            if (k == TK_BAD || k == TK_EOB) break;
+                        }
+                        if (pw != p) atomicOr(&S.err, SEGF_EXOTIC);  // cannot happen
+                        before = cum;
+                    }
+                    cnt = acc + cnt1 - before;
                     e = e1;
                     st = st1;
                 } else {
@@ -1073,26 +1392,40 @@ __global__ __launch_bounds__(PJ_NT) void k_inflate_pj(InflateArgs A) {
                     cnt = acc;
                     st = stn;
                 }
+                if (A.dbg) {
+                    atomicAdd(&S.dcount[0], dbg_tok);
+                    atomicAdd(&S.dcount[merged ? 1 : 2], 1u);
+                }
             }
             __syncthreads();
         }
         if (t == 0 && !settled) S.err |= SEGF_EXOTIC;
-        if (t == (int)te) {
+        DMX_PHASE(A.dbg, j, 3);
+        if (A.dbg && t == 0) {
+            A.dbg[j * kPhaseSlots + 9] = settle_rounds;
+            A.dbg[j * kPhaseSlots + 11] = S.dcount[0];
+            A.dbg[j * kPhaseSlots + 12] = S.dcount[1];
+            A.dbg[j * kPhaseSlots + 13] = S.dcount[2];
+            A.dbg[j * kPhaseSlots + 14] = nl;
+        }
+        if (r == te) {
             if (st == 2) {
                 S.err |= SEGF_ERR_DATA;
             } else {
                 // end of block: BFINAL ends the stream, else the marker block must follow
-                const uint64_t pe = hs + e;
-                if (S.bfinal) {
-                    S.end_byte = (pe + 7) >> 3;
+                const uint32_t pe = hs + e;
+                const uint64_t pe_abs = S.ws * 32 + pe;
+                if (pe_abs > end_bytes * 8) {
+                    S.err |= SEGF_OVERREAD;
+                } else if (S.bfinal) {
+                    S.end_byte = (pe_abs + 7) >> 3;
                 } else {
-                    br.seek(pe);
-                    const uint32_t h3 = br.bits(3);
-                    const uint64_t m = (pe + 3 + 7) >> 3;
-                    const uint8_t* src = reinterpret_cast<const uint8_t*>(A.in_words);
-                    if (h3 == 0 && m + 4 <= A.misalign + A.n && src[m] == 0 && src[m + 1] == 0 &&
-                        src[m + 2] == 0xFF && src[m + 3] == 0xFF)
-                        S.end_byte = m + 4;
+                    const uint32_t h3 = lds_peek32(win, pe) & 7;
+                    const uint32_t m = (pe + 3 + 7) >> 3;  // byte offset in the staged words
+                    const uint8_t* sb = reinterpret_cast<const uint8_t*>(win);
+                    if (h3 == 0 && m + 4 <= S.nst * 4 && sb[m] == 0 && sb[m + 1] == 0 &&
+                        sb[m + 2] == 0xFF && sb[m + 3] == 0xFF && S.ws * 4 + m + 4 <= end_bytes)
+                        S.end_byte = S.ws * 4 + m + 4;
                     else
                         S.err |= SEGF_EXOTIC;
                 }
@@ -1100,51 +1433,88 @@ __global__ __launch_bounds__(PJ_NT) void k_inflate_pj(InflateArgs A) {
         }
         // no end of block before the split end: several blocks, or the next candidate is not
         // this segment's end
-        if (te >= PJ_NT && t == 0) S.err |= SEGF_EXOTIC;
-        const uint32_t mycnt = t <= (int)te ? cnt : 0u;
-        // ---- 4. scan + emit ----
-        const uint32_t inc = wave_incl_scan(mycnt);
+        if (te >= (uint32_t)NT && t == 0) S.err |= SEGF_EXOTIC;
+        const uint32_t mycnt = r <= te ? cnt : 0u;
+        // ---- 4. scan in range order, then emit ----
+        S.cntr[r] = mycnt;
+        __syncthreads();
+        const uint32_t cv = S.cntr[t];
+        const uint32_t inc = wave_incl_scan(cv);
         if ((t & 63) == 63) S.part[wave] = inc;
         __syncthreads();
-        uint32_t base = 0;
-        for (int w = 0; w < wave; w++) base += S.part[w];
-        const uint32_t total = S.part[0] + S.part[1] + S.part[2] + S.part[3];
+        uint32_t base = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            const uint32_t v = S.part[w];
+            base += w < wave ? v : 0u;
+            total += v;
+        }
+        S.endp[t] = base + inc - cv;  // exclusive output offset of range t
         if (t == 0) {
             S.total = total;
-            if (total > SEG_CAP) S.err |= SEGF_OVERFLOW;
+            if (total > (uint32_t)SEG) S.err |= SEGF_EXOTIC;  // larger segments: other decoder
         }
         __syncthreads();
-        if (!S.err && t <= (int)te && mycnt) {
-            uint32_t o = base + inc - mycnt;
-            br.seek(hs + s);
-            uint32_t p = s;
+        if (!S.err) {
+            // wave-uniform token loop: matches of 16+ bytes are expanded by the whole wave
+            uint32_t o = S.endp[r];
+            uint32_t p = s, pa = hs + s;
+            bool act = r <= te && mycnt != 0;
             uint32_t bad = 0;
-            while (p < sp1) {
-                uint32_t a, d;
-                const uint32_t k = pj_token(br, S.T, &a, &d);
-                p = (uint32_t)(br.pos - hs);
-                if (k == TK_LIT) {
-                    S.P[o++] = (uint16_t)(PJ_LIT | a);
-                } else if (k == TK_MATCH) {
-                    if (!a || !d) continue;
-                    if (d > o) {  // before the segment: cross-segment or stream-start reference
-                        bad = j == 0 ? SEGF_EXOTIC : SEGF_XREF;
-                        break;
-                    }
-                    uint32_t src = o - d, r = 0;
-                    for (uint32_t i = 0; i < a; i++) {
-                        S.P[o + i] = (uint16_t)(src + r);
-                        if (++r == d) r = 0;
-                    }
-                    o += a;
-                } else {
-                    break;
+            uint32_t* P2 = reinterpret_cast<uint32_t*>(S.P);
+            const uint32_t lane = t & 63;
+            for (;;) {
+                const bool live = act && p < sp1;
+                if (!__ballot(live)) break;
+                uint32_t k = TK_EOB, a = 0, d = 0;
+                if (live) {
+                    k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
+                    p = pa - hs;
+                    if (k == TK_LIT) S.P[o++] = (uint16_t)(PJ_LIT | a);
+                    if (k == TK_EOB || k == TK_BAD) act = false;
                 }
+                bool mt = live && k == TK_MATCH && a && d;
+                if (mt && d > o) {  // before the segment: cross-segment or stream-start reference
+                    bad = j == 0 ? SEGF_EXOTIC : SEGF_XREF;
+                    act = false;
+                    mt = false;
+                }
+                const bool longm = mt && a >= 16;
+                if (mt && !longm) {
+                    const uint32_t src = o - d;
+                    uint32_t rr = 0;
+                    for (uint32_t i = 0; i < a; i++) {
+                        S.P[o + i] = (uint16_t)(src + rr);
+                        if (++rr == d) rr = 0;
+                    }
+                }
+                uint64_t lm = __ballot(longm);
+                while (lm) {
+                    const int l = __builtin_ctzll(lm);
+                    lm &= lm - 1;
+                    const uint32_t ol = __builtin_amdgcn_readlane(o, l);
+                    const uint32_t dl = __builtin_amdgcn_readlane(d, l);
+                    const uint32_t al = __builtin_amdgcn_readlane(a, l);
+                    const uint32_t src = ol - dl;
+                    if (dl >= al) {
+                        for (uint32_t i = lane; i < al; i += 64) S.P[ol + i] = (uint16_t)(src + i);
+                    } else {
+                        uint32_t rr = lane % dl;
+                        const uint32_t step = 64 % dl;
+                        for (uint32_t i = lane; i < al; i += 64) {
+                            S.P[ol + i] = (uint16_t)(src + rr);
+                            rr += step;
+                            if (rr >= dl) rr -= dl;
+                        }
+                    }
+                }
+                if (mt) o += a;
             }
+            (void)P2;
             if (bad) atomicOr(&S.err, bad);
         }
         __syncthreads();
-        DMX_PHASE(A.dbg, j, 2);
+        DMX_PHASE(A.dbg, j, 4);
         // ---- 5. pointer jumping ----
         if (!S.err) {
             uint32_t* P2 = reinterpret_cast<uint32_t*>(S.P);
@@ -1152,24 +1522,43 @@ __global__ __launch_bounds__(PJ_NT) void k_inflate_pj(InflateArgs A) {
             bool open = true;
             for (int round = 0; round < 24 && open; round++) {
                 uint32_t any = 0;
-                for (uint32_t i = t; i < npair; i += PJ_NT) {
-                    const uint32_t v = P2[i];
-                    uint32_t lo = v & 0xFFFF, hi = v >> 16;
-                    const bool plo = !(lo & PJ_LIT), phi = !(hi & PJ_LIT) && 2 * i + 1 < total;
-                    if (plo | phi) {
-                        if (plo) lo = S.P[lo];
-                        if (phi) hi = S.P[hi];
-                        if (phi) S.P[2 * i + 1] = (uint16_t)hi;
-                        if (plo) S.P[2 * i] = (uint16_t)lo;
-                        any |= (plo && !(lo & PJ_LIT)) || (phi && !(hi & PJ_LIT));
+                for (uint32_t i0 = t; i0 < npair; i0 += 4 * NT) {
+                    uint32_t v[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t i = i0 + u * NT;
+                        v[u] = i < npair ? P2[i] : (PJ_LIT | (PJ_LIT << 16));
+                    }
+                    uint32_t lo[4], hi[4];
+                    bool plo[4], phi[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t i = i0 + u * NT;
+                        lo[u] = v[u] & 0xFFFF;
+                        hi[u] = v[u] >> 16;
+                        plo[u] = !(lo[u] & PJ_LIT);
+                        phi[u] = !(hi[u] & PJ_LIT) && 2 * i + 1 < total;
+                        if (plo[u]) lo[u] = S.P[lo[u]];
+                        if (phi[u]) hi[u] = S.P[hi[u]];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t i = i0 + u * NT;
+                        if (plo[u] | phi[u]) {
+                            if (!phi[u]) hi[u] = v[u] >> 16;
+                            if (!plo[u]) lo[u] = v[u] & 0xFFFF;
+                            P2[i] = lo[u] | (hi[u] << 16);
+                            any |= (plo[u] && !(lo[u] & PJ_LIT)) || (phi[u] && !(hi[u] & PJ_LIT));
+                        }
                     }
                 }
                 open = __syncthreads_or(any) != 0;
+                if (A.dbg && t == 0) A.dbg[j * kPhaseSlots + 10] = round + 1;
             }
             if (open && t == 0) S.err |= SEGF_EXOTIC;
             __syncthreads();
         }
-        DMX_PHASE(A.dbg, j, 3);
+        DMX_PHASE(A.dbg, j, 5);
         // ---- 6. low bytes of P to the slot ----
         if (!S.err) {
             const uint32_t nb16 = total / 16;
@@ -1177,7 +1566,7 @@ __global__ __launch_bounds__(PJ_NT) void k_inflate_pj(InflateArgs A) {
             const bool vec = (((uintptr_t)dst) & 15) == 0 && obase + total <= A.cap;
             const uint4* P4 = reinterpret_cast<const uint4*>(S.P);
             if (vec) {
-                for (uint32_t i = t; i < nb16; i += PJ_NT) {
+                for (uint32_t i = t; i < nb16; i += NT) {
                     const uint4 a = P4[2 * i], b = P4[2 * i + 1];
                     uint4 o;
                     o.x = __builtin_amdgcn_perm(a.y, a.x, 0x06040200u);
@@ -1186,9 +1575,9 @@ __global__ __launch_bounds__(PJ_NT) void k_inflate_pj(InflateArgs A) {
                     o.w = __builtin_amdgcn_perm(b.w, b.z, 0x06040200u);
                     reinterpret_cast<uint4*>(dst)[i] = o;
                 }
-                for (uint32_t i = nb16 * 16 + t; i < total; i += PJ_NT) dst[i] = (uint8_t)S.P[i];
+                for (uint32_t i = nb16 * 16 + t; i < total; i += NT) dst[i] = (uint8_t)S.P[i];
             } else {
-                for (uint32_t i = t; i < total; i += PJ_NT)
+                for (uint32_t i = t; i < total; i += NT)
                     if (obase + i < A.cap) dst[i] = (uint8_t)S.P[i];
             }
         }
@@ -1201,12 +1590,16 @@ __global__ __launch_bounds__(PJ_NT) void k_inflate_pj(InflateArgs A) {
         A.recs[j].flags = err | (S.bfinal && !err ? SEGF_FINAL : 0u);
         A.recs[j].offset = obase;
     }
-    DMX_PHASE(A.dbg, j, 4);
+    DMX_PHASE(A.dbg, j, 6);
 }
 
-hipError_t launch_inflate_pj(const InflateArgs& A, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+hipError_t launch_inflate_pj(const InflateArgs& A, uint32_t seg, hipStream_t st, hipEvent_t ev0,
+                             hipEvent_t ev1) {
     if (ev0) (void)hipEventRecord(ev0, st);
-    hipLaunchKernelGGL(k_inflate_pj, dim3((uint32_t)A.ncand), dim3(PJ_NT), 0, st, A);
+    if (seg == 16384)
+        hipLaunchKernelGGL((k_inflate_pj<16384, 256>), dim3((uint32_t)A.ncand), dim3(256), 0, st, A);
+    else
+        hipLaunchKernelGGL((k_inflate_pj<32768, 512>), dim3((uint32_t)A.ncand), dim3(512), 0, st, A);
     if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();
 }
@@ -1215,16 +1608,17 @@ hipError_t launch_inflate_pj(const InflateArgs& A, hipStream_t st, hipEvent_t ev
 // without error and ended exactly at the next candidate.  Speculative mode additionally needs
 // every segment before k to have segment 0's size (else status 1: re-run with look-back).
 __global__ __launch_bounds__(1024) void k_inflate_validate(InflateArgs A, InflateResult* res) {
-    __shared__ unsigned long long kmin, bmin, umin, xmin;
+    __shared__ unsigned long long kmin, bmin, umin, xmin, xcnt;
     const int t = threadIdx.x;
-    if (t == 0) { kmin = ~0ull; bmin = ~0ull; umin = ~0ull; xmin = ~0ull; }
+    if (t == 0) { kmin = ~0ull; bmin = ~0ull; umin = ~0ull; xmin = ~0ull; xcnt = 0; }
     __syncthreads();
     // mode 2 (k_inflate_lanes) placed segment j at j * 32768
-    const uint32_t size0 = A.mode == 2 ? 32768u : A.recs[0].out_size;
+    const uint32_t size0 = A.mode >= 2 ? A.slot : A.recs[0].out_size;
     for (uint64_t j = t; j < A.ncand; j += 1024) {
         const SegRecord r = A.recs[j];
         if (r.flags & SEGF_EXOTIC) {  // k_inflate_pj declined this candidate
             atomicMin(&xmin, (unsigned long long)j);
+            atomicAdd(&xcnt, 1ull);
             continue;
         }
         const bool fin = (r.flags & SEGF_FINAL) != 0;
@@ -1238,6 +1632,7 @@ __global__ __launch_bounds__(1024) void k_inflate_validate(InflateArgs A, Inflat
     if (t == 0) {
         const uint64_t k = kmin;
         res->fin_index = (uint32_t)k;
+        res->exotic = xcnt;
         if (xmin < A.ncand) {
             res->status = 1;
             res->total = 0;

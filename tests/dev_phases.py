@@ -7,7 +7,7 @@ out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "ph
 os.environ["DMX_PHASES"] = out
 import torch  # noqa: E402
 import dmx  # noqa: E402
-ctx = dmx.Context()
+ctx = dmx.Context(segment_bytes=int(os.environ.get("DMX_SEG", "32768")))
 ctx.set_timing(True)
 n = 256 << 20
 for kind in ("repeat", "text", "mixed", "random"):
