@@ -175,7 +175,8 @@ def main():
     # roofline of the dominant kernel: algorithmic bytes = N read + C written (deflate) or
     # C read + N written (inflate), per launch, over its HIP-event duration
     alg = n + comp_bytes
-    dom = "inflate_segments" if k_inf >= k_def else "deflate_segments"
+    inf_kernel = "k_inflate_pj" if recs[-1][4].path == 3 else "k_inflate_segments"
+    dom = inf_kernel if k_inf >= k_def else "k_deflate_segments"
     kms = max(k_inf, k_def)
     achieved = alg / (kms * 1e-3) / 1e9
     traffic = None
@@ -212,7 +213,8 @@ def main():
             "ratio": round(ratio, 4),
             "ref_ratio": REF_RATIO_L2.get(a.corpus) if a.level == 2 else None,
             "ref_ratio_note": REF_NOTES.get(a.corpus, "reference L2 stream round-trips"),
-            "kernel_ms": {"deflate_segments": round(k_def, 4), "inflate_segments": round(k_inf, 4)},
+            "kernel_ms": {"k_deflate_segments": round(k_def, 4), inf_kernel: round(k_inf, 4)},
+            "inflate_path": int(recs[-1][4].path),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                          "traffic": traffic, "kernel": dom,
