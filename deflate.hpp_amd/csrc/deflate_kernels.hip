@@ -631,14 +631,16 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
         if (level >= 2) {
             bool pok[2] = {false, false};
             uint32_t ph[2] = {0, 0}, pp[2] = {0, 0};
+            const uint32_t wave = t >> 6, lane = t & 63;
             for (uint32_t r0 = 0, rr = 0; r0 < nb; r0 += 2 * DF_NT, rr++) {
-                uint32_t h[2], p[2];
+                uint32_t h[2], p[2], key[2];
                 bool ok[2];
 #pragma unroll
                 for (int k = 0; k < 2; k++) {
                     p[k] = r0 + k * DF_NT + t;
                     ok[k] = p[k] + 4 <= nb;
-                    h[k] = ok[k] ? (ld32u(S.data32, p[k]) * 0x1E35A7BDu) >> (32 - DF_HB) : 0;
+                    key[k] = ok[k] ? ld32u(S.data32, p[k]) : 0;
+                    h[k] = ok[k] ? (key[k] * 0x1E35A7BDu) >> (32 - DF_HB) : 0;
                     if (ok[k]) atomicMax(&first[h[k]], (rr << 16) | (0xFFFFu - p[k]));  // first in round
                     if (pok[k]) atomicMax(&head[ph[k]], pp[k] + 1);                     // previous round
                 }
@@ -657,8 +659,22 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                             if (q) c = p[k] - (q - 1);
                         }
                         if (c > 32768) c = 0;
+                        // keep only matches of >= 3 bytes inside this 256-byte chunk (matches
+                        // never cross a chunk, so the parse lanes stay independent)
+                        if (c) {
+                            const uint32_t cend = min(p[k] / DF_CHUNK * DF_CHUNK + DF_CHUNK, nb);
+                            if (cend - p[k] < 3 || ((key[k] ^ ld32u(S.data32, p[k] - c)) & 0xFFFFFFu)) c = 0;
+                        }
                     }
                     if (p[k] < nb) S.cand[p[k]] = (uint16_t)c;
+                    // bit p of tokmap = "a match of >= 3 starts at p" until the walk turns it
+                    // into token starts
+                    const uint64_t m = __ballot(c != 0);
+                    const uint32_t w0 = (r0 + k * DF_NT + wave * 64) >> 5;
+                    if (lane == 0 && w0 < NMAP) {
+                        S.tokmap[w0] = (uint32_t)m;
+                        if (w0 + 1 < NMAP) S.tokmap[w0 + 1] = (uint32_t)(m >> 32);
+                    }
                     pok[k] = ok[k];
                     ph[k] = h[k];
                     pp[k] = p[k];
@@ -666,39 +682,12 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                 __syncthreads();
             }
             DMX_PHASE(A.dbg, seg, 14);
-            // ---- match lengths capped at 16 (and at the chunk end), data-parallel; bit p of
-            //      tokmap = "a match of >= 3 starts at p" until the walk turns it into tokens
-            uint8_t* const L16 = reinterpret_cast<uint8_t*>(S.U);
-            const uint32_t wave = t >> 6, lane = t & 63;
-            for (uint32_t b = wave * 64; b < nb; b += DF_NT) {
-                const uint32_t q = b + lane;
-                uint32_t L = 0;
-                if (q < nb) {
-                    const uint32_t d = S.cand[q];
-                    if (d) {
-                        const uint32_t cap = min(16u, min(q / DF_CHUNK * DF_CHUNK + DF_CHUNK, nb) - q);
-                        L = matchlen(S.data32, q, q - d, cap);
-                        if (L < 3) {
-                            L = 0;
-                            S.cand[q] = 0;
-                        }
-                    }
-                    L16[q] = (uint8_t)L;
-                }
-                const uint64_t m = __ballot(L >= 3);
-                if (lane == 0) {
-                    S.tokmap[b >> 5] = (uint32_t)m;
-                    if ((b >> 5) + 1 < NMAP) S.tokmap[(b >> 5) + 1] = (uint32_t)(m >> 32);
-                }
-            }
-            __syncthreads();
         }
         DMX_PHASE(A.dbg, seg, 2);
 
         // ---- parse walk: one 256-byte chunk per lane; jumps over literal runs with the
         //      match bitmap, turns it into the token-start bitmap in place ------------------
         if (level >= 2 && t < NWALK) {
-            const uint8_t* const L16 = reinterpret_cast<const uint8_t*>(S.U);
             const uint32_t lo = t * DF_CHUNK;
             const uint32_t hi = min(lo + DF_CHUNK, nb);
             const uint32_t wlast = (hi - 1) >> 5;
@@ -706,15 +695,14 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                 const uint32_t e = b - w * 32;
                 return (e >= 32 ? 0xFFFFFFFFu : ((1u << e) - 1u)) & (0xFFFFFFFFu << (a & 31));
             };
-            auto full_len = [&](uint32_t q) -> uint32_t {
-                uint32_t L = L16[q];
-                if (L == 16 && hi - q > 16) {
-                    const uint32_t d = S.cand[q];
-                    L = 16 + matchlen(S.data32, q + 16, q + 16 - d, min(258u, hi - q) - 16);
-                }
-                return L;
+            auto full_len = [&](uint32_t q) -> uint32_t {  // >= 3: verified in the rounds
+                return matchlen(S.data32, q, q - S.cand[q], min(258u, hi - q));
             };
             uint32_t p = lo, w = lo >> 5, mw = S.tokmap[w], tok = 0;
+            auto mbit = [&](uint32_t q) -> bool {  // original match bit (w or the word after)
+                const uint32_t wq = q >> 5;
+                return ((wq == w ? mw : S.tokmap[wq]) >> (q & 31)) & 1u;
+            };
             while (p < hi) {
                 const uint32_t wi = p >> 5;
                 if (wi != w) {
@@ -735,8 +723,7 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                 tok |= bits_range(p, q, w);  // literals before the match
                 p = q;
                 uint32_t L = full_len(p);
-                const uint32_t l1 = (level == 3 && L < 258 && p + 1 < hi) ? L16[p + 1] : 0;
-                if (l1 > L || (l1 == 16 && L >= 16)) {
+                if (level == 3 && L < 258 && p + 1 < hi && mbit(p + 1)) {
                     if (full_len(p + 1) > L) {  // lazy: literal here, the longer match next
                         tok |= 1u << (p & 31);
                         S.cand[p] = 0;
