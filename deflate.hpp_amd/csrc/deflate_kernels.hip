@@ -36,6 +36,8 @@ namespace dmx {
 constexpr int DF_NT = 1024;    // threads per workgroup (16 waves)
 constexpr int DF_CHUNK = 256;  // bytes per parse lane
 constexpr int DF_HB = 12;      // hash bits of each of the two match tables
+constexpr int DF_PPT = 2;      // positions per thread in one match round (4 halves the rounds
+                               // but loses recent candidates: -4% ratio on repeat, -1% on text)
 
 // ---------------------------------------------------------------------------------------
 // block primitives
@@ -236,13 +238,34 @@ struct BitOr {
     }
 };
 
+// common prefix of the bytes at p and q, up to maxl; 16 bytes per step (five independent word
+// reads per side, one LDS latency per step).  The segment buffer is zero-padded past its end.
 __device__ __forceinline__ uint32_t matchlen(const uint32_t* w, uint32_t p, uint32_t q,
                                              uint32_t maxl) {
     uint32_t L = 0;
     while (L < maxl) {
-        uint32_t x = ld32u(w, p + L) ^ ld32u(w, q + L);
-        if (x) { L += (uint32_t)__builtin_ctz(x) >> 3; break; }
-        L += 4;
+        const uint32_t ip = (p + L) >> 2, sp = (p + L) & 3, iq = (q + L) >> 2, sq = (q + L) & 3;
+        uint32_t a[5], b[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            a[k] = w[ip + k];
+            b[k] = w[iq + k];
+        }
+        uint32_t x = 0, off = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t d = __builtin_amdgcn_alignbyte(a[k + 1], a[k], sp) ^
+                               __builtin_amdgcn_alignbyte(b[k + 1], b[k], sq);
+            if (!x && d) {
+                x = d;
+                off = 4 * k;
+            }
+        }
+        if (x) {
+            L += off + ((uint32_t)__builtin_ctz(x) >> 3);
+            break;
+        }
+        L += 16;
     }
     return min(L, maxl);
 }
@@ -629,14 +652,14 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
     if (level != 0) {
         // ---- match candidates: rounds of 2*DF_NT positions, two per thread ---------------
         if (level >= 2) {
-            bool pok[2] = {false, false};
-            uint32_t ph[2] = {0, 0}, pp[2] = {0, 0};
+            bool pok[DF_PPT] = {};
+            uint32_t ph[DF_PPT] = {}, pp[DF_PPT] = {};
             const uint32_t wave = t >> 6, lane = t & 63;
-            for (uint32_t r0 = 0, rr = 0; r0 < nb; r0 += 2 * DF_NT, rr++) {
-                uint32_t h[2], p[2], key[2];
-                bool ok[2];
+            for (uint32_t r0 = 0, rr = 0; r0 < nb; r0 += DF_PPT * DF_NT, rr++) {
+                uint32_t h[DF_PPT], p[DF_PPT], key[DF_PPT];
+                bool ok[DF_PPT];
 #pragma unroll
-                for (int k = 0; k < 2; k++) {
+                for (int k = 0; k < DF_PPT; k++) {
                     p[k] = r0 + k * DF_NT + t;
                     ok[k] = p[k] + 4 <= nb;
                     key[k] = ok[k] ? ld32u(S.data32, p[k]) : 0;
@@ -646,7 +669,7 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                 }
                 __syncthreads();
 #pragma unroll
-                for (int k = 0; k < 2; k++) {
+                for (int k = 0; k < DF_PPT; k++) {
                     uint32_t c = 0;
                     if (ok[k]) {
                         const uint32_t f = first[h[k]];
