@@ -27,17 +27,18 @@
 namespace dmx {
 
 constexpr int IF_NT = 64;  // one wavefront per segment decoder
+constexpr int IF_STAGE = 512;  // input words staged in LDS per candidate (fits 4 decoders/CU)
 constexpr int SEG_CAP = 32768;
-constexpr int LUT_L = 10;  // primary lit/len lookup bits
-constexpr int LUT_D = 8;   // primary distance lookup bits
+constexpr int LUT_L = 9;  // primary lit/len lookup bits (32-bit entries, see lit_entry)
+constexpr int LUT_D = 7;  // primary distance lookup bits (32-bit entries, see dist_entry)
 
 struct TreeMeta {
     uint32_t lo[16], hi[16], cnt[16], offs[16];
 };
 
 struct Tables {
-    uint16_t llut[1 << LUT_L];
-    uint16_t dlut[1 << LUT_D];
+    uint32_t llut[1 << LUT_L];
+    uint32_t dlut[1 << LUT_D];
     uint16_t plut[128];
     uint16_t lsorted[320];
     uint16_t dsorted[320];
@@ -60,18 +61,28 @@ struct BitIn {
     uint32_t cnt;  // valid bits in buf
     uint64_t wi;   // index of the word held in q0
     uint32_t q0, q1;  // raw words wi, wi + 1 (loaded two refills ahead of use)
+    const uint32_t* sw;  // optional LDS copy of words [sws, sws + snw)
+    uint64_t sws, snw;
 
     __device__ void init(const uint32_t* words, uint64_t misalign, uint64_t n) {
         w = words;
         end_bytes = misalign + n;
         end_bits = end_bytes * 8;
         nwords = (end_bytes + 3) / 4;
+        sw = nullptr;
+        sws = snw = 0;
     }
-    // Unconditional load with a clamped index (no branch, so the wait lands at first use).
-    // The decoder state is wave-uniform, so the input is read through the scalar cache
-    // (s_load, constant address space): a vector load would be waited on immediately to move
-    // its value into an SGPR, defeating the two-word prefetch.
+    __device__ void stage(const uint32_t* lds, uint64_t first, uint64_t count) {
+        sw = lds;
+        sws = first;
+        snw = count;
+    }
+    // Staged words come from LDS.  Otherwise: unconditional load with a clamped index (no
+    // branch, so the wait lands at first use); the decoder state is wave-uniform, so the input
+    // is read through the scalar cache (s_load, constant address space).  Scalar loads share
+    // lgkmcnt with LDS, so every table lookup also waits for them -- hence the staging.
     __device__ uint32_t raw(uint64_t i) const {
+        if (i - sws < snw) return sw[i - sws];
         const __attribute__((address_space(4))) uint32_t* cw =
             (const __attribute__((address_space(4))) uint32_t*)w;
         return cw[i < nwords ? i : nwords - 1];
@@ -123,6 +134,11 @@ struct BitIn {
     __device__ uint8_t byte_at(uint64_t b) const {  // b relative to the aligned base
         return (uint8_t)(w[b >> 2] >> ((b & 3) * 8));
     }
+    __device__ uint32_t window32() {  // the next 32 bits (LSB first)
+        ensure(32);
+        return (uint32_t)buf;
+    }
+    __device__ uint64_t abspos() const { return pos; }
 };
 
 // ---------------------------------------------------------------------------------------
@@ -219,6 +235,48 @@ __device__ void fill_lut(uint16_t* lut, const TreeMeta& m, const uint16_t* sorte
     }
 }
 
+// 32-bit decode entries: bits 0-3 code length, 4-5 class (0 literal, 1 end of block, 2 length),
+// 6-9 extra-bit count, 16-31 literal byte / length base / distance base.  Length symbols 286+
+// decode as length 0 and distance symbols 30+ as distance 0 (no copy, inflate.hpp:243-270).
+__device__ __forceinline__ uint32_t lit_entry(uint32_t sym, uint32_t len) {
+    if (sym < 256) return len | (sym << 16);
+    if (sym == 256) return len | (1u << 4);
+    if (sym > 285) return len | (2u << 4);
+    return len | (2u << 4) | (len_extra(sym) << 6) | (len_base(sym) << 16);
+}
+__device__ __forceinline__ uint32_t dist_entry(uint32_t ds, uint32_t len) {
+    if (ds >= 30) return len;
+    return len | (dist_extra(ds) << 6) | (dist_base(ds) << 16);
+}
+
+template <int PB, bool DIST>
+__device__ void fill_lut32(uint32_t* lut, const TreeMeta& m, const uint16_t* sorted) {
+    uint32_t lo[PB + 1], hi[PB + 1], cn[PB + 1], of[PB + 1];
+#pragma unroll
+    for (int k = 1; k <= PB; k++) {
+        lo[k] = m.lo[k];
+        hi[k] = m.hi[k];
+        cn[k] = m.cnt[k];
+        of[k] = m.offs[k];
+    }
+    for (int wv = lane_id(); wv < (1 << PB); wv += 64) {
+        const uint32_t v = bitrev(wv, PB);
+        uint32_t idx = 0, len = 0;
+#pragma unroll
+        for (int k = 1; k <= PB; k++) {
+            const uint32_t x = v >> (PB - k);
+            if (!len && cn[k] && x <= hi[k]) {
+                const uint32_t cm = x + (((hi[k] - x) >> k) << k);
+                if (cm >= lo[k]) {
+                    idx = of[k] + cm - lo[k];
+                    len = k;
+                }
+            }
+        }
+        lut[wv] = len ? (DIST ? dist_entry(sorted[idx], len) : lit_entry(sorted[idx], len)) : 0u;
+    }
+}
+
 // precode LUT: the stored code must also equal the bits read (inflate.hpp:175)
 __device__ void fill_prelut(uint16_t* lut, const TreeMeta& m, const uint16_t* sorted) {
     for (int wv = lane_id(); wv < 128; wv += 64) {
@@ -259,109 +317,17 @@ __device__ void load_fixed(Tables& T) {
     wave_sync();
     build_tree(T.llen, 288, T.lsorted, T.lm);
     build_tree(T.dlen, 32, T.dsorted, T.dm);
-    fill_lut<LUT_L>(T.llut, T.lm, T.lsorted);
-    fill_lut<LUT_D>(T.dlut, T.dm, T.dsorted);
+    fill_lut32<LUT_L, false>(T.llut, T.lm, T.lsorted);
+    fill_lut32<LUT_D, true>(T.dlut, T.dm, T.dsorted);
     wave_sync();
 }
 
-// code-length sequence(s) (inflate.hpp:166-206).  Reference mode: called once per sequence,
-// last literal length starts at 0, a repeat may overshoot (entries keep their index as the
-// symbol value).  RFC mode: one call over both sequences (nb > 0).  Returns SEGF_* or 0 and
-// the number of entries written to a (and b).
-template <class BR>
-__device__ uint32_t read_code_lengths(BR& br, const Tables& T, uint8_t* a, uint32_t na,
-                                      uint8_t* b, uint32_t nb, bool rfc, uint32_t* outa,
-                                      uint32_t* outb) {
-    const int lane = lane_id();
-    const uint32_t total = na + nb;
-    const uint32_t cap = rfc ? total : 300;
-    uint32_t i = 0, last = 0;
-    while (i < total) {
-        br.ensure(14);
-        const uint16_t e = T.plut[br.peek(7)];
-        if (!e) return SEGF_ERR_DATA;
-        br.consume(e >> 9);
-        const uint32_t s = e & 511;
-        uint32_t rep, val;
-        if (s == 16) {
-            if (rfc && i == 0) return SEGF_ERR_DATA;
-            rep = 3 + br.bits(2);
-            val = last;
-        } else if (s == 17) {
-            rep = 3 + br.bits(3);
-            val = 0;
-        } else if (s == 18) {
-            rep = 11 + br.bits(7);
-            val = 0;
-        } else {
-            rep = 1;
-            val = s;
-        }
-        if (rfc || s < 16) last = val;
-        if (br.over()) return SEGF_OVERREAD;
-        if (i + rep > cap) {
-            if (rfc || val != 0) return SEGF_ERR_DATA;  // reference: value >= 300 is UB
-        }
-        for (uint32_t j = lane; j < rep; j += 64) {
-            const uint32_t idx = i + j;
-            if (idx < cap) {
-                if (!rfc || idx < na) a[idx] = (uint8_t)val;  // reference: overshoot entries
-                else b[idx - na] = (uint8_t)val;               // keep their index as value
-            }
-        }
-        i += rep;
-    }
-    wave_sync();
-    if (!rfc) {
-        *outa = min(i, 300u);
-        *outb = 0;
-    } else {
-        *outa = na;
-        *outb = nb;
-    }
-    return 0;
-}
-
-template <class BR>
-__device__ uint32_t read_dynamic_header(BR& br, Tables& T, bool rfc, bool fill = true) {
-    const int lane = lane_id();
-    br.ensure(14);
-    const uint32_t hlit = br.bits(5), hdist = br.bits(5), hclen = br.bits(4);
-    if (lane < 32) T.plen[lane] = 0;
-    wave_sync();
-    for (uint32_t i = 0; i < hclen + 4; i++) {
-        const uint32_t v = br.bits(3);
-        if (lane == 0) T.plen[kPerm[i]] = (uint8_t)v;
-    }
-    if (br.over()) return SEGF_OVERREAD;
-    wave_sync();
-    build_tree(T.plen, 19, T.psorted, T.pm);
-    fill_prelut(T.plut, T.pm, T.psorted);
-    wave_sync();
-    uint32_t nl, nd, err;
-    if (!rfc) {
-        uint32_t dummy;
-        err = read_code_lengths(br, T, T.llen, 257 + hlit, nullptr, 0, false, &nl, &dummy);
-        if (err) return err;
-        err = read_code_lengths(br, T, T.dlen, 1 + hdist, nullptr, 0, false, &nd, &dummy);
-        if (err) return err;
-    } else {
-        err = read_code_lengths(br, T, T.llen, 257 + hlit, T.dlen, 1 + hdist, true, &nl, &nd);
-        if (err) return err;
-    }
-    build_tree(T.llen, nl, T.lsorted, T.lm);
-    build_tree(T.dlen, nd, T.dsorted, T.dm);
-    if (fill) {
-        fill_lut<LUT_L>(T.llut, T.lm, T.lsorted);
-        fill_lut<LUT_D>(T.dlut, T.dm, T.dsorted);
-    }
-    wave_sync();
-    return 0;
-}
 
 // ---------------------------------------------------------------------------------------
-// Wave-level dynamic header reader (inflate.hpp:136-224 semantics, as read_code_lengths
-// above).  The 64 lanes hold a 2048-bit window of the stream, one word each; every step
+// Wave-level dynamic header reader (inflate.hpp:136-224).  Reference mode: the lit/len and
+// distance code lengths are two sequences, each with its own count and overshoot (entries keep
+// their index as the symbol value), and 16 repeats the last literal length, which starts at 0
+// per sequence (A-11, A-12); RFC mode: one sequence, 16 repeats the previous length.  The 64 lanes hold a 2048-bit window of the stream, one word each; every step
 // decodes the precode symbol (and its repeat bits) at 64 consecutive bit offsets at once, and
 // the true symbol chain is then walked with v_readlane -- a few scalar instructions per code
 // length instead of a dependent bit-reader refill + table lookup.
@@ -376,11 +342,70 @@ struct GlobalWords {  // stream words in HBM, masked at the stream end
         return lim >= 4 ? v : v & ((1u << (8 * lim)) - 1u);
     }
 };
+struct BitInWords {  // the words a BitIn reads (LDS-staged range, else HBM), masked at the end
+    const uint32_t* sw;
+    uint64_t sws, snw;
+    const uint32_t* w;
+    uint64_t nwords, end_bytes;
+    __device__ uint32_t word(uint64_t i) const {
+        if (i >= nwords) return 0u;
+        const uint32_t v = i - sws < snw ? sw[i - sws] : w[i];
+        const uint64_t lim = end_bytes - 4 * i;
+        return lim >= 4 ? v : v & ((1u << (8 * lim)) - 1u);
+    }
+};
 struct StagedWords {  // words [ws, ws + nw) staged in LDS (already masked)
     const uint32_t* w;
     uint64_t ws, nw;
     __device__ uint32_t word(uint64_t i) const { return (i >= ws && i < ws + nw) ? w[i - ws] : 0u; }
 };
+__device__ __forceinline__ BitInWords reader_words(const BitIn& br) {
+    return BitInWords{br.sw, br.sws, br.snw, br.w, br.nwords, br.end_bytes};
+}
+
+// Wave-uniform bit reader over a candidate staged whole in LDS (words [ws, ws + nw), masked at
+// the stream end, zero-padded): a 32-bit relative position and one ds_read2 + alignbit per
+// 32-bit window, instead of BitIn's 64-bit buffer and refill bookkeeping.
+struct StageReader {
+    const uint32_t* w;
+    uint64_t ws;
+    uint32_t nw;
+    uint32_t p;     // bits relative to ws * 32
+    uint32_t endp;  // stream end, same origin (clamped)
+    uint64_t end_bytes, end_bits;
+
+    __device__ void init(const uint32_t* lds, uint64_t first, uint32_t count, uint64_t misalign, uint64_t n) {
+        w = lds;
+        ws = first;
+        nw = count;
+        end_bytes = misalign + n;
+        end_bits = end_bytes * 8;
+        const uint64_t e = end_bits - first * 32;
+        endp = e > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)e;
+    }
+    __device__ uint32_t window32() const {
+        const uint32_t i = p >> 5;
+        return __builtin_amdgcn_alignbit(w[i + 1], w[i], p & 31);
+    }
+    __device__ void ensure(uint32_t) {}
+    __device__ void consume(uint32_t k) { p += k; }
+    __device__ uint32_t bits(uint32_t k) {
+        const uint32_t v = window32() & ((1u << k) - 1u);
+        p += k;
+        return v;
+    }
+    __device__ void align() { p = (p + 7) & ~7u; }
+    __device__ bool over() const { return p > endp; }
+    __device__ uint64_t abspos() const { return ws * 32 + p; }
+    __device__ void seek(uint64_t abs) { p = (uint32_t)(abs - ws * 32); }
+    __device__ uint8_t byte_at(uint64_t b) const {
+        const uint32_t r = (uint32_t)(b - ws * 4);
+        return (uint8_t)(w[r >> 2] >> ((r & 3) * 8));
+    }
+    __device__ StagedWords words() const { return StagedWords{w, ws, nw}; }
+};
+
+__device__ __forceinline__ StagedWords reader_words(const StageReader& br) { return br.words(); }
 
 // 32 bits at window bit b; every lane passes its own b (all lanes must be active)
 __device__ __forceinline__ uint32_t win_bits(uint32_t win, uint32_t b) {
@@ -540,8 +565,8 @@ __device__ uint32_t fast_header(const Src& src, uint64_t* pos_io, uint64_t end_b
     wave_sync();
     FH_STAMP(2);
     if (fill) {
-        fill_lut<LUT_L>(T.llut, T.lm, T.lsorted);
-        fill_lut<LUT_D>(T.dlut, T.dm, T.dsorted);
+        fill_lut32<LUT_L, false>(T.llut, T.lm, T.lsorted);
+        fill_lut32<LUT_D, true>(T.dlut, T.dm, T.dsorted);
     }
     wave_sync();
     FH_STAMP(3);
@@ -552,19 +577,48 @@ __device__ uint32_t fast_header(const Src& src, uint64_t* pos_io, uint64_t end_b
 // periodic LZ77 copy: out[pos + i] = out[pos - dist + (i mod dist)], i < L (equal to the
 // reference's byte-serial overlapping copy, inflate.hpp:268-270); every source byte lies
 // before pos, so all lanes copy independently.
+// Four independent byte reads per lane are issued before the writes (one LDS latency per
+// 256 bytes); the modulo bookkeeping needs a division only for distances below 64.
 template <uint32_t MASK>
 __device__ __forceinline__ void lz_copy_lds(uint8_t* win, uint32_t pos, uint32_t L, uint32_t dist) {
     const uint32_t lane = lane_id();
     const uint32_t src = pos - dist;
     if (dist >= L) {
-        for (uint32_t i = lane; i < L; i += 64) win[(pos + i) & MASK] = win[(src + i) & MASK];
+        for (uint32_t i0 = 0; i0 < L; i0 += 256) {
+            uint8_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t i = i0 + u * 64 + lane;
+                v[u] = i < L ? win[(src + i) & MASK] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t i = i0 + u * 64 + lane;
+                if (i < L) win[(pos + i) & MASK] = v[u];
+            }
+        }
     } else {
         uint32_t r = dist >= 64 ? lane : lane % dist;
         const uint32_t step = dist >= 64 ? 64 : 64 % dist;
-        for (uint32_t i = lane; i < L; i += 64) {
-            win[(pos + i) & MASK] = win[(src + r) & MASK];
-            r += step;
-            if (r >= dist) r -= dist;
+        for (uint32_t i0 = 0; i0 < L; i0 += 256) {
+            uint8_t v[4];
+            uint32_t rr[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                rr[u] = r;
+                r += step;
+                if (r >= dist) r -= dist;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t i = i0 + u * 64 + lane;
+                v[u] = i < L ? win[(src + rr[u]) & MASK] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t i = i0 + u * 64 + lane;
+                if (i < L) win[(pos + i) & MASK] = v[u];
+            }
         }
     }
 }
@@ -593,7 +647,8 @@ struct SegSink {
         pos += L;
         return true;
     }
-    __device__ bool stored(const BitIn& br, uint64_t b0, uint32_t len) {
+    template <class BR>
+    __device__ bool stored(const BR& br, uint64_t b0, uint32_t len) {
         if (pos + len > SEG_CAP) { err |= SEGF_OVERFLOW; return false; }
         for (uint32_t i = lane_id(); i < len; i += 64) win[pos + i] = br.byte_at(b0 + i);
         pos += len;
@@ -638,7 +693,8 @@ struct RingSink {
         pos += L;
         return true;
     }
-    __device__ bool stored(const BitIn& br, uint64_t b0, uint32_t len) {
+    template <class BR>
+    __device__ bool stored(const BR& br, uint64_t b0, uint32_t len) {
         if (!count_only) {
             for (uint32_t i = lane_id(); i < len; i += 64) {
                 const uint8_t v = br.byte_at(b0 + i);
@@ -651,48 +707,42 @@ struct RingSink {
     }
 };
 
-// decompressHuffmanBlock (inflate.hpp:226-275) with table lookups
-template <class Sink>
-__device__ uint32_t decode_huffman(BitIn& br, const Tables& T, Sink& sk) {
+// decompressHuffmanBlock (inflate.hpp:226-275) with 32-bit table entries: one 32-bit window
+// per half token (code + extra bits), no per-symbol base / extra arithmetic.
+template <class BR, class Sink>
+__device__ uint32_t decode_huffman(BR& br, const Tables& T, Sink& sk) {
     for (;;) {
-        br.ensure(20);
-        uint32_t v = br.peek(15);
+        uint32_t v = br.window32();
         uint32_t e = T.llut[v & ((1u << LUT_L) - 1)];
-        uint32_t sym, len;
-        if (e) {
-            sym = e & 511;
-            len = e >> 9;
-        } else if (!slow_decode(T.lm, T.lsorted, v, LUT_L + 1, &sym, &len)) {
-            return SEGF_ERR_DATA;
+        if (!e) {
+            uint32_t sym, len;
+            if (!slow_decode(T.lm, T.lsorted, v & 0x7FFF, LUT_L + 1, &sym, &len)) return SEGF_ERR_DATA;
+            e = lit_entry(sym, len);
         }
-        br.consume(len);
-        if (sym < 256) {
+        const uint32_t cl = e & 15, ty = (e >> 4) & 3;
+        if (ty == 0) {
+            br.consume(cl);
             if (br.over()) return SEGF_OVERREAD;
-            if (!sk.literal(sym)) return sk.err;
+            if (!sk.literal(e >> 16)) return sk.err;
             continue;
         }
-        if (sym == 256) return br.over() ? SEGF_OVERREAD : 0;
-        uint32_t L = 0;
-        if (sym <= 285) {
-            const uint32_t ex = len_extra(sym);
-            L = len_base(sym) + (ex ? br.bits(ex) : 0);
+        if (ty == 1) {
+            br.consume(cl);
+            return br.over() ? SEGF_OVERREAD : 0;
         }
-        br.ensure(28);
-        v = br.peek(15);
-        e = T.dlut[v & ((1u << LUT_D) - 1)];
-        uint32_t ds, dl;
-        if (e) {
-            ds = e & 511;
-            dl = e >> 9;
-        } else if (!slow_decode(T.dm, T.dsorted, v, LUT_D + 1, &ds, &dl)) {
-            return SEGF_ERR_DATA;
+        const uint32_t ex = (e >> 6) & 15;
+        const uint32_t L = (e >> 16) + ((v >> cl) & ((1u << ex) - 1u));
+        br.consume(cl + ex);
+        v = br.window32();
+        uint32_t de = T.dlut[v & ((1u << LUT_D) - 1)];
+        if (!de) {
+            uint32_t ds, dl;
+            if (!slow_decode(T.dm, T.dsorted, v & 0x7FFF, LUT_D + 1, &ds, &dl)) return SEGF_ERR_DATA;
+            de = dist_entry(ds, dl);
         }
-        br.consume(dl);
-        uint32_t dist = 0;
-        if (ds < 30) {
-            const uint32_t ex = dist_extra(ds);
-            dist = dist_base(ds) + (ex ? br.bits(ex) : 0);
-        }
+        const uint32_t dl = de & 15, dx = (de >> 6) & 15;
+        const uint32_t dist = (de >> 16) + ((v >> dl) & ((1u << dx) - 1u));
+        br.consume(dl + dx);
         if (br.over()) return SEGF_OVERREAD;
         if (!sk.copy(L, dist)) return sk.err;
     }
@@ -700,8 +750,8 @@ __device__ uint32_t decode_huffman(BitIn& br, const Tables& T, Sink& sk) {
 
 // realDecompress (inflate.hpp:277-322).  With stop_at_marker the segment ends at an empty,
 // non-final stored block whose NLEN is FFFF (the "00 00 FF FF" the scanner keyed on).
-template <class Sink>
-__device__ uint32_t inflate_blocks(BitIn& br, Tables& T, Sink& sk, bool rfc, bool stop_at_marker,
+template <class BR, class Sink>
+__device__ uint32_t inflate_blocks(BR& br, Tables& T, Sink& sk, bool rfc, bool stop_at_marker,
                                    uint64_t* end_byte, bool* fin, uint64_t* hdr_cycles = nullptr) {
     *fin = false;
     for (;;) {
@@ -715,14 +765,14 @@ __device__ uint32_t inflate_blocks(BitIn& br, Tables& T, Sink& sk, bool rfc, boo
             const uint32_t len = br.bits(16);
             const uint32_t nlen = br.bits(16);
             if (br.over()) return SEGF_OVERREAD;
-            const uint64_t b0 = br.pos >> 3;
+            const uint64_t b0 = br.abspos() >> 3;
             if (stop_at_marker && !bfinal && len == 0 && nlen == 0xFFFF) {
                 *end_byte = b0;
                 return 0;
             }
             if (b0 + len > br.end_bytes) return SEGF_OVERREAD;
             if (!sk.stored(br, b0, len)) return sk.err;
-            br.seek(br.pos + 8ull * len);
+            br.seek(br.abspos() + 8ull * len);
             wave_sync();
         } else if (btype == 1) {
             if (!T.fixed_loaded) {
@@ -734,9 +784,9 @@ __device__ uint32_t inflate_blocks(BitIn& br, Tables& T, Sink& sk, bool rfc, boo
         } else if (btype == 2) {
             T.fixed_loaded = 0;
             const uint64_t h0 = hdr_cycles ? __builtin_amdgcn_s_memtime() : 0;
-            uint64_t hp = br.pos;
-            const GlobalWords src{br.w, br.nwords, br.end_bytes};
-            uint32_t err = fast_header(src, &hp, br.end_bits, T, rfc, true, hdr_cycles ? hdr_cycles + 1 : nullptr);
+            uint64_t hp = br.abspos();
+            uint32_t err = fast_header(reader_words(br), &hp, br.end_bits, T, rfc, true,
+                                       hdr_cycles ? hdr_cycles + 1 : nullptr);
             if (hdr_cycles) *hdr_cycles += __builtin_amdgcn_s_memtime() - h0;
             if (err) return err;
             br.seek(hp);
@@ -745,7 +795,7 @@ __device__ uint32_t inflate_blocks(BitIn& br, Tables& T, Sink& sk, bool rfc, boo
         }  // btype 3: no-op block (inflate.hpp:292 has no case 3)
         if (bfinal) {
             *fin = true;
-            *end_byte = (br.pos + 7) >> 3;
+            *end_byte = (br.abspos() + 7) >> 3;
             return 0;
         }
     }
@@ -839,6 +889,7 @@ constexpr unsigned long long LB_A = 1ull << 62, LB_P = 2ull << 62, LB_V = (1ull 
 __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t win[SEG_CAP + 16];
     __shared__ Tables T;
+    __shared__ uint32_t stg[IF_STAGE];
     __shared__ unsigned long long s_j, s_excl;
     const int lane = threadIdx.x;
     // dynamic segment index: workgroups that start earlier take earlier segments, so a
@@ -853,14 +904,54 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
     const uint64_t start = A.cands[j];
     uint64_t hdr_cycles[5] = {0, 0, 0, 0, 0};
 
-    BitIn br;
-    br.init(A.in_words, A.misalign, A.n);
-    br.seek((A.misalign + start) * 8);
+    // stage IF_STAGE - 2 words from the candidate on in LDS (masked at the stream end, two zero
+    // words after).  When the next candidate lies inside the stage the segment is read by
+    // StageReader; if that read ever came within 32 bits of the stage end (a false marker made
+    // the segment look short), or the segment is long, it is read by BitIn.
+    const uint64_t end_bytes = A.misalign + A.n;
+    const uint64_t nwords = (end_bytes + 3) / 4;
+    const uint64_t ws = (A.misalign + start) >> 2;
+    const uint64_t nextb = j + 1 < A.ncand ? A.cands[j + 1] : A.n;
+    const uint64_t we = min((A.misalign + nextb + 3) / 4 + 2, nwords);
+    const uint32_t nst = (uint32_t)min((uint64_t)IF_STAGE - 2, nwords - ws);
+    const bool to_end = ws + nst == nwords;
+    for (uint32_t i = lane; i < nst + 2; i += IF_NT) {
+        uint32_t v = 0;
+        if (i < nst) {
+            const uint64_t wi = ws + i;
+            v = A.in_words[wi];
+            const uint64_t lim = end_bytes - 4 * wi;
+            if (lim < 4) v &= (1u << (8 * lim)) - 1u;
+        }
+        stg[i] = v;
+    }
+    __syncthreads();
     SegSink sk{win, 0, j == 0, 0};
     uint64_t end_byte = 0;
     bool fin = false;
-    uint32_t err = inflate_blocks(br, T, sk, (A.flags & DMX_CFG_RFC_STRICT) != 0, true, &end_byte, &fin,
-                                  A.dbg ? hdr_cycles : nullptr);
+    const bool rfc = (A.flags & DMX_CFG_RFC_STRICT) != 0;
+    uint32_t err = 0;
+    bool staged = we - ws + 2 <= (uint64_t)nst + 2;
+    if (staged) {
+        StageReader br;
+        br.init(stg, ws, nst, A.misalign, A.n);
+        br.seek((A.misalign + start) * 8);
+        err = inflate_blocks(br, T, sk, rfc, true, &end_byte, &fin, A.dbg ? hdr_cycles : nullptr);
+        if (!to_end && br.p + 32 > nst * 32) staged = false;  // read past the stage: redo
+    }
+    if (!staged) {
+        sk.pos = 0;
+        sk.err = 0;
+        fin = false;
+        end_byte = 0;
+        T.fixed_loaded = 0;
+        wave_sync();
+        BitIn br;
+        br.init(A.in_words, A.misalign, A.n);
+        br.stage(stg, ws, nst);
+        br.seek((A.misalign + start) * 8);
+        err = inflate_blocks(br, T, sk, rfc, true, &end_byte, &fin, A.dbg ? hdr_cycles : nullptr);
+    }
     const uint32_t size = err ? 0 : sk.pos;
     DMX_PHASE(A.dbg, j, 1);
     if (A.dbg && lane_id() == 0)
@@ -992,58 +1083,6 @@ struct PjSmem {
     uint64_t sb0;
     uint32_t total;
     uint64_t end_byte;
-};
-
-// wave-uniform bit reader over the staged words (same contract as BitIn)
-struct LdsBitIn {
-    const uint32_t* w;
-    uint64_t ws, nw;
-    uint64_t nwords, end_bytes, end_bits;
-    uint64_t pos;
-    uint64_t buf;
-    uint32_t cnt;
-    uint64_t wi;
-
-    __device__ void init(const uint32_t* lds, uint64_t first, uint64_t count, uint64_t misalign, uint64_t n) {
-        w = lds;
-        ws = first;
-        nw = count;
-        end_bytes = misalign + n;
-        end_bits = end_bytes * 8;
-        nwords = (end_bytes + 3) / 4;
-    }
-    __device__ uint32_t raw(uint64_t i) const { return (i >= ws && i < ws + nw) ? w[i - ws] : 0u; }
-    __device__ void refill() {
-        if (cnt <= 32) {
-            buf |= (uint64_t)raw(wi) << cnt;  // staged words are already masked at the stream end
-            cnt += 32;
-            wi++;
-        }
-    }
-    __device__ void seek(uint64_t bitpos) {
-        pos = bitpos;
-        const uint64_t i = bitpos >> 5;
-        buf = (uint64_t)(raw(i) >> (bitpos & 31));
-        cnt = 32 - (uint32_t)(bitpos & 31);
-        wi = i + 1;
-        refill();
-    }
-    __device__ void ensure(uint32_t k) {
-        if (cnt < k) refill();
-    }
-    __device__ uint32_t peek(uint32_t k) const { return (uint32_t)buf & ((1u << k) - 1u); }
-    __device__ void consume(uint32_t k) {
-        buf >>= k;
-        cnt -= k;
-        pos += k;
-    }
-    __device__ uint32_t bits(uint32_t k) {
-        ensure(k);
-        const uint32_t v = peek(k);
-        consume(k);
-        return v;
-    }
-    __device__ bool over() const { return pos > end_bits; }
 };
 
 // 32 bits at bit p of the staged words (LSB = bit p)
