@@ -71,8 +71,106 @@ __device__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* tot
 // Zero or one used symbol -> two codes of length 1 (complete code, as zlib emits).
 // Stands in for FlatHuffmanTree::generateCodeLengths (common.hpp:322-404), a serial
 // priority-queue Huffman; this one stays within ~1% of optimal.
-__device__ void wave_build_lengths(const uint32_t* freq, int nsym, int maxbits, uint8_t* lens) {
+// Kraft repair and slack fill on the class sizes cnt[1..15] of a code whose lengths are
+// non-decreasing in frequency rank: lengthen the last (least frequent) members of a class while
+// the code is over-full, then shorten the first (most frequent) members while slack remains.
+// Ends with a complete code (Kraft sum exactly 2^maxbits), as zlib and the reference require.
+__device__ __forceinline__ void fit_classes(uint32_t (&cnt)[17], int maxbits) {
+    const uint32_t U = 1u << maxbits;
+    int64_t K = 0;
+#pragma unroll
+    for (int L = 1; L <= 15; L++) K += (int64_t)cnt[L] * (int64_t)(U >> L);
+    while (K > (int64_t)U) {
+#pragma unroll
+        for (int L = 14; L >= 1; L--) {
+            if (L < maxbits && K > (int64_t)U && cnt[L]) {
+                const int64_t gain = U >> (L + 1);
+                const int64_t need = (K - (int64_t)U + gain - 1) / gain;
+                const uint32_t k = (uint32_t)min(need, (int64_t)cnt[L]);
+                cnt[L] -= k;
+                cnt[L + 1] += k;
+                K -= (int64_t)k * gain;
+            }
+        }
+    }
+    uint32_t R = (uint32_t)((int64_t)U - K);
+    for (int pass = 0; pass < 64 && R; pass++) {
+        bool changed = false;
+#pragma unroll
+        for (int L = 2; L <= 15; L++) {
+            const uint32_t c = U >> L;
+            if (L <= maxbits && cnt[L] && c <= R) {
+                const uint32_t k = min(cnt[L], R / c);
+                cnt[L] -= k;
+                cnt[L - 1] += k;
+                R -= k * c;
+                changed = true;
+            }
+        }
+        if (!changed) break;
+    }
+}
+
+// initial length round(log2(F/f)) clamped to [1, maxbits] (0 for f == 0)
+__device__ __forceinline__ uint32_t init_len(uint32_t f, uint32_t F, int maxbits) {
+    if (!f) return 0;
+    const uint32_t L0 = 31 - __clz(F / f);
+    const uint64_t a = (uint64_t)f << (L0 + 1);
+    const uint32_t L = L0 + ((a * a <= 2ull * F * F) ? 1u : 0u);
+    return max(1u, min((uint32_t)maxbits, L));
+}
+
+// the same for at most 64 symbols (precode, distance code): one key per lane, 64-key sort
+__device__ void wave_build_lengths64(const uint32_t* freq, int nsym, int maxbits, uint8_t* lens) {
     const int lane = lane_id();
+    const uint32_t f = lane < nsym ? freq[lane] : 0;
+    uint32_t key = f ? (f << 9) | (511 - lane) : 0;
+    if (lane < nsym) lens[lane] = 0;
+    const uint32_t F = wave_sum(f);
+    const uint64_t nzm = __ballot(f != 0);
+    if (__popcll(nzm) <= 1) {
+        const uint32_t u = nzm ? 64 - __clzll(nzm) : 0;  // highest used symbol + 1
+        if (lane == 0) {
+            if (u == 0) { lens[0] = 1; lens[1] = 1; }
+            else { lens[u - 1] = 1; lens[u - 1 == 0 ? 1 : 0] = 1; }
+        }
+        return;
+    }
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            const uint32_t o = __shfl_xor(key, stride, 64);
+            const bool lower = (lane & stride) == 0;
+            const bool desc = (lane & size) == 0;
+            key = (lower == desc) ? max(key, o) : min(key, o);
+        }
+    }
+    const uint32_t L0 = init_len(key >> 9, F, maxbits);
+    uint32_t cnt[17];
+    cnt[0] = cnt[16] = 0;
+#pragma unroll
+    for (int L = 1; L <= 15; L++) cnt[L] = __popcll(__ballot(L0 == (uint32_t)L));
+    fit_classes(cnt, maxbits);
+    uint32_t S = 0, L = 0;
+#pragma unroll
+    for (int l = 1; l <= 15; l++) {
+        L += (uint32_t)lane >= S ? 1u : 0u;
+        S += cnt[l];
+    }
+    if (key >> 9) lens[511 - (key & 511)] = (uint8_t)L;
+}
+
+__device__ void wave_build_lengths(const uint32_t* freq, int nsym, int maxbits, uint8_t* lens,
+                                   uint64_t* st = nullptr) {
+    const int lane = lane_id();
+    uint64_t t0 = st ? __builtin_amdgcn_s_memtime() : 0;
+#define WB_STAMP(k)                                       \
+    if (st && lane == 0) {                                \
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(); \
+        st[k] = t1 - t0;                                  \
+        t0 = t1;                                          \
+    }
     uint32_t key[8];
     uint32_t fs = 0, nzs = 0, used = 0;
 #pragma unroll
@@ -97,82 +195,46 @@ __device__ void wave_build_lengths(const uint32_t* freq, int nsym, int maxbits, 
         }
         return;
     }
+    WB_STAMP(0);
     wave_sort512_desc(key);
+    WB_STAMP(1);
+    // Initial lengths round(log2(F/f)) clamped to [1, maxbits].  Frequencies are sorted in
+    // descending order by rank (rank = lane * 8 + r), so the lengths are non-decreasing in rank
+    // and every length class is a contiguous rank range.  The Kraft repair (lengthen the least
+    // frequent members of a class) and the slack fill (shorten the most frequent ones) keep
+    // that property, so both run on the 15 class sizes alone, in scalar code.
     uint32_t len[8];
-    bool val[8];
-    uint32_t ks = 0;
+#pragma unroll
+    for (int r = 0; r < 8; r++) len[r] = init_len(key[r] >> 9, F, maxbits);
+    WB_STAMP(2);
+    uint32_t cnt[17];
+    cnt[0] = cnt[16] = 0;
+#pragma unroll
+    for (int L = 1; L <= 15; L++) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int r = 0; r < 8; r++) c += __popcll(__ballot(len[r] == (uint32_t)L));
+        cnt[L] = c;
+    }
+    WB_STAMP(3);
+    fit_classes(cnt, maxbits);
+    WB_STAMP(4);
+    // rank q has length = number of classes l in [1, 15] whose first rank S_l <= q
+    uint32_t S[16];
+    S[1] = 0;
+#pragma unroll
+    for (int L = 2; L <= 15; L++) S[L] = S[L - 1] + cnt[L - 1];
 #pragma unroll
     for (int r = 0; r < 8; r++) {
-        const uint32_t f = key[r] >> 9;
-        val[r] = f != 0;
+        if (!(key[r] >> 9)) continue;
+        const uint32_t q = (uint32_t)lane * 8 + r;
         uint32_t L = 0;
-        if (f) {
-            const uint32_t L0 = 31 - __clz(F / f);
-            const uint64_t a = (uint64_t)f << (L0 + 1);
-            L = L0 + ((a * a <= 2ull * F * F) ? 1u : 0u);
-            L = max(1u, min((uint32_t)maxbits, L));
-            ks += U >> L;
-        }
-        len[r] = L;
+#pragma unroll
+        for (int l = 1; l <= 15; l++) L += q >= S[l] ? 1u : 0u;
+        lens[511 - (key[r] & 511)] = (uint8_t)L;
     }
-    uint32_t K = wave_sum(ks);
-    const uint64_t ltmask = (1ull << lane) - 1ull;
-    // class L members: ballots per register slot give the class size and each member's
-    // position in rank order (rank = lane * 8 + r)
-    auto class_scan = [&](uint32_t L, uint32_t (&pos)[8], uint32_t& total) {
-        uint64_t B[8];
-        total = 0;
-        uint32_t below = 0;
-#pragma unroll
-        for (int r = 0; r < 8; r++) {
-            B[r] = __ballot(val[r] && len[r] == L);
-            total += __popcll(B[r]);
-            below += __popcll(B[r] & ltmask);
-        }
-        uint32_t run = below;
-#pragma unroll
-        for (int r = 0; r < 8; r++) {
-            pos[r] = run;
-            run += (uint32_t)((B[r] >> lane) & 1ull);
-        }
-    };
-    // Kraft repair (over-full after rounding / clamping): lengthen lowest-frequency codes
-    while (K > U) {
-        for (int L = maxbits - 1; L >= 1 && K > U; L--) {
-            const uint32_t gain = U >> (L + 1);
-            const uint32_t need = (K - U + gain - 1) / gain;
-            uint32_t pos[8], total;
-            class_scan(L, pos, total);
-            const uint32_t k = min(need, total);
-            if (!k) continue;
-#pragma unroll
-            for (int r = 0; r < 8; r++)
-                if (val[r] && len[r] == (uint32_t)L && pos[r] >= total - k) len[r] = L + 1;
-            K -= k * gain;
-        }
-    }
-    // slack fill: shorten the most frequent codes of each class while the budget allows
-    uint32_t R = U - K;
-    for (int pass = 0; pass < 64 && R; pass++) {
-        bool changed = false;
-        for (int L = 2; L <= maxbits && R; L++) {
-            const uint32_t c = U >> L;
-            if (c > R) continue;
-            uint32_t pos[8], total;
-            class_scan(L, pos, total);
-            const uint32_t k = min(total, R / c);
-            if (!k) continue;
-            changed = true;
-            R -= k * c;
-#pragma unroll
-            for (int r = 0; r < 8; r++)
-                if (val[r] && len[r] == (uint32_t)L && pos[r] < k) len[r] = L - 1;
-        }
-        if (!changed) break;
-    }
-#pragma unroll
-    for (int r = 0; r < 8; r++)
-        if (val[r]) lens[511 - (key[r] & 511)] = (uint8_t)len[r];
+    WB_STAMP(5);
+#undef WB_STAMP
 }
 
 // Canonical codes (RFC 1951 3.2.2; reference FlatHuffmanTree::construct common.hpp:104-145),
@@ -407,12 +469,15 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t
 
     // ---- code lengths + canonical codes (wave 0: lit/len, wave 1: distance) -------------
     if (t < 64) {
-        wave_build_lengths(S.litfreq, 286, 15, S.litlen);
+        uint64_t wst[6] = {0, 0, 0, 0, 0, 0};
+        wave_build_lengths(S.litfreq, 286, 15, S.litlen, dbg ? wst : nullptr);
+        if (dbg && t == 0) dbg[seg * kPhaseSlots + 11] = (wst[0] & 0xFFFF) | ((wst[1] & 0xFFFF) << 16) | ((wst[3] & 0xFFFF) << 32) | ((wst[4] & 0xFFFF) << 48);
+        if (dbg && t == 0) dbg[seg * kPhaseSlots + 15] = (wst[2] & 0xFFFF) | ((wst[5] & 0xFFFF) << 16);
         DMX_PHASE(dbg, seg, 12);
         wave_assign_codes(S.litlen, 286, S.litcode);
         DMX_PHASE(dbg, seg, 13);
     } else if (t < 128) {
-        wave_build_lengths(S.distfreq, 30, 15, S.distlen);
+        wave_build_lengths64(S.distfreq, 30, 15, S.distlen);
         wave_assign_codes(S.distlen, 30, S.distcode);
     }
     if (t < 8) S.sh[32 + t] = 0;
@@ -477,7 +542,7 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t
     }
     __syncthreads();
     if (t < 64) {
-        wave_build_lengths(S.prefreq, 19, 7, S.prelen);
+        wave_build_lengths64(S.prefreq, 19, 7, S.prelen);
         wave_assign_codes(S.prelen, 19, S.precode);
     }
     __syncthreads();

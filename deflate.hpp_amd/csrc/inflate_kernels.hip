@@ -206,35 +206,6 @@ __device__ __forceinline__ bool key_hit(const TreeMeta& m, uint32_t k, uint32_t 
     return true;
 }
 
-// primary LUT over PB bits: entry = sym | (len << 9), 0 = no code of length <= PB matches
-template <int PB>
-__device__ void fill_lut(uint16_t* lut, const TreeMeta& m, const uint16_t* sorted) {
-    uint32_t lo[PB + 1], hi[PB + 1], cn[PB + 1], of[PB + 1];
-#pragma unroll
-    for (int k = 1; k <= PB; k++) {
-        lo[k] = m.lo[k];
-        hi[k] = m.hi[k];
-        cn[k] = m.cnt[k];
-        of[k] = m.offs[k];
-    }
-    for (int wv = lane_id(); wv < (1 << PB); wv += 64) {
-        const uint32_t v = bitrev(wv, PB);
-        uint32_t idx = 0, len = 0;
-#pragma unroll
-        for (int k = 1; k <= PB; k++) {
-            const uint32_t x = v >> (PB - k);
-            if (!len && cn[k] && x <= hi[k]) {
-                const uint32_t cm = x + (((hi[k] - x) >> k) << k);
-                if (cm >= lo[k]) {
-                    idx = of[k] + cm - lo[k];
-                    len = k;
-                }
-            }
-        }
-        lut[wv] = len ? (uint16_t)(sorted[idx] | (len << 9)) : (uint16_t)0;
-    }
-}
-
 // 32-bit decode entries: bits 0-3 code length, 4-5 class (0 literal, 1 end of block, 2 length),
 // 6-9 extra-bit count, 16-31 literal byte / length base / distance base.  Length symbols 286+
 // decode as length 0 and distance symbols 30+ as distance 0 (no copy, inflate.hpp:243-270).
@@ -332,16 +303,6 @@ __device__ void load_fixed(Tables& T) {
 // the true symbol chain is then walked with v_readlane -- a few scalar instructions per code
 // length instead of a dependent bit-reader refill + table lookup.
 // ---------------------------------------------------------------------------------------
-struct GlobalWords {  // stream words in HBM, masked at the stream end
-    const uint32_t* w;
-    uint64_t nwords, end_bytes;
-    __device__ uint32_t word(uint64_t i) const {
-        if (i >= nwords) return 0u;
-        const uint64_t lim = end_bytes - 4 * i;
-        const uint32_t v = w[i];
-        return lim >= 4 ? v : v & ((1u << (8 * lim)) - 1u);
-    }
-};
 struct BitInWords {  // the words a BitIn reads (LDS-staged range, else HBM), masked at the end
     const uint32_t* sw;
     uint64_t sws, snw;
