@@ -140,7 +140,15 @@ __device__ void wave_build_lengths64(const uint32_t* freq, int nsym, int maxbits
     for (int size = 2; size <= 64; size <<= 1) {
 #pragma unroll
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            const uint32_t o = __shfl_xor(key, stride, 64);
+            uint32_t o;
+            switch (stride) {
+                case 1: o = xor_lane<1>(key); break;
+                case 2: o = xor_lane<2>(key); break;
+                case 4: o = xor_lane<4>(key); break;
+                case 8: o = xor_lane<8>(key); break;
+                case 16: o = xor_lane<16>(key); break;
+                default: o = xor_lane<32>(key); break;
+            }
             const bool lower = (lane & stride) == 0;
             const bool desc = (lane & size) == 0;
             key = (lower == desc) ? max(key, o) : min(key, o);

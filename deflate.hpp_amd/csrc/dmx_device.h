@@ -92,6 +92,39 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 
 // Sorts 512 keys held as k[8] per lane (element index = lane * 8 + r) into descending order
 // with a register bitonic network (45 stages; cross-lane stages use ds_bpermute shuffles).
+// v from lane (lane ^ M) for a compile-time M: DPP on the VALU for M < 16 (quad_perm for 1/2,
+// mirrors composed for 4/8), ds_swizzle for 16, ds_bpermute only for 32.
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+    if constexpr (M == 1) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // [1,0,3,2]
+    } else if constexpr (M == 2) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // [2,3,0,1]
+    } else if constexpr (M == 4) {                                                  // ^7 then ^3
+        const int h = __builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);     // row_half_mirror
+        return (uint32_t)__builtin_amdgcn_mov_dpp(h, 0x1B, 0xF, 0xF, false);         // [3,2,1,0]
+    } else if constexpr (M == 8) {                                                  // ^15 then ^7
+        const int m = __builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);     // row_mirror
+        return (uint32_t)__builtin_amdgcn_mov_dpp(m, 0x141, 0xF, 0xF, false);        // row_half_mirror
+    } else if constexpr (M == 16) {
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);               // xor_mask 16
+    } else {
+        return (uint32_t)__shfl_xor((int)v, M, 64);
+    }
+}
+
+template <int M>
+__device__ __forceinline__ void sort512_xstage(uint32_t (&k)[8], int lane, int stride, int size) {
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const int i = lane * 8 + r;
+        const uint32_t o = xor_lane<M>(k[r]);
+        const bool lower = (i & stride) == 0;
+        const bool desc = (i & size) == 0;
+        k[r] = (lower == desc) ? max(k[r], o) : min(k[r], o);
+    }
+}
+
 __device__ __forceinline__ void wave_sort512_desc(uint32_t (&k)[8]) {
     const int lane = lane_id();
 #pragma unroll
@@ -99,13 +132,13 @@ __device__ __forceinline__ void wave_sort512_desc(uint32_t (&k)[8]) {
 #pragma unroll
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
             if (stride >= 8) {
-#pragma unroll
-                for (int r = 0; r < 8; r++) {
-                    const int i = lane * 8 + r;
-                    const uint32_t o = __shfl_xor(k[r], stride >> 3, 64);
-                    const bool lower = (i & stride) == 0;
-                    const bool desc = (i & size) == 0;
-                    k[r] = (lower == desc) ? max(k[r], o) : min(k[r], o);
+                switch (stride >> 3) {
+                    case 1: sort512_xstage<1>(k, lane, stride, size); break;
+                    case 2: sort512_xstage<2>(k, lane, stride, size); break;
+                    case 4: sort512_xstage<4>(k, lane, stride, size); break;
+                    case 8: sort512_xstage<8>(k, lane, stride, size); break;
+                    case 16: sort512_xstage<16>(k, lane, stride, size); break;
+                    default: sort512_xstage<32>(k, lane, stride, size); break;
                 }
             } else {
 #pragma unroll
