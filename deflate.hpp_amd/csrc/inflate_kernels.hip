@@ -424,95 +424,130 @@ __device__ uint32_t fast_header(const Src& src, uint64_t* pos_io, uint64_t end_b
         const uint32_t ex = sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u;
         const uint32_t xv = (v >> len) & ((1u << ex) - 1u);
         const uint32_t rep_l = sym < 16 ? 1u : sym == 18 ? 11u + xv : 3u + xv;
-        const uint32_t pack = e ? (sym | (rep_l << 8) | ((len + ex) << 16)) : 0xFFFFFFFFu;
-        // serial part: the chain of true symbol starts, their first index and value;
-        // the code lengths themselves are written afterwards by the lanes in parallel
+        const uint32_t tl = e ? len + ex : 0u;  // symbol + repeat bits; 0 = no precode symbol
         const uint64_t end_rel64 = end_bits > w0 * 32 ? end_bits - w0 * 32 : 0;
         const uint32_t end_rel = end_rel64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)end_rel64;
-        uint32_t widx = 0xFFFFFFFFu, wval = 0;  // per lane: (seq << 16 | index), value
-        uint32_t p = 0, err = 0;
-        bool done = false;
+        // serial part: the chain of true symbol starts in this window (one readlane per symbol)
+        uint64_t M = 0;
+        uint32_t p = 0;
         while (p < 64) {
-            const uint32_t pk = __builtin_amdgcn_readlane(pack, p);
-            if (pk == 0xFFFFFFFFu) {
-                err = SEGF_ERR_DATA;
-                break;
+            M |= 1ull << p;
+            const uint32_t t = __builtin_amdgcn_readlane(tl, p);
+            if (!t) break;  // no precode symbol: reported below if it is reached
+            p += t;
+        }
+        // parallel part, in chain order: run index (prefix sum of repeats), sequence switch and
+        // end, the value a 16 repeats, errors, then the writes
+        const bool onp = (M >> lane) & 1ull;
+        const uint64_t below = (1ull << lane) - 1ull;
+        const uint32_t rep = onp && e ? rep_l : 0u;
+        const uint32_t incl = wave_incl_scan(rep);
+        const uint32_t excl = incl - rep;
+        const uint64_t sw = __ballot(onp && i + incl >= target);
+        int b1 = sw ? __builtin_ctzll(sw) : 64;  // first lane that completes the current sequence
+        int endl = 64;                           // last processed lane (64: the window continues)
+        int b2 = 64;
+        uint32_t incl_b1 = b1 < 64 ? __builtin_amdgcn_readlane(incl, b1) : 0u;
+        const bool switching = !rfc && seq == 0 && b1 < 64;
+        if (b1 < 64) {
+            if (!switching) {
+                endl = b1;
+            } else {  // reference mode: the distance lengths start after lane b1
+                const uint64_t sw2 = __ballot(onp && lane > b1 && incl - incl_b1 >= nd);
+                b2 = sw2 ? __builtin_ctzll(sw2) : 64;
+                if (b2 < 64) endl = b2;
             }
-            const uint32_t s = pk & 0xFF, rep = (pk >> 8) & 0xFF;
-            const uint32_t at = p;
-            p += pk >> 16;
-            if (s == 16 && rfc && i == 0) {
-                err = SEGF_ERR_DATA;
-                break;
-            }
-            const uint32_t val = s < 16 ? s : s == 16 ? last : 0u;
-            if (rfc || s < 16) last = val;
-            if (rp + p > end_rel) {
-                err = SEGF_OVERREAD;
-                break;
-            }
-            if (i + rep > cap && (rfc || val != 0)) {  // reference: value >= 300 is UB
-                err = SEGF_ERR_DATA;
-                break;
-            }
-            widx = lane == (int)at ? (i | (seq << 16)) : widx;
-            wval = lane == (int)at ? val : wval;
-            i += rep;
-            if (i >= target) {
-                if (rfc) {
-                    done = true;
-                    break;
-                }
-                if (seq == 0) {  // reference mode: the distance lengths are a second sequence
-                    nl = min(i, 300u);
-                    seq = 1;
-                    target = nd;
-                    i = 0;
-                    last = 0;
-                } else {
-                    ndd = min(i, 300u);
-                    done = true;
-                    break;
+        }
+        const bool proc = onp && lane <= endl;
+        const bool in2 = switching && lane > b1;          // lane belongs to the distance sequence
+        const uint32_t idx = in2 ? excl - incl_b1 : i + excl;
+        const uint32_t sq = in2 ? 1u : seq;
+        // value a 16 repeats: the nearest earlier lane of the same sequence that sets "last"
+        // (reference: literal lengths only; RFC: any non-16 symbol), else the carried value
+        const uint32_t symv = sym < 16 ? sym : 0u;
+        const uint64_t qual = __ballot(onp && (rfc ? sym != 16 : sym < 16));
+        const uint64_t seq2m = switching ? ~((2ull << b1) - 1ull) : ~0ull;  // distance-sequence lanes
+        const uint64_t qb = (in2 ? qual & seq2m : qual) & below;
+        const uint32_t src = qb ? 63u - (uint32_t)__builtin_clzll(qb) : 0u;
+        const uint32_t qv = (uint32_t)__shfl((int)symv, (int)src, 64);
+        const uint32_t lastv = qb ? qv : (in2 ? 0u : last);
+        const uint32_t val = sym < 16 ? sym : sym == 16 ? lastv : 0u;
+        // errors, in the reference's order per symbol (inflate.hpp:166-206)
+        uint32_t lerr = 0;
+        if (proc) {
+            if (!e) lerr = SEGF_ERR_DATA;
+            else if (sym == 16 && rfc && idx == 0) lerr = SEGF_ERR_DATA;
+            else if (rp + (uint32_t)lane + tl > end_rel) lerr = SEGF_OVERREAD;
+            else if (idx + rep_l > cap && (rfc || val != 0)) lerr = SEGF_ERR_DATA;
+        }
+        const uint64_t em = __ballot(lerr != 0);
+        const uint32_t err = em ? __builtin_amdgcn_readlane(lerr, __builtin_ctzll(em)) : 0u;
+        // writes: entries idx < cap keep the value (reference: overshoot entries keep their index
+        // as the symbol value); long runs are written by the whole wave
+        const bool mine = proc && e;
+        const bool longr = mine && rep_l > 8;
+        if (mine && !longr) {
+            for (uint32_t jj = 0; jj < rep_l; jj++) {
+                const uint32_t k = idx + jj;
+                if (k < cap) {
+                    if (!rfc) (sq ? T.dlen : T.llen)[k] = (uint8_t)val;
+                    else if (k < na) T.llen[k] = (uint8_t)val;
+                    else T.dlen[k - na] = (uint8_t)val;
                 }
             }
         }
-        // parallel writes: entries idx < cap keep the value (reference: overshoot entries
-        // keep their index as the symbol value); long runs are written by the whole wave
-        {
-            const bool mine = widx != 0xFFFFFFFFu;
-            const uint32_t i0 = widx & 0xFFFF, sq = widx >> 16;
-            const bool longr = mine && rep_l > 8;
-            if (mine && !longr) {
-                for (uint32_t jj = 0; jj < rep_l; jj++) {
-                    const uint32_t idx = i0 + jj;
-                    if (idx < cap) {
-                        if (!rfc) (sq ? T.dlen : T.llen)[idx] = (uint8_t)wval;
-                        else if (idx < na) T.llen[idx] = (uint8_t)wval;
-                        else T.dlen[idx - na] = (uint8_t)wval;
-                    }
+        uint64_t lm = __ballot(longr);
+        while (lm) {
+            const int l = __builtin_ctzll(lm);
+            lm &= lm - 1;
+            const uint32_t il = __builtin_amdgcn_readlane(idx, l);
+            const uint32_t vl = __builtin_amdgcn_readlane(val, l);
+            const uint32_t rl = __builtin_amdgcn_readlane(rep_l, l);
+            const uint32_t ql = __builtin_amdgcn_readlane(sq, l);
+            for (uint32_t jj = lane; jj < rl; jj += 64) {
+                const uint32_t k = il + jj;
+                if (k < cap) {
+                    if (!rfc) (ql ? T.dlen : T.llen)[k] = (uint8_t)vl;
+                    else if (k < na) T.llen[k] = (uint8_t)vl;
+                    else T.dlen[k - na] = (uint8_t)vl;
                 }
             }
-            uint64_t lm = __ballot(longr);
-            while (lm) {
-                const int l = __builtin_ctzll(lm);
-                lm &= lm - 1;
-                const uint32_t wl = __builtin_amdgcn_readlane(widx, l);
-                const uint32_t vl = __builtin_amdgcn_readlane(wval, l);
-                const uint32_t rl = __builtin_amdgcn_readlane(rep_l, l);
-                const uint32_t b0 = wl & 0xFFFF;
-                for (uint32_t jj = lane; jj < rl; jj += 64) {
-                    const uint32_t idx = b0 + jj;
-                    if (idx < cap) {
-                        if (!rfc) ((wl >> 16) ? T.dlen : T.llen)[idx] = (uint8_t)vl;
-                        else if (idx < na) T.llen[idx] = (uint8_t)vl;
-                        else T.dlen[idx - na] = (uint8_t)vl;
-                    }
-                }
+        }
+        if (err) return err;
+        // carry to the next window
+        const uint64_t procm = __ballot(proc);
+        const int lastl = 63 - __builtin_clzll(procm);  // last processed lane (lane 0 always is)
+        const uint32_t inc_last = __builtin_amdgcn_readlane(incl, lastl);
+        const uint64_t qp = qual & procm & seq2m;  // setters in the sequence that continues
+        if (rfc) {
+            last = __builtin_amdgcn_readlane(val, lastl);
+        } else if (qp) {
+            last = __builtin_amdgcn_readlane(symv, 63 - __builtin_clzll(qp));
+        } else if (switching) {
+            last = 0;
+        }
+        if (endl < 64) {  // the header ends inside this window
+            if (rfc) {
+                nl = na;
+                ndd = nd;
+            } else if (switching) {
+                nl = min(i + incl_b1, 300u);
+                ndd = min(inc_last - incl_b1, 300u);
+            } else {
+                ndd = min(i + inc_last, 300u);
             }
+            rp += (uint32_t)endl + __builtin_amdgcn_readlane(tl, endl);
+            break;
+        }
+        if (switching) {
+            nl = min(i + incl_b1, 300u);
+            seq = 1;
+            target = nd;
+            i = inc_last - incl_b1;
+        } else {
+            i += inc_last;
         }
         rp += p;
-        if (err) return err;
-        if (done) break;
     }
     if (rfc) {
         nl = na;
