@@ -1058,8 +1058,8 @@ struct PjSmem {
     static constexpr int IN_WORDS = (SEG + 2048) / 4 + 8;
     uint16_t P[SEG];
     uint32_t in[IN_WORDS];  // the candidate's compressed words, in[0] = stream word ws
-    uint16_t llut[1 << PJ_LL];
-    uint16_t dlut[1 << PJ_LD];
+    uint32_t llut[1 << PJ_LL];  // 32-bit entries (lit_entry / dist_entry)
+    uint32_t dlut[1 << PJ_LD];
     Tables T;
     uint32_t endp[NT];      // where range r's current path crossed into range r+1; later the
                             // exclusive output offset of range r
@@ -1087,9 +1087,9 @@ __device__ __forceinline__ uint32_t lds_peek32(const uint32_t* w, uint32_t p) {
     return __builtin_amdgcn_alignbit(w[i + 1], w[i], p & 31);
 }
 
-// primary lookup table over PB bits filled by the whole workgroup (same entries as fill_lut)
-template <int PB>
-__device__ void fill_lut_wg(uint16_t* lut, const TreeMeta& m, const uint16_t* sorted, int tid, int nthr) {
+// primary lookup table over PB bits with 32-bit entries, filled by the whole workgroup
+template <int PB, bool DIST>
+__device__ void fill_lut32_wg(uint32_t* lut, const TreeMeta& m, const uint16_t* sorted, int tid, int nthr) {
     uint32_t lo[16], hi[16], cn[16], of[16];
 #pragma unroll
     for (int k = 1; k < 16; k++) {
@@ -1112,7 +1112,7 @@ __device__ void fill_lut_wg(uint16_t* lut, const TreeMeta& m, const uint16_t* so
                 }
             }
         }
-        lut[wv] = len ? (uint16_t)(sorted[idx] | (len << 9)) : (uint16_t)0;
+        lut[wv] = len ? (DIST ? dist_entry(sorted[idx], len) : lit_entry(sorted[idx], len)) : 0u;
     }
 }
 
@@ -1120,51 +1120,41 @@ enum : uint32_t { TK_LIT = 0, TK_MATCH = 1, TK_EOB = 2, TK_BAD = 3 };
 
 // one token of decompressHuffmanBlock (inflate.hpp:226-275) at bit *p of the staged words:
 // a literal (*a = byte), a match (*a = length, *d = distance; 0 for symbols 286+ / 30+), the
-// end of block, or no code.  A literal reads one 32-bit window, a match two.
-__device__ __forceinline__ uint32_t pj_token(const uint32_t* w, uint32_t* p, const uint16_t* llut,
-                                             const uint16_t* dlut, const Tables& T, uint32_t* a,
+// end of block, or no code.  A literal reads one 32-bit window, a match two; the 32-bit table
+// entries carry class, code length, base and extra-bit count.
+__device__ __forceinline__ uint32_t pj_token(const uint32_t* w, uint32_t* p, const uint32_t* llut,
+                                             const uint32_t* dlut, const Tables& T, uint32_t* a,
                                              uint32_t* d) {
     uint32_t v = lds_peek32(w, *p);
     uint32_t e = llut[v & ((1u << PJ_LL) - 1)];
-    uint32_t sym, len;
-    if (e) {
-        sym = e & 511;
-        len = e >> 9;
-    } else if (!slow_decode(T.lm, T.lsorted, v & 0x7FFF, PJ_LL + 1, &sym, &len)) {
-        return TK_BAD;
+    if (!e) {
+        uint32_t sym, len;
+        if (!slow_decode(T.lm, T.lsorted, v & 0x7FFF, PJ_LL + 1, &sym, &len)) return TK_BAD;
+        e = lit_entry(sym, len);
     }
-    if (sym < 256) {
-        *p += len;
-        *a = sym;
+    const uint32_t cl = e & 15, ty = (e >> 4) & 3;
+    if (ty == 0) {
+        *p += cl;
+        *a = e >> 16;
         return TK_LIT;
     }
-    if (sym == 256) {
-        *p += len;
+    if (ty == 1) {
+        *p += cl;
         return TK_EOB;
     }
-    uint32_t L = 0, ex = 0;
-    if (sym <= 285) {
-        ex = len_extra(sym);
-        L = len_base(sym) + ((v >> len) & ((1u << ex) - 1u));
-    }
-    *p += len + ex;
+    const uint32_t ex = (e >> 6) & 15;
+    *a = (e >> 16) + ((v >> cl) & ((1u << ex) - 1u));
+    *p += cl + ex;
     v = lds_peek32(w, *p);
-    e = dlut[v & ((1u << PJ_LD) - 1)];
-    uint32_t ds, dl;
-    if (e) {
-        ds = e & 511;
-        dl = e >> 9;
-    } else if (!slow_decode(T.dm, T.dsorted, v & 0x7FFF, PJ_LD + 1, &ds, &dl)) {
-        return TK_BAD;
+    uint32_t de = dlut[v & ((1u << PJ_LD) - 1)];
+    if (!de) {
+        uint32_t ds, dl;
+        if (!slow_decode(T.dm, T.dsorted, v & 0x7FFF, PJ_LD + 1, &ds, &dl)) return TK_BAD;
+        de = dist_entry(ds, dl);
     }
-    uint32_t dist = 0, dx = 0;
-    if (ds < 30) {
-        dx = dist_extra(ds);
-        dist = dist_base(ds) + ((v >> dl) & ((1u << dx) - 1u));
-    }
+    const uint32_t dl = de & 15, dx = (de >> 6) & 15;
+    *d = (de >> 16) + ((v >> dl) & ((1u << dx) - 1u));
     *p += dl + dx;
-    *a = L;
-    *d = dist;
     return TK_MATCH;
 }
 
@@ -1303,8 +1293,8 @@ __global__ __launch_bounds__(NT) void k_inflate_pj(InflateArgs A) {
         __syncthreads();
         DMX_PHASE(A.dbg, j, 1);
         if (!S.err) {
-            fill_lut_wg<PJ_LL>(S.llut, S.T.lm, S.T.lsorted, t, NT);
-            fill_lut_wg<PJ_LD>(S.dlut, S.T.dm, S.T.dsorted, t, NT);
+            fill_lut32_wg<PJ_LL, false>(S.llut, S.T.lm, S.T.lsorted, t, NT);
+            fill_lut32_wg<PJ_LD, true>(S.dlut, S.T.dm, S.T.dsorted, t, NT);
         }
         __syncthreads();
     }
