@@ -1046,7 +1046,6 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
 // above the staging buffer, a split that does not settle -- is flagged SEGF_EXOTIC and the
 // stream is redone by k_inflate_segments, so results never depend on this path's coverage.
 // ---------------------------------------------------------------------------------------
-constexpr int PJ_K = 8;
 constexpr uint32_t PJ_LIT = 0x8000u;
 constexpr int PJ_ROUNDS = 64;
 constexpr uint32_t PJ_MINBITS = 256;
@@ -1309,15 +1308,18 @@ __global__ __launch_bounds__(NT) void k_inflate_pj(InflateArgs A) {
         const uint32_t r = (uint32_t)((t & 63) * NW + wave);
         const uint32_t sp = r < nl ? (uint32_t)(((uint64_t)hlen * r) / nl) : hlen;
         const uint32_t sp1 = r + 1 < nl ? (uint32_t)(((uint64_t)hlen * (r + 1)) / nl) : hlen;
-        // P is free until the emit pass: it holds the first pass's token-start bitmap
+        // P is free until the emit pass: it holds the first pass's token-start bitmap, then
+        // (from word cw0) the running output count after each of a range's first ccap tokens,
+        // entry k of range r at cw0 * 2 + k * NT + r (u16)
         uint32_t* bmap = reinterpret_cast<uint32_t*>(S.P);
-        for (uint32_t i = t; i < hlen / 32 + 2; i += NT) bmap[i] = 0;
+        const uint32_t cw0 = hlen / 32 + 2;
+        const uint32_t ccap = min(64u, (uint32_t)(SEG / 2 - cw0) * 2 / NT);
+        uint16_t* cbuf = S.P + cw0 * 2;
+        for (uint32_t i = t; i < cw0; i += NT) bmap[i] = 0;
         if (t < 2) S.te2[t] = NT;
         __syncthreads();
         // ---- 2. first pass over the ranges (positions relative to hs) ----
-        uint32_t q[PJ_K], c[PJ_K];
-#pragma unroll
-        for (int k = 0; k < PJ_K; k++) q[k] = c[k] = 0xFFFFFFFFu;
+        uint32_t qc = sp, cc = 0;  // token boundary ccap of the first pass, its count
         uint32_t e1, cnt1 = 0, st1 = 0, nb = 0;
         {
             uint32_t p = sp, pa = hs + sp;
@@ -1329,12 +1331,8 @@ __global__ __launch_bounds__(NT) void k_inflate_pj(InflateArgs A) {
                 p = pa - hs;
                 if (k == TK_EOB) { st1 = 1; break; }
                 cnt1 += tok_bytes(k, a, d);
-                if (nb < PJ_K) {
-#pragma unroll
-                    for (int m = 0; m < PJ_K; m++)
-                        if (m == (int)nb) { q[m] = p; c[m] = cnt1; }
-                    nb++;
-                }
+                if (nb < ccap) cbuf[nb * NT + r] = (uint16_t)cnt1;
+                if (++nb == ccap) { qc = p; cc = cnt1; }
             }
             e1 = p;
         }
@@ -1365,7 +1363,7 @@ __global__ __launch_bounds__(NT) void k_inflate_pj(InflateArgs A) {
                 // decode from the true start until the path meets a token start of this
                 // range's first pass (from there on both paths are the same)
                 s = want;
-                uint32_t p = want, pa = hs + want, acc = 0, stn = 0, dbg_tok = 0;
+                uint32_t p = want, pa = hs + want, acc = 0, stn = 0, dbg_tok = 0, dbg_walk = 0;
                 bool merged = false;
                 for (;;) {
                     if (p >= sp1) break;
@@ -1382,25 +1380,26 @@ __global__ __launch_bounds__(NT) void k_inflate_pj(InflateArgs A) {
                     acc += tok_bytes(k, a, d);
                 }
                 if (merged) {
-                    // first-pass bytes of the tokens before p: kept boundaries, else re-walk
-                    uint32_t before = 0, from = sp, cum = 0;
-                    bool found = p == sp;
-#pragma unroll
-                    for (int m = 0; m < PJ_K; m++) {
-                        if (!found && q[m] == p) {
-                            before = c[m];
-                            found = true;
-                        }
-                        if (!found && q[m] < p) {
-                            from = q[m];
-                            cum = c[m];
-                        }
+                    // first-pass bytes of the tokens before p: p is token boundary kb of the
+                    // first pass (kb = its marks in [sp, p)); counts of boundaries past ccap
+                    // are re-walked from boundary ccap
+                    uint32_t kb = 0;
+                    for (uint32_t wi = sp >> 5; wi <= (p >> 5); wi++) {
+                        uint32_t m = bmap[wi];
+                        if (wi == (sp >> 5)) m &= ~0u << (sp & 31);
+                        if (wi == (p >> 5)) m &= (1u << (p & 31)) - 1u;
+                        kb += __builtin_popcount(m);
                     }
-                    if (!found) {
-                        uint32_t pw = from, pwa = hs + from;
+                    uint32_t before = 0;
+                    if (kb == 0) {
+                        before = 0;
+                    } else if (kb <= ccap) {
+                        before = cbuf[(kb - 1) * NT + r];
+                    } else {
+                        uint32_t pw = qc, pwa = hs + qc, cum = cc;
                         while (pw < p) {
                             uint32_t a, d;
-                            dbg_tok++;
+                            dbg_walk++;
                             const uint32_t k = pj_token(win, &pwa, S.llut, S.dlut, S.T, &a, &d);
                             pw = pwa - hs;
                             cum += tok_bytes(k, a, d);
@@ -1419,6 +1418,7 @@ __global__ __launch_bounds__(NT) void k_inflate_pj(InflateArgs A) {
                 }
                 if (A.dbg) {
                     atomicAdd(&S.dcount[0], dbg_tok);
+                    atomicAdd(&S.dcount[3], dbg_walk);
                     atomicAdd(&S.dcount[merged ? 1 : 2], 1u);
                 }
             }
@@ -1432,6 +1432,7 @@ __global__ __launch_bounds__(NT) void k_inflate_pj(InflateArgs A) {
             A.dbg[j * kPhaseSlots + 12] = S.dcount[1];
             A.dbg[j * kPhaseSlots + 13] = S.dcount[2];
             A.dbg[j * kPhaseSlots + 14] = nl;
+            A.dbg[j * kPhaseSlots + 15] = S.dcount[3];
         }
         if (r == te) {
             if (st == 2) {
