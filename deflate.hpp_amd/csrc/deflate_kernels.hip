@@ -36,6 +36,11 @@ namespace dmx {
 constexpr int DF_NT = 1024;    // threads per workgroup (16 waves)
 constexpr int DF_CHUNK = 256;  // bytes per parse lane
 constexpr int DF_HB = 12;      // hash bits of each of the two match tables
+// Code-length limits of the emitted lit/len and distance codes.  RFC 1951 allows 15; 9 and 6
+// keep every code inside the one-level lookup tables of the lane decoder
+// (inflate_lanes.hip: 512 + 64 entries per segment in LDS) at < 1% ratio cost.
+constexpr int DF_LIT_MAXBITS = 9;
+constexpr int DF_DIST_MAXBITS = 6;
 constexpr int DF_PPT = 2;      // positions per thread in one match round (4 halves the rounds
                                // but loses recent candidates: -4% ratio on repeat, -1% on text)
 
@@ -478,14 +483,14 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t
     // ---- code lengths + canonical codes (wave 0: lit/len, wave 1: distance) -------------
     if (t < 64) {
         uint64_t wst[6] = {0, 0, 0, 0, 0, 0};
-        wave_build_lengths(S.litfreq, 286, 15, S.litlen, dbg ? wst : nullptr);
+        wave_build_lengths(S.litfreq, 286, DF_LIT_MAXBITS, S.litlen, dbg ? wst : nullptr);
         if (dbg && t == 0) dbg[seg * kPhaseSlots + 11] = (wst[0] & 0xFFFF) | ((wst[1] & 0xFFFF) << 16) | ((wst[3] & 0xFFFF) << 32) | ((wst[4] & 0xFFFF) << 48);
         if (dbg && t == 0) dbg[seg * kPhaseSlots + 15] = (wst[2] & 0xFFFF) | ((wst[5] & 0xFFFF) << 16);
         DMX_PHASE(dbg, seg, 12);
         wave_assign_codes(S.litlen, 286, S.litcode);
         DMX_PHASE(dbg, seg, 13);
     } else if (t < 128) {
-        wave_build_lengths64(S.distfreq, 30, 15, S.distlen);
+        wave_build_lengths64(S.distfreq, 30, DF_DIST_MAXBITS, S.distlen);
         wave_assign_codes(S.distlen, 30, S.distcode);
     }
     if (t < 8) S.sh[32 + t] = 0;

@@ -6,6 +6,7 @@
 // created once per process (std::call_once) on the caller's current device.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -58,6 +59,7 @@ struct dmx_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     DevBuf in, out, slots, sizes, offs, scal, cands, tiles, tileoffs, recs, status, dbg;
+    DevBuf ltok, ltokoff, lntok, lcaps;  // lane decoder token lists (mode 4)
     bool timing = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     dmx_stats stats{};
@@ -243,37 +245,52 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     A.flags = c->flags;
     A.dbg = phase_buf(c, ncand);
     InflateResult r{};
-    // Plan: the workgroup-per-segment decoder with the context's segment size (segment j
-    // lands at j * seg), then with the other size, then the wave-per-segment decoder, which
-    // places segments of any size <= 32 KiB by look-back; each pass runs only if the previous
-    // one reported status 1 (a segment outside its layout or sizes not uniform).
+    // Plan: the lane decoder (one lane per segment decodes tokens, one wave per segment
+    // resolves them; segment j lands at j * seg) with a patch pass of the exact wave decoder
+    // for the candidates it declines; then the older workgroup-per-segment decoder with both
+    // segment sizes; then the wave-per-segment decoder, which places segments of any size
+    // <= 32 KiB by look-back.  Each pass runs only if the previous one reported status 1 (a
+    // segment outside its layout or sizes not uniform); status 2 goes to the serial decoder.
     static const int path_env = [] {
         const char* e = std::getenv("DMX_INFLATE_PATH");
         return e ? std::atoi(e) : -1;
     }();
-    // High-ratio streams (few compressed bytes per candidate: long matches, few tokens) go to
-    // the wave decoder first; the others to the workgroup decoder.
     const bool few_bits = n / ncand < 4096;
-    uint32_t plan[6][2];
+    uint32_t plan[8][2];
     int np = 0;
+    if (path_env == -1 || path_env == 4) {
+        const uint64_t words = std::min<uint64_t>(ncand * 32788ull, 8ull * n + 20ull * ncand);
+        if (c->ltok.ensure(words * 4) && c->ltokoff.ensure((ncand + 1) * 8) &&
+            c->lntok.ensure(ncand * 4) && c->lcaps.ensure(ncand * 4)) {
+            plan[np][0] = 4, plan[np][1] = c->seg, np++;
+            plan[np][0] = 3, plan[np][1] = c->seg, np++;  // patch the declined candidates
+        }
+    }
     if (path_env == 0 || path_env == 1) {
         plan[np][0] = (uint32_t)path_env, plan[np][1] = 0, np++;
+    } else if (path_env == 4) {
     } else if (few_bits && path_env != 2) {
         plan[np][0] = 0, plan[np][1] = 0, np++;
     } else {
         plan[np][0] = 2, plan[np][1] = c->seg, np++;
-        plan[np][0] = 3, plan[np][1] = c->seg, np++;  // patch the declined candidates
+        plan[np][0] = 3, plan[np][1] = c->seg, np++;
         plan[np][0] = 2, plan[np][1] = c->seg == 32768 ? 16384u : 32768u, np++;
         plan[np][0] = 3, plan[np][1] = c->seg == 32768 ? 16384u : 32768u, np++;
     }
-    if (path_env != 1) plan[np][0] = 1, plan[np][1] = 0, np++;
+    if (path_env != 1 && path_env != 4) plan[np][0] = 1, plan[np][1] = 0, np++;
+    uint32_t lead_mode = 0;
     for (int pi = 0; pi < np; pi++) {
         const uint32_t mode = plan[pi][0];
         if (mode == 3 && (r.exotic == 0 || r.exotic > ncand / 8)) continue;  // nothing / too many
         A.mode = mode;
         A.slot = plan[pi][1];
-        hipEvent_t e0 = c->timing ? c->ev[1] : nullptr, e1 = c->timing ? c->ev[2] : nullptr;
-        if (mode == 2) {
+        // main-kernel window: from the first pass's launch to the end of the last pass run
+        hipEvent_t e0 = (c->timing && pi == 0) ? c->ev[1] : nullptr, e1 = c->timing ? c->ev[2] : nullptr;
+        if (mode != 3) lead_mode = mode;
+        if (mode == 4) {
+            HIPCHK(launch_inflate_lanes(A, c->ltok.as<uint32_t>(), c->ltokoff.as<uint64_t>(),
+                                        c->lntok.as<uint32_t>(), c->lcaps.as<uint32_t>(), st, e0, e1));
+        } else if (mode == 2) {
             HIPCHK(launch_inflate_pj(A, A.slot, st, e0, e1));
         } else {
             HIPCHK(hipMemsetAsync(A.status, 0, ncand * 8, st));
@@ -306,7 +323,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     c->stats.in_bytes = n;
     if (r.status == 0) {
         end_timing(c, st);
-        c->stats.path = A.mode >= 2 ? 3 : A.mode;
+        c->stats.path = lead_mode == 4 ? 4 : lead_mode >= 2 ? 3 : lead_mode;
         c->stats.out_bytes = r.total;
         *total_out = r.total;
         if (dev_out) *dev_out = out;

@@ -57,7 +57,8 @@ struct InflateArgs {
     uint32_t mode;               // 0 = speculative uniform segment sizes, 1 = decoupled look-back,
                                  // 2 = k_inflate_pj (segment j at j * slot),
                                  // 3 = k_inflate_segments redoing only SEGF_EXOTIC candidates
-                                 //     of a mode-2 pass, at the same slots
+                                 //     of a mode-2 / mode-4 pass, at the same slots,
+                                 // 4 = k_inflate_lanes + k_inflate_resolve (segment j at j * slot)
     uint32_t slot;               // mode 2: segment bytes (16384 or 32768)
     uint64_t* dbg;               // optional per-segment phase timestamps (DMX_PHASES)
 };
@@ -90,6 +91,12 @@ hipError_t launch_inflate_segments(const InflateArgs& A, hipStream_t st, hipEven
 // segment j lands at j * 32768 (mode 2)
 hipError_t launch_inflate_pj(const InflateArgs& A, uint32_t seg, hipStream_t st, hipEvent_t ev0,
                              hipEvent_t ev1);
+// lane-per-segment Huffman decode (k_inflate_lanes) + wave-per-segment LZ77 resolve
+// (k_inflate_resolve); segment j lands at j * A.slot (mode 4).  tok holds
+// min(ncand * 32788, 8 * n + 20 * ncand) words; tokoff ncand + 1, ntok / caps ncand entries.
+hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* tokoff,
+                                uint32_t* ntok, uint32_t* caps, hipStream_t st, hipEvent_t ev0,
+                                hipEvent_t ev1);
 hipError_t launch_inflate_validate(const InflateArgs& A, InflateResult* res, hipStream_t st);
 hipError_t launch_inflate_serial(const InflateArgs& A, int count_only, InflateResult* res,
                                  hipStream_t st);

@@ -1,0 +1,636 @@
+// inflate_lanes.hip -- two-phase inflate of segment-structured streams (gfx950).
+//
+// Phase A, k_inflate_lanes: ONE LANE PER CANDIDATE SEGMENT.  Huffman decoding is serial within
+// a segment, but a 1 GiB stream holds ~32K independent segments (libdmx's deflate, or any
+// encoder's full-flush points), so 64 segments decode side by side in one wavefront and the
+// whole stream is in flight at once.  Each lane owns a 1280-byte LDS region:
+//     [   0, 1024)  lit/len lookup table, 512 x u16, indexed by the next <= 9 stream bits
+//     [1024, 1152)  distance lookup table, 64 x u16 (<= 6-bit codes)
+//     [1152, 1280)  code-length (precode) lookup table, 128 x u8 (<= 7-bit codes, RFC 1951)
+// 64 lanes x 1280 B = 80 KiB per workgroup, two workgroups per CU: 32768 lanes on 256 CUs.
+// The block header is read twice (pass 1 counts the code lengths, pass 2 re-decodes them and
+// fills the tables), so no per-symbol code-length array is stored; per-length counters and
+// next-code values live in packed registers (dynamic "indexing" by shifts).  The decoded
+// tokens go to HBM as 32-bit words:
+//     match        1 | L(16) | d-1(15)          consecutive matches with the same distance are
+//                                               merged: one periodic copy of their summed length
+//     literal run  0 | count(7) = 1..3 | bytes(24)
+//     stored       0 | 0 | len(24), then the data's byte offset from the candidate start
+// Lanes accept exactly the layout libdmx's deflate emits: one stored / fixed / dynamic block
+// (lit/len codes <= 9 bits, distance codes <= 6 bits, complete codes, no A-11/A-12 header
+// quirks, output <= 32 KiB, no reference before the segment start) ended by the empty stored
+// block "00 00 FF FF" or by BFINAL.  Anything else is flagged SEGF_EXOTIC and redone by the
+// exact wave decoder (k_inflate_segments mode 3), so results never depend on this path's
+// coverage.  Decode semantics on the accepted layout are the reference's
+// (decompressHuffmanBlock inflate.hpp:226-275, readDynamicTreeCodes :166-206, realDecompress
+// :277-322), including "distance beyond the output so far copies nothing" at the stream start.
+//
+// Phase B, k_inflate_resolve: one wavefront per segment rebuilds the output in a 32 KiB LDS
+// window from the token list, 64 tokens per step (wave prefix sum of token lengths):
+// literal runs and short matches whose source lies before the step go in parallel (4 bytes
+// per iteration when d >= 4), long or self-dependent matches are copied by the whole wave in
+// token order (periodic copy out[o + i] = out[o - d + (i mod d)], as the reference's
+// byte-serial copy inflate.hpp:268-270), then 16-byte stores put the window at j * slot.
+#include "../../include/dmx.h"
+#include "dmx_device.h"
+#include "dmx_internal.h"
+
+namespace dmx {
+
+constexpr uint32_t LN_REGION = 1280;
+constexpr uint32_t LN_DIST = 1024;
+constexpr uint32_t LN_PRE = 1152;
+constexpr uint32_t LN_OUT_CAP = 32768;
+
+__constant__ const uint8_t kLnPerm[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5,
+                                          11, 4,  12, 3, 13, 2, 14, 1, 15};
+
+// per-lane LSB-first bit reader over the stream in HBM: 64-bit bit buffer, the current 16-byte
+// block and one prefetched block (its load is in flight while the current one is consumed).
+// Positions are bytes from blk (the 16-byte aligned base); bytes at or past E read as zero.
+struct LaneIn {
+    const uint4* blk;
+    uint64_t nblk, E;
+    uint4 cur, nxt;
+    uint64_t pb, wi;  // next block to fetch; absolute index of the next word to shift in
+    uint32_t ci, nb;  // word index in cur; valid bits in bb
+    uint64_t bb;
+    __device__ __forceinline__ uint4 fetch(uint64_t b) const {
+        return b < nblk ? blk[b] : make_uint4(0, 0, 0, 0);
+    }
+    __device__ __forceinline__ void refill() {  // requires nb <= 32
+        uint32_t w = cur.x;  // cur is a queue: shift instead of indexing (keeps it in VGPRs)
+        cur.x = cur.y;
+        cur.y = cur.z;
+        cur.z = cur.w;
+        const uint64_t wb = wi * 4;
+        if (wb + 4 > E) w = wb >= E ? 0u : (w & ((1u << (8 * (uint32_t)(E - wb))) - 1u));
+        bb |= (uint64_t)w << nb;
+        nb += 32;
+        wi++;
+        if (++ci == 4) {
+            ci = 0;
+            cur = nxt;
+            nxt = fetch(pb);
+            pb++;
+        }
+    }
+    __device__ void seek(uint64_t abyte) {
+        const uint64_t b = abyte >> 4;
+        cur = fetch(b);
+        nxt = fetch(b + 1);
+        pb = b + 2;
+        ci = (uint32_t)(abyte >> 2) & 3;
+        wi = abyte >> 2;
+        for (uint32_t k = 0; k < ci; k++) {  // drop the words before the start
+            cur.x = cur.y;
+            cur.y = cur.z;
+            cur.z = cur.w;
+        }
+        bb = 0;
+        nb = 0;
+        refill();
+        refill();
+        const uint32_t sk = (uint32_t)(abyte & 3) * 8;
+        bb >>= sk;
+        nb -= sk;
+    }
+    __device__ __forceinline__ void ensure(uint32_t k) {  // k <= 32
+        if (nb < k) refill();
+    }
+    __device__ __forceinline__ uint32_t bits(uint32_t n) {  // n <= 32, after ensure(n)
+        const uint32_t v = n ? (uint32_t)(bb & ((1ull << n) - 1ull)) : 0u;
+        bb >>= n;
+        nb -= n;
+        return v;
+    }
+    __device__ __forceinline__ void consume(uint32_t n) {
+        bb >>= n;
+        nb -= n;
+    }
+    __device__ __forceinline__ uint64_t bitpos() const { return wi * 32 - nb; }
+    __device__ __forceinline__ void align() { consume((uint32_t)(-bitpos()) & 7u); }  // next byte
+};
+
+struct LaneArgs {
+    uint32_t* tok;          // token words
+    const uint64_t* tokoff; // ncand + 1 word offsets (exclusive scan of the capacities)
+    uint32_t* ntok;         // ncand token counts
+    uint32_t* caps;         // ncand capacities (words)
+};
+
+// lit/len table entry: literal / end-of-block  0 | cl(4) << 11 | sym(9)
+//                      length               1 | cl(4) << 11 | extra(3) << 8 | base - 3 (8)
+// symbols 286/287 (fixed code only) are entered as literals >= 257 -> flagged on use.
+__device__ __forceinline__ uint32_t ln_lit_entry(uint32_t s, uint32_t l) {
+    if (s >= 257 && s <= 285) return 0x8000u | (l << 11) | (len_extra(s) << 8) | (len_base(s) - 3);
+    return (l << 11) | s;
+}
+
+__global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[64 * LN_REGION];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t j = (uint64_t)blockIdx.x * 64 + lane;
+    if (j >= A.ncand) return;  // lanes are independent: no barrier anywhere in this kernel
+    uint8_t* const R = lds + lane * LN_REGION;
+    const uint32_t rot = 4 * lane;  // rotate each lane's region by one bank per lane
+    auto at = [&](uint32_t b) -> uint32_t {
+        const uint32_t x = b + rot;
+        return x >= LN_REGION ? x - LN_REGION : x;
+    };
+    auto lut16 = [&](uint32_t b) -> uint32_t { return *reinterpret_cast<const uint16_t*>(R + at(b)); };
+
+    const uintptr_t base4 = reinterpret_cast<uintptr_t>(A.in_words);
+    const uintptr_t base16 = base4 & ~(uintptr_t)15;
+    const uint64_t off0 = (uint64_t)(base4 - base16) + A.misalign;  // stream byte 0
+    LaneIn br;
+    br.blk = reinterpret_cast<const uint4*>(base16);
+    br.E = off0 + A.n;
+    br.nblk = (br.E + 15) / 16;
+    const uint64_t start = A.cands[j];
+    br.seek(off0 + start);
+
+    uint32_t flags = 0, outpos = 0;
+    bool fin = false;
+    uint64_t end_byte = 0;
+
+    // token output: pending token (merges), 4-word queue, 16-byte stores
+    uint32_t* const tk = B.tok + B.tokoff[j];
+    const uint32_t tcap = B.caps[j];
+    uint32_t ntok = 0, qn = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+    uint32_t pk = 0, pa = 0, pd = 0;  // pending: kind (1 literal run, 2 match), bytes / L, count / d
+    auto push = [&](uint32_t w) {
+        q0 = q1;  // shift register (no indexed writes: stays in VGPRs)
+        q1 = q2;
+        q2 = q3;
+        q3 = w;
+        if (++qn == 4) {
+            if (ntok + 4 <= tcap) *reinterpret_cast<uint4*>(tk + ntok) = make_uint4(q0, q1, q2, q3);
+            ntok += 4;
+            qn = 0;
+        }
+    };
+    auto flushp = [&]() {
+        if (pk == 1) push((pd << 24) | pa);
+        else if (pk == 2) push(0x80000000u | (pa << 15) | (pd - 1));
+        pk = 0;
+    };
+
+    br.ensure(3);
+    const uint32_t bfinal = br.bits(1);
+    const uint32_t btype = br.bits(2);
+    if (btype == 0) {
+        // stored block (libdmx emits these for incompressible segments) or an empty segment
+        br.align();
+        br.ensure(32);
+        const uint32_t len = br.bits(16), nlen = br.bits(16);
+        const uint64_t b0 = br.bitpos() >> 3;  // absolute byte of the data
+        if (!bfinal && len == 0 && nlen == 0xFFFF) {
+            end_byte = b0 - off0;  // empty segment: the candidate is itself a marker
+        } else if (b0 + len > br.E || len > LN_OUT_CAP) {
+            flags |= SEGF_EXOTIC;
+        } else {
+            push(len);
+            push((uint32_t)(b0 - off0 - start));
+            outpos = len;
+            br.seek(b0 + len);
+            if (bfinal) {
+                fin = true;
+                end_byte = b0 + len - off0;
+            } else {
+                br.ensure(3);
+                const uint32_t f2 = br.bits(1), t2 = br.bits(2);
+                br.align();
+                br.ensure(32);
+                const uint32_t l2 = br.bits(16), n2 = br.bits(16);
+                if (f2 || t2 != 0 || l2 != 0 || n2 != 0xFFFF) flags |= SEGF_EXOTIC;
+                end_byte = (br.bitpos() >> 3) - off0;
+            }
+        }
+    } else if (btype == 3) {
+        flags |= SEGF_EXOTIC;  // reference: empty block, then more blocks -- not this layout
+    } else {
+        // ---- code lengths: counts per length (pass 1) ---------------------------------------
+        uint32_t hlit = 288, hdist = 32, lmaxl = 9, lmaxd = 5;
+        uint64_t lc0 = 0, lc1 = 0, dcn = 0;  // lit counts: l 1..6 / 7..9 in 10-bit fields; dist 8-bit
+        LaneIn saved;
+        if (btype == 1) {  // fixed code (RFC 1951 3.2.6): 24 x 7, 152 x 8, 112 x 9; 32 x 5
+            lc1 = 24ull | (152ull << 10) | (112ull << 20);
+            dcn = 32ull << (8 * 4);
+        } else {
+            br.ensure(14);
+            hlit = br.bits(5) + 257;
+            hdist = br.bits(5) + 1;
+            const uint32_t hclen = br.bits(4) + 4;
+            uint64_t pl = 0;  // 19 x 3-bit precode lengths, by symbol
+            for (uint32_t i = 0; i < hclen; i++) {
+                br.ensure(3);
+                pl |= (uint64_t)br.bits(3) << (3 * kLnPerm[i]);
+            }
+            if (hlit > 286 || hdist > 30) flags |= SEGF_EXOTIC;
+            // precode: counts (5-bit fields), completeness, next codes (8-bit fields)
+            uint64_t pc = 0;
+            for (uint32_t s = 0; s < 19; s++) {
+                const uint32_t l = (uint32_t)(pl >> (3 * s)) & 7;
+                if (l) pc += 1ull << (5 * l);
+            }
+            uint32_t kr = 0, code = 0;
+            uint64_t pn = 0;
+            for (uint32_t l = 1; l <= 7; l++) {
+                const uint32_t c = (uint32_t)(pc >> (5 * l)) & 31;
+                kr += c << (7 - l);
+                code = (code + ((uint32_t)(pc >> (5 * (l - 1))) & 31) * (l > 1)) << 1;
+                pn |= (uint64_t)code << (8 * l);
+            }
+            if (kr != 128) flags |= SEGF_EXOTIC;
+            // precode table fill, one entry (or one symbol) per iteration
+            {
+                uint32_t s = 0, frem = 0, fp = 0, fst = 0, fe = 0;
+                while (!flags && (s < 19 || frem)) {
+                    if (frem) {
+                        R[at(LN_PRE + fp)] = (uint8_t)fe;
+                        fp += fst;
+                        frem--;
+                    } else {
+                        const uint32_t l = (uint32_t)(pl >> (3 * s)) & 7;
+                        if (l) {
+                            const uint32_t c = (uint32_t)(pn >> (8 * l)) & 255;
+                            pn += 1ull << (8 * l);
+                            fp = bitrev(c, l);
+                            fst = 1u << l;
+                            frem = 128u >> l;
+                            fe = s | (l << 5);
+                        }
+                        s++;
+                    }
+                }
+            }
+            saved = br;
+            // pass 1: decode the code-length sequence, count lengths, reject quirks
+            uint32_t i = 0, prev = 0, lm = 0, dm = 0;
+            bool prevok = false;
+            const uint32_t total = hlit + hdist;
+            while (!flags && i < total) {
+                br.ensure(14);
+                const uint32_t e = R[at(LN_PRE + (uint32_t)(br.bb & 127))];
+                br.consume(e >> 5);
+                const uint32_t sym = e & 31;
+                uint32_t val = 0, run = 1;
+                if (sym < 16) {
+                    val = sym;
+                    prev = sym;
+                    prevok = true;
+                } else if (sym == 16) {
+                    if (!prevok || i == hlit) flags |= SEGF_EXOTIC;  // A-12 / sequence-start repeat
+                    val = prev;
+                    run = 3 + br.bits(2);
+                } else if (sym == 17) {
+                    run = 3 + br.bits(3);
+                    prevok = false;
+                } else {
+                    run = 11 + br.bits(7);
+                    prevok = false;
+                }
+                if ((i < hlit && i + run > hlit) || i + run > total) flags |= SEGF_EXOTIC;  // A-11
+                if (val) {
+                    if (i < hlit) {
+                        if (val > 9) flags |= SEGF_EXOTIC;
+                        else if (val <= 6) lc0 += (uint64_t)run << (10 * (val - 1));
+                        else lc1 += (uint64_t)run << (10 * (val - 7));
+                        lm = max(lm, val);
+                    } else {
+                        if (val > 6) flags |= SEGF_EXOTIC;
+                        else dcn += (uint64_t)run << (8 * (val - 1));
+                        dm = max(dm, val);
+                    }
+                }
+                i += run;
+            }
+            lmaxl = lm;
+            lmaxd = dm;
+        }
+        // ---- completeness (both codes must fill their table exactly) and next codes --------
+        uint64_t nl0 = 0, nl1 = 0, nd = 0;  // next code per length (10-bit / 8-bit fields)
+        if (!flags) {
+            uint32_t kl = 0, kd = 0, code = 0, prevc = 0;
+            for (uint32_t l = 1; l <= 9; l++) {
+                const uint32_t c = (uint32_t)((l <= 6 ? lc0 >> (10 * (l - 1)) : lc1 >> (10 * (l - 7))) & 1023);
+                kl += c << (9 - l);
+                code = (code + prevc) << 1;
+                prevc = c;
+                if (l <= 6) nl0 |= (uint64_t)code << (10 * (l - 1));
+                else nl1 |= (uint64_t)code << (10 * (l - 7));
+            }
+            code = 0;
+            prevc = 0;
+            for (uint32_t l = 1; l <= 6; l++) {
+                const uint32_t c = (uint32_t)(dcn >> (8 * (l - 1))) & 255;
+                kd += c << (6 - l);
+                code = (code + prevc) << 1;
+                prevc = c;
+                nd |= (uint64_t)code << (8 * (l - 1));
+            }
+            if (kl != 512 || kd != 64 || lmaxl == 0 || lmaxd == 0) flags |= SEGF_EXOTIC;
+        }
+        // ---- pass 2: re-decode the lengths (or walk the fixed runs) and fill the tables ----
+        if (!flags) {
+            if (btype == 2) br = saved;
+            const uint32_t total = hlit + hdist;
+            uint32_t i = 0, runrem = 0, runval = 0, fk = 0, prev = 0;
+            uint32_t frem = 0, fp = 0, fst = 0, fe = 0, fb = 0;
+            while (i < total || frem) {
+                if (frem) {
+                    *reinterpret_cast<uint16_t*>(R + at(fb + 2 * fp)) = (uint16_t)fe;
+                    fp += fst;
+                    frem--;
+                } else if (runrem) {
+                    const uint32_t s = i++;
+                    runrem--;
+                    const uint32_t l = runval;
+                    if (l) {
+                        fst = 1u << l;
+                        if (s < hlit) {
+                            const bool lo = l <= 6;
+                            const uint32_t sh = 10 * (lo ? l - 1 : l - 7);
+                            const uint32_t c = (uint32_t)((lo ? nl0 : nl1) >> sh) & 1023;
+                            nl0 += lo ? 1ull << sh : 0ull;
+                            nl1 += lo ? 0ull : 1ull << sh;
+                            fp = bitrev(c, l);
+                            frem = (1u << lmaxl) >> l;
+                            fe = ln_lit_entry(s, l);
+                            fb = 0;
+                        } else {
+                            const uint32_t sh = 8 * (l - 1);
+                            const uint32_t c = (uint32_t)(nd >> sh) & 255;
+                            nd += 1ull << sh;
+                            fp = bitrev(c, l);
+                            frem = (1u << lmaxd) >> l;
+                            fe = 0x8000u | (l << 8) | (s - hlit);
+                            fb = LN_DIST;
+                        }
+                    }
+                } else if (btype == 1) {  // fixed: (8 x 144) (9 x 112) (7 x 24) (8 x 8) (5 x 32)
+                    runval = (0x58798u >> (4 * fk)) & 15;
+                    runrem = (uint32_t)(0x2008187090ull >> (8 * fk)) & 255;
+                    fk++;
+                } else {
+                    br.ensure(14);
+                    const uint32_t e = R[at(LN_PRE + (uint32_t)(br.bb & 127))];
+                    br.consume(e >> 5);
+                    const uint32_t sym = e & 31;
+                    if (sym < 16) {
+                        runval = sym;
+                        prev = sym;
+                        runrem = 1;
+                    } else if (sym == 16) {
+                        runval = prev;
+                        runrem = 3 + br.bits(2);
+                    } else if (sym == 17) {
+                        runval = 0;
+                        runrem = 3 + br.bits(3);
+                    } else {
+                        runval = 0;
+                        runrem = 11 + br.bits(7);
+                    }
+                }
+            }
+        }
+        // ---- tokens until end-of-block -------------------------------------------------------
+        if (!flags) {
+            const uint32_t lmask = (1u << lmaxl) - 1u, dmask = (1u << lmaxd) - 1u;
+            bool going = true;
+            while (going) {
+                if (br.nb < 32) br.refill();
+                const uint32_t e = lut16(2 * (uint32_t)(br.bb & lmask));
+                const uint32_t cl = (e >> 11) & 15;
+                if (e & 0x8000u) {
+                    const uint32_t ex = (e >> 8) & 7;
+                    const uint32_t L = (e & 255) + 3 + ((uint32_t)(br.bb >> cl) & ((1u << ex) - 1u));
+                    br.consume(cl + ex);
+                    if (br.nb < 19) br.refill();
+                    const uint32_t de = lut16(LN_DIST + 2 * (uint32_t)(br.bb & dmask));
+                    const uint32_t dcl = (de >> 8) & 7, ds = de & 31;
+                    const uint32_t dx = dist_extra(ds);
+                    const uint32_t d = dist_base(ds) + ((uint32_t)(br.bb >> dcl) & ((1u << dx) - 1u));
+                    br.consume(dcl + dx);
+                    if (ds >= 30) {
+                        flags |= SEGF_EXOTIC;  // reference: distance symbols 30/31 = distance 0
+                        going = false;
+                    } else if (d > outpos) {
+                        if (j != 0) {
+                            flags |= SEGF_XREF;
+                            going = false;
+                        }  // stream start: the reference copies nothing
+                    } else if (outpos + L > LN_OUT_CAP) {
+                        flags |= SEGF_EXOTIC;
+                        going = false;
+                    } else {
+                        if (pk == 2 && pd == d && pa + L <= 0xFFFFu) {
+                            pa += L;
+                        } else {
+                            flushp();
+                            pk = 2;
+                            pa = L;
+                            pd = d;
+                        }
+                        outpos += L;
+                    }
+                } else {
+                    const uint32_t sym = e & 511;
+                    br.consume(cl);
+                    if (sym < 256) {
+                        if (outpos >= LN_OUT_CAP) {
+                            flags |= SEGF_EXOTIC;
+                            going = false;
+                        } else {
+                            if (pk == 1 && pd < 3) {
+                                pa |= sym << (8 * pd);
+                                pd++;
+                            } else {
+                                flushp();
+                                pk = 1;
+                                pa = sym;
+                                pd = 1;
+                            }
+                            outpos++;
+                        }
+                    } else {
+                        if (sym != 256) flags |= SEGF_EXOTIC;  // 286/287: reference length 0
+                        going = false;
+                    }
+                }
+                if (br.bitpos() > 8 * br.E) {
+                    flags |= SEGF_EXOTIC;  // over-read: the exact decoder decides
+                    going = false;
+                }
+            }
+        }
+        // ---- what follows the block: BFINAL, or the empty stored block of a segment end ------
+        if (!flags) {
+            if (bfinal) {
+                fin = true;
+                end_byte = ((br.bitpos() + 7) >> 3) - off0;
+            } else {
+                br.ensure(3);
+                const uint32_t f2 = br.bits(1), t2 = br.bits(2);
+                br.align();
+                br.ensure(32);
+                const uint32_t l2 = br.bits(16), n2 = br.bits(16);
+                if (f2 || t2 != 0 || l2 != 0 || n2 != 0xFFFF) flags |= SEGF_EXOTIC;
+                end_byte = (br.bitpos() >> 3) - off0;
+            }
+        }
+    }
+    if (br.bitpos() > 8 * br.E) flags |= SEGF_EXOTIC;
+    flushp();
+    if (qn) {  // the queue's last partial group: the newest qn words, q[4 - qn .. 3]
+        if (ntok + qn <= tcap) {
+            if (qn == 3) {
+                tk[ntok] = q1;
+                tk[ntok + 1] = q2;
+                tk[ntok + 2] = q3;
+            } else if (qn == 2) {
+                tk[ntok] = q2;
+                tk[ntok + 1] = q3;
+            } else {
+                tk[ntok] = q3;
+            }
+        }
+        ntok += qn;
+    }
+    if (ntok > tcap) flags |= SEGF_EXOTIC;
+    SegRecord r;
+    r.end_byte = end_byte;
+    r.offset = j * (uint64_t)A.slot;
+    r.out_size = flags ? 0u : outpos;
+    r.flags = flags | (fin ? SEGF_FINAL : 0u);
+    A.recs[j] = r;
+    B.ntok[j] = ntok;
+}
+
+// token-list capacity per candidate: min(32 KiB of tokens, one per compressed bit) + 16,
+// rounded to whole 16-byte groups
+__global__ void k_lane_caps(const uint64_t* cands, uint64_t ncand, uint64_t n, uint32_t* caps) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ncand) return;
+    const uint64_t nxt = j + 1 < ncand ? cands[j + 1] : n;
+    const uint64_t bits = 8 * (nxt - cands[j]);
+    const uint64_t c = min(bits, (uint64_t)LN_OUT_CAP) + 16;
+    caps[j] = (uint32_t)((c + 3) & ~3ull);
+}
+
+// wave-cooperative periodic copy out[o + i] = out[o - d + (i mod d)], i < L (every source
+// byte precedes o, so all lanes copy independently); 4 bytes per lane per 256-byte step
+__device__ __forceinline__ void ln_copy_wave(uint8_t* win, uint32_t o, uint32_t L, uint32_t d) {
+    const uint32_t lane = lane_id();
+    const uint32_t src = o - d;
+    uint32_t r = (4 * lane) % d;             // (i mod d) for i = 4 * lane
+    const uint32_t st = 256 % d;             // advance of (i mod d) per 256-byte step
+    for (uint32_t i0 = 0; i0 < L; i0 += 256) {
+        const uint32_t i = i0 + 4 * lane;
+        uint32_t r1 = r + 1, r2 = r + 2, r3 = r + 3;
+        if (r1 >= d) r1 -= d;
+        if (r2 >= d) r2 -= d;
+        if (r3 >= d) r3 -= d;
+        if (r2 >= d) r2 -= d;
+        if (r3 >= d) r3 -= d;
+        if (r3 >= d) r3 -= d;
+        const uint8_t b0 = win[src + r], b1 = win[src + r1], b2 = win[src + r2], b3 = win[src + r3];
+        if (i < L) win[o + i] = b0;
+        if (i + 1 < L) win[o + i + 1] = b1;
+        if (i + 2 < L) win[o + i + 2] = b2;
+        if (i + 3 < L) win[o + i + 3] = b3;
+        r += st;
+        if (r >= d) r -= d;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs B) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[LN_OUT_CAP + 64];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t j = blockIdx.x;
+    const SegRecord rec = A.recs[j];
+    if (rec.flags & ~SEGF_FINAL) return;
+    const uint64_t dst0 = j * (uint64_t)A.slot;
+    if (dst0 >= A.cap) return;
+    const uint32_t size = rec.out_size;
+    const uint32_t nb = (uint32_t)min((uint64_t)size, A.cap - dst0);
+    uint8_t* const dst = A.out + dst0;
+    const uint32_t n = B.ntok[j];
+    const uint32_t* const tk = B.tok + B.tokoff[j];
+    if (n == 0) return;
+    const uint32_t w0 = tk[0];
+    if ((w0 >> 24) == 0) {  // stored segment: HBM -> HBM
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(A.in_words) + A.misalign + A.cands[j] + tk[1];
+        for (uint32_t i = lane; i < nb; i += 64) dst[i] = src[i];
+        return;
+    }
+    uint32_t pos = 0;
+    for (uint32_t t0 = 0; t0 < n; t0 += 64) {
+        const uint32_t w = t0 + lane < n ? tk[t0 + lane] : 0u;
+        const bool ism = (w >> 31) != 0;
+        const uint32_t L = ism ? (w >> 15) & 0xFFFFu : (w >> 24) & 0x7Fu;
+        const uint32_t d = (w & 0x7FFFu) + 1;
+        const uint32_t inc = wave_incl_scan(L);
+        const uint32_t off = pos + inc - L;
+        const uint32_t tot = (uint32_t)__shfl(inc, 63, 64);
+        if (!ism) {
+            if (L > 0) win[off] = (uint8_t)w;
+            if (L > 1) win[off + 1] = (uint8_t)(w >> 8);
+            if (L > 2) win[off + 2] = (uint8_t)(w >> 16);
+        }
+        // short matches whose source lies before this step: each lane copies its own
+        const bool simple = ism && L <= 32 && off + min(L, d) <= pos + d;
+        if (simple) {
+            if (d >= 4) {
+                for (uint32_t i = 0; i < L; i += 4) {
+                    const uint32_t v = ld32u(reinterpret_cast<const uint32_t*>(win), off + i - d);
+                    win[off + i] = (uint8_t)v;
+                    if (i + 1 < L) win[off + i + 1] = (uint8_t)(v >> 8);
+                    if (i + 2 < L) win[off + i + 2] = (uint8_t)(v >> 16);
+                    if (i + 3 < L) win[off + i + 3] = (uint8_t)(v >> 24);
+                }
+            } else {
+                for (uint32_t i = 0; i < L; i++) win[off + i] = win[off + i - d];
+            }
+        }
+        wave_sync();
+        uint64_t m = __ballot(ism && !simple);
+        while (m) {
+            const int k = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t ok = (uint32_t)__shfl(off, k, 64);
+            const uint32_t Lk = (uint32_t)__shfl(L, k, 64);
+            const uint32_t dk = (uint32_t)__shfl(d, k, 64);
+            ln_copy_wave(win, ok, Lk, dk);
+            wave_sync();
+        }
+        pos += tot;
+    }
+    if ((((uintptr_t)dst) & 15) == 0) {
+        const uint32_t nv = nb / 16;
+        const uint4* s4 = reinterpret_cast<const uint4*>(win);
+        uint4* d4 = reinterpret_cast<uint4*>(dst);
+        for (uint32_t i = lane; i < nv; i += 64) d4[i] = s4[i];
+        for (uint32_t i = nv * 16 + lane; i < nb; i += 64) dst[i] = win[i];
+    } else {
+        for (uint32_t i = lane; i < nb; i += 64) dst[i] = win[i];
+    }
+}
+
+hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* tokoff,
+                                uint32_t* ntok, uint32_t* caps, hipStream_t st, hipEvent_t ev0,
+                                hipEvent_t ev1) {
+    if (ev0) (void)hipEventRecord(ev0, st);
+    const uint32_t g = (uint32_t)((A.ncand + 255) / 256);
+    hipLaunchKernelGGL(k_lane_caps, dim3(g), dim3(256), 0, st, A.cands, A.ncand, A.n, caps);
+    hipError_t e = launch_scan_u32(caps, tokoff, A.ncand, tokoff + A.ncand, st);
+    if (e != hipSuccess) return e;
+    LaneArgs B{tok, tokoff, ntok, caps};
+    hipLaunchKernelGGL(k_inflate_lanes, dim3((uint32_t)((A.ncand + 63) / 64)), dim3(64), 0, st, A, B);
+    hipLaunchKernelGGL(k_inflate_resolve, dim3((uint32_t)A.ncand), dim3(64), 0, st, A, B);
+    if (ev1) (void)hipEventRecord(ev1, st);
+    return hipGetLastError();
+}
+
+}  // namespace dmx
