@@ -7,7 +7,8 @@
 //     [   0, 1024)  lit/len lookup table, 512 x u16, indexed by the next <= 9 stream bits
 //     [1024, 1152)  distance lookup table, 64 x u16 (<= 6-bit codes)
 //     [1152, 1280)  code-length (precode) lookup table, 128 x u8 (<= 7-bit codes, RFC 1951)
-// 64 lanes x 1280 B = 80 KiB per workgroup, two workgroups per CU: 32768 lanes on 256 CUs.
+// 16 lanes x 1280 B = 20 KiB per workgroup (a quarter wave: the decode is issue-bound, so eight
+// one-wave workgroups per CU put two waves on every SIMD): 32768 lanes on 256 CUs.
 // The block header is read twice (pass 1 counts the code lengths, pass 2 re-decodes them and
 // fills the tables), so no per-symbol code-length array is stored; per-length counters and
 // next-code values live in packed registers (dynamic "indexing" by shifts).  The decoded
@@ -41,52 +42,83 @@ constexpr uint32_t LN_REGION = 1280;
 constexpr uint32_t LN_DIST = 1024;
 constexpr uint32_t LN_PRE = 1152;
 constexpr uint32_t LN_OUT_CAP = 32768;
+constexpr uint32_t LN_LANES = 16;  // segments per 64-thread workgroup: 16 x 1280 B = 20 KiB of LDS,
+                                   // eight workgroups per CU, two decoding waves on every SIMD
+                                   // (the decode is issue-bound: lanes per wave cost nothing,
+                                   // waves per SIMD double the issue rate)
 
 __constant__ const uint8_t kLnPerm[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5,
                                           11, 4,  12, 3, 13, 2, 14, 1, 15};
 
-// per-lane LSB-first bit reader over the stream in HBM: 64-bit bit buffer, the current 16-byte
-// block and one prefetched block (its load is in flight while the current one is consumed).
-// Positions are bytes from blk (the 16-byte aligned base); bytes at or past E read as zero.
+// per-lane LSB-first bit reader over the stream in HBM: a 64-bit bit buffer fed from a ring
+// of eight 16-byte quads held in VGPRs (quad q of the stream lives in Q[q & 7]).  Loads are
+// issued only in wave-wide top-ups (every lane refills all its consumed quads at once, one
+// memory latency for the wave), never one lane at a time: s_waitcnt is per wave, so a lane's
+// lone reload would stall all 64.  Positions are bytes from blk (the 16-byte aligned base);
+// bytes at or past E read as zero.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 GUint4;  // global, not flat: a flat
+                                                               // load also counts in lgkmcnt
+constexpr uint32_t LN_RING_LOW = 16;  // top up when fewer words than this are buffered
+
 struct LaneIn {
-    const uint4* blk;
+    GUint4* blk;
     uint64_t nblk, E;
-    uint4 cur, nxt;
-    uint64_t pb, wi;  // next block to fetch; absolute index of the next word to shift in
-    uint32_t ci, nb;  // word index in cur; valid bits in bb
+    u32x4 Q0, Q1, Q2, Q3, Q4, Q5, Q6, Q7;
+    uint64_t fq;  // quads [.., fq) are in the ring
+    uint64_t wi;  // absolute index of the next word to shift into bb
+    uint32_t nb;  // valid bits in bb
     uint64_t bb;
-    __device__ __forceinline__ uint4 fetch(uint64_t b) const {
-        return b < nblk ? blk[b] : make_uint4(0, 0, 0, 0);
+    // clamped to the last block (refill() zeroes bytes past E), so the load is unconditional
+    // within the lanes that issue it
+    __device__ __forceinline__ u32x4 fetch(uint64_t b) const { return blk[min(b, nblk - 1)]; }
+    __device__ __forceinline__ bool low() const { return fq * 4 < wi + LN_RING_LOW; }
+    // load quads [fq, wi/4 + 8): slot k gets the quad q == k (mod 8) in that range, or --
+    // when there is none -- its current quad again (same bytes), so all eight loads are
+    // unconditional.  The addresses are pinned in registers of their own before the first
+    // load: computed inside the loads' registers, each would first wait for the previous
+    // top-up's load there (vmcnt(0), which also drains the loads just issued).
+    __device__ __forceinline__ void topup() {
+        const uint64_t lim = (wi >> 2) + 8, last = nblk - 1;
+        uint64_t a[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) {
+            uint64_t q = fq + ((uint64_t)(k - (uint32_t)fq) & 7u);
+            if (q >= lim) q -= 8;
+            a[k] = reinterpret_cast<uint64_t>(blk + min(q, last));
+        }
+        asm volatile("" : : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]),
+                     "v"(a[6]), "v"(a[7]));
+        Q0 = *reinterpret_cast<GUint4*>(a[0]);
+        Q1 = *reinterpret_cast<GUint4*>(a[1]);
+        Q2 = *reinterpret_cast<GUint4*>(a[2]);
+        Q3 = *reinterpret_cast<GUint4*>(a[3]);
+        Q4 = *reinterpret_cast<GUint4*>(a[4]);
+        Q5 = *reinterpret_cast<GUint4*>(a[5]);
+        Q6 = *reinterpret_cast<GUint4*>(a[6]);
+        Q7 = *reinterpret_cast<GUint4*>(a[7]);
+        fq = lim;
     }
-    __device__ __forceinline__ void refill() {  // requires nb <= 32
-        uint32_t w = cur.x;  // cur is a queue: shift instead of indexing (keeps it in VGPRs)
-        cur.x = cur.y;
-        cur.y = cur.z;
-        cur.z = cur.w;
+    __device__ __forceinline__ uint32_t word() const {
+        const uint32_t qs = (uint32_t)(wi >> 2) & 7, ws = (uint32_t)wi & 3;
+        const bool b0 = qs & 1, b1 = qs & 2, b2 = qs & 4;
+        const u32x4 p01 = b0 ? Q1 : Q0, p23 = b0 ? Q3 : Q2, p45 = b0 ? Q5 : Q4, p67 = b0 ? Q7 : Q6;
+        const u32x4 p03 = b1 ? p23 : p01, p47 = b1 ? p67 : p45;
+        const u32x4 q = b2 ? p47 : p03;
+        return (ws & 2) ? ((ws & 1) ? q.w : q.z) : ((ws & 1) ? q.y : q.x);
+    }
+    __device__ __forceinline__ void refill() {  // requires nb <= 32 and a word in the ring
+        uint32_t w = word();
         const uint64_t wb = wi * 4;
         if (wb + 4 > E) w = wb >= E ? 0u : (w & ((1u << (8 * (uint32_t)(E - wb))) - 1u));
         bb |= (uint64_t)w << nb;
         nb += 32;
         wi++;
-        if (++ci == 4) {
-            ci = 0;
-            cur = nxt;
-            nxt = fetch(pb);
-            pb++;
-        }
     }
     __device__ void seek(uint64_t abyte) {
-        const uint64_t b = abyte >> 4;
-        cur = fetch(b);
-        nxt = fetch(b + 1);
-        pb = b + 2;
-        ci = (uint32_t)(abyte >> 2) & 3;
         wi = abyte >> 2;
-        for (uint32_t k = 0; k < ci; k++) {  // drop the words before the start
-            cur.x = cur.y;
-            cur.y = cur.z;
-            cur.z = cur.w;
-        }
+        fq = wi >> 2;
+        topup();
         bb = 0;
         nb = 0;
         refill();
@@ -128,10 +160,11 @@ __device__ __forceinline__ uint32_t ln_lit_entry(uint32_t s, uint32_t l) {
 }
 
 __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[64 * LN_REGION];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LN_LANES * LN_REGION];
     const uint32_t lane = threadIdx.x;
-    const uint64_t j = (uint64_t)blockIdx.x * 64 + lane;
-    if (j >= A.ncand) return;  // lanes are independent: no barrier anywhere in this kernel
+    const uint64_t j = (uint64_t)blockIdx.x * LN_LANES + lane;
+    // lanes are independent: no barrier anywhere in this kernel
+    if (lane >= LN_LANES || j >= A.ncand) return;
     uint8_t* const R = lds + lane * LN_REGION;
     const uint32_t rot = 4 * lane;  // rotate each lane's region by one bank per lane
     auto at = [&](uint32_t b) -> uint32_t {
@@ -144,10 +177,13 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
     const uintptr_t base16 = base4 & ~(uintptr_t)15;
     const uint64_t off0 = (uint64_t)(base4 - base16) + A.misalign;  // stream byte 0
     LaneIn br;
-    br.blk = reinterpret_cast<const uint4*>(base16);
+    br.blk = (GUint4*)base16;
     br.E = off0 + A.n;
     br.nblk = (br.E + 15) / 16;
     const uint64_t start = A.cands[j];
+    uint64_t* const dbg = A.dbg ? A.dbg + j * kPhaseSlots : nullptr;  // DMX_PHASES developer aid
+    uint32_t n_iter = 0, n_top = 0;
+    if (dbg) dbg[0] = __builtin_amdgcn_s_memtime();
     br.seek(off0 + start);
 
     uint32_t flags = 0, outpos = 0;
@@ -157,6 +193,9 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
     // token output: pending token (merges), 4-word queue, 16-byte stores
     uint32_t* const tk = B.tok + B.tokoff[j];
     const uint32_t tcap = B.caps[j];
+    // consume the loads above now: a later first use would wait with vmcnt(0), draining the
+    // stream prefetch in flight at that point
+    if (tcap == 0 || (reinterpret_cast<uintptr_t>(tk) & 15)) flags |= SEGF_EXOTIC;
     uint32_t ntok = 0, qn = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;
     uint32_t pk = 0, pa = 0, pd = 0;  // pending: kind (1 literal run, 2 match), bytes / L, count / d
     auto push = [&](uint32_t w) {
@@ -271,6 +310,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             bool prevok = false;
             const uint32_t total = hlit + hdist;
             while (!flags && i < total) {
+                if (__any(br.low())) br.topup();
                 br.ensure(14);
                 const uint32_t e = R[at(LN_PRE + (uint32_t)(br.bb & 127))];
                 br.consume(e >> 5);
@@ -309,6 +349,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             lmaxl = lm;
             lmaxd = dm;
         }
+        if (dbg) dbg[1] = __builtin_amdgcn_s_memtime();
         // ---- completeness (both codes must fill their table exactly) and next codes --------
         uint64_t nl0 = 0, nl1 = 0, nd = 0;  // next code per length (10-bit / 8-bit fields)
         if (!flags) {
@@ -339,6 +380,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             uint32_t i = 0, runrem = 0, runval = 0, fk = 0, prev = 0;
             uint32_t frem = 0, fp = 0, fst = 0, fe = 0, fb = 0;
             while (i < total || frem) {
+                if (__any(br.low())) br.topup();
                 if (frem) {
                     *reinterpret_cast<uint16_t*>(R + at(fb + 2 * fp)) = (uint16_t)fe;
                     fp += fst;
@@ -395,11 +437,17 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
                 }
             }
         }
+        if (dbg) dbg[2] = __builtin_amdgcn_s_memtime();
         // ---- tokens until end-of-block -------------------------------------------------------
         if (!flags) {
             const uint32_t lmask = (1u << lmaxl) - 1u, dmask = (1u << lmaxd) - 1u;
             bool going = true;
             while (going) {
+                if (dbg) n_iter++;
+                if (__any(br.low())) {
+                    br.topup();
+                    if (dbg) n_top++;
+                }
                 if (br.nb < 32) br.refill();
                 const uint32_t e = lut16(2 * (uint32_t)(br.bb & lmask));
                 const uint32_t cl = (e >> 11) & 15;
@@ -465,6 +513,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
                 }
             }
         }
+        if (dbg) dbg[3] = __builtin_amdgcn_s_memtime();
         // ---- what follows the block: BFINAL, or the empty stored block of a segment end ------
         if (!flags) {
             if (bfinal) {
@@ -506,6 +555,13 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
     r.flags = flags | (fin ? SEGF_FINAL : 0u);
     A.recs[j] = r;
     B.ntok[j] = ntok;
+    if (dbg) {
+        dbg[4] = __builtin_amdgcn_s_memtime();
+        dbg[8] = n_iter;
+        dbg[9] = n_top;
+        dbg[10] = ntok;
+        dbg[11] = outpos;
+    }
 }
 
 // token-list capacity per candidate: min(32 KiB of tokens, one per compressed bit) + 16,
@@ -519,27 +575,48 @@ __global__ void k_lane_caps(const uint64_t* cands, uint64_t ncand, uint64_t n, u
     caps[j] = (uint32_t)((c + 3) & ~3ull);
 }
 
-// wave-cooperative periodic copy out[o + i] = out[o - d + (i mod d)], i < L (every source
-// byte precedes o, so all lanes copy independently); 4 bytes per lane per 256-byte step
+// wave-cooperative periodic copy out[o + i] = out[o - d + (i mod d)], i < L.  Every source
+// byte precedes o, so all lanes copy independently.  The body is written as aligned dwords
+// (one per lane per 256-byte step): a dword whose 4 source bytes do not wrap the period is
+// one unaligned LDS read (two aligned words + alignbyte); the unaligned head / tail bytes and
+// the wrapping dwords go byte by byte.
+__device__ __forceinline__ uint32_t ln_mod_small(uint32_t x, uint32_t d) {  // x < d + 3
+    if (x >= d) x -= d;
+    if (x >= d) x -= d;
+    if (x >= d) x -= d;
+    return x;
+}
 __device__ __forceinline__ void ln_copy_wave(uint8_t* win, uint32_t o, uint32_t L, uint32_t d) {
     const uint32_t lane = lane_id();
-    const uint32_t src = o - d;
-    uint32_t r = (4 * lane) % d;             // (i mod d) for i = 4 * lane
-    const uint32_t st = 256 % d;             // advance of (i mod d) per 256-byte step
-    for (uint32_t i0 = 0; i0 < L; i0 += 256) {
-        const uint32_t i = i0 + 4 * lane;
-        uint32_t r1 = r + 1, r2 = r + 2, r3 = r + 3;
-        if (r1 >= d) r1 -= d;
-        if (r2 >= d) r2 -= d;
-        if (r3 >= d) r3 -= d;
-        if (r2 >= d) r2 -= d;
-        if (r3 >= d) r3 -= d;
-        if (r3 >= d) r3 -= d;
-        const uint8_t b0 = win[src + r], b1 = win[src + r1], b2 = win[src + r2], b3 = win[src + r3];
-        if (i < L) win[o + i] = b0;
-        if (i + 1 < L) win[o + i + 1] = b1;
-        if (i + 2 < L) win[o + i + 2] = b2;
-        if (i + 3 < L) win[o + i + 3] = b3;
+    uint32_t* const W = reinterpret_cast<uint32_t*>(win);
+    const uint32_t src = o - d, end = o + L;
+    const uint32_t a0 = min((o + 3) & ~3u, end);  // first aligned body byte
+    const uint32_t a1 = max(a0, end & ~3u);       // first tail byte
+    const uint32_t nw = (a1 - a0) >> 2;
+    if (d >= L) {  // plain copy (i mod d == i): no division, no wrap
+        if (lane < a0 - o) win[o + lane] = win[src + lane];
+        if (lane < end - a1) win[a1 + lane] = win[src + (a1 - o) + lane];
+        for (uint32_t k = lane; k < nw; k += 64) W[(a0 >> 2) + k] = ld32u(W, src + (a0 - o) + 4 * k);
+        return;
+    }
+    if (lane < a0 - o) win[o + lane] = win[src + ln_mod_small(lane, d)];
+    if (lane < end - a1) {
+        const uint32_t i = a1 - o + lane;
+        win[a1 + lane] = win[src + i % d];
+    }
+    if (nw == 0) return;
+    uint32_t r = (a0 - o + 4 * lane) % d;  // (i mod d) of this lane's first dword
+    const uint32_t st = 256 % d;
+    for (uint32_t k = lane; k < nw; k += 64) {
+        uint32_t v;
+        if (r + 4 <= d) {
+            v = ld32u(W, src + r);
+        } else {
+            v = (uint32_t)win[src + r] | ((uint32_t)win[src + ln_mod_small(r + 1, d)] << 8) |
+                ((uint32_t)win[src + ln_mod_small(r + 2, d)] << 16) |
+                ((uint32_t)win[src + ln_mod_small(r + 3, d)] << 24);
+        }
+        W[(a0 >> 2) + k] = v;
         r += st;
         if (r >= d) r -= d;
     }
@@ -560,12 +637,30 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
     const uint32_t* const tk = B.tok + B.tokoff[j];
     if (n == 0) return;
     const uint32_t w0 = tk[0];
-    if ((w0 >> 24) == 0) {  // stored segment: HBM -> HBM
+    if ((w0 >> 24) == 0) {  // stored segment: 16-byte loads into LDS, 16-byte stores out
         const uint8_t* src = reinterpret_cast<const uint8_t*>(A.in_words) + A.misalign + A.cands[j] + tk[1];
-        for (uint32_t i = lane; i < nb; i += 64) dst[i] = src[i];
+        const uintptr_t s16 = reinterpret_cast<uintptr_t>(src) & ~(uintptr_t)15;
+        const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(src) - s16);
+        const uint32_t nblk = (sh + nb + 15) / 16;  // <= 2049 blocks: fits the window + pad
+        const uint4* g = reinterpret_cast<const uint4*>(s16);
+        uint4* w4 = reinterpret_cast<uint4*>(win);
+        for (uint32_t i = lane; i < nblk; i += 64) w4[i] = g[i];
+        wave_sync();
+        const uint32_t* W = reinterpret_cast<const uint32_t*>(win);
+        if ((((uintptr_t)dst) & 15) == 0) {
+            uint4* d4 = reinterpret_cast<uint4*>(dst);
+            for (uint32_t i = lane; i < nb / 16; i += 64)
+                d4[i] = make_uint4(ld32u(W, sh + 16 * i), ld32u(W, sh + 16 * i + 4),
+                                   ld32u(W, sh + 16 * i + 8), ld32u(W, sh + 16 * i + 12));
+            for (uint32_t i = (nb & ~15u) + lane; i < nb; i += 64) dst[i] = win[sh + i];
+        } else {
+            for (uint32_t i = lane; i < nb; i += 64) dst[i] = win[sh + i];
+        }
         return;
     }
-    uint32_t pos = 0;
+    uint64_t* const dbg = (A.dbg && lane == 0) ? A.dbg + j * kPhaseSlots : nullptr;
+    if (dbg) dbg[5] = __builtin_amdgcn_s_memtime();
+    uint32_t pos = 0, n_cx = 0;
     for (uint32_t t0 = 0; t0 < n; t0 += 64) {
         const uint32_t w = t0 + lane < n ? tk[t0 + lane] : 0u;
         const bool ism = (w >> 31) != 0;
@@ -573,7 +668,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
         const uint32_t d = (w & 0x7FFFu) + 1;
         const uint32_t inc = wave_incl_scan(L);
         const uint32_t off = pos + inc - L;
-        const uint32_t tot = (uint32_t)__shfl(inc, 63, 64);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         if (!ism) {
             if (L > 0) win[off] = (uint8_t)w;
             if (L > 1) win[off + 1] = (uint8_t)(w >> 8);
@@ -599,13 +694,18 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
         while (m) {
             const int k = __builtin_ctzll(m);
             m &= m - 1;
-            const uint32_t ok = (uint32_t)__shfl(off, k, 64);
-            const uint32_t Lk = (uint32_t)__shfl(L, k, 64);
-            const uint32_t dk = (uint32_t)__shfl(d, k, 64);
+            const uint32_t ok = (uint32_t)__builtin_amdgcn_readlane((int)off, k);
+            const uint32_t Lk = (uint32_t)__builtin_amdgcn_readlane((int)L, k);
+            const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)d, k);
             ln_copy_wave(win, ok, Lk, dk);
             wave_sync();
+            n_cx++;
         }
         pos += tot;
+    }
+    if (dbg) {
+        dbg[6] = __builtin_amdgcn_s_memtime();
+        dbg[12] = n_cx;
     }
     if ((((uintptr_t)dst) & 15) == 0) {
         const uint32_t nv = nb / 16;
@@ -616,6 +716,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
     } else {
         for (uint32_t i = lane; i < nb; i += 64) dst[i] = win[i];
     }
+    if (dbg) dbg[7] = __builtin_amdgcn_s_memtime();
 }
 
 hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* tokoff,
@@ -627,7 +728,7 @@ hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* t
     hipError_t e = launch_scan_u32(caps, tokoff, A.ncand, tokoff + A.ncand, st);
     if (e != hipSuccess) return e;
     LaneArgs B{tok, tokoff, ntok, caps};
-    hipLaunchKernelGGL(k_inflate_lanes, dim3((uint32_t)((A.ncand + 63) / 64)), dim3(64), 0, st, A, B);
+    hipLaunchKernelGGL(k_inflate_lanes, dim3((uint32_t)((A.ncand + LN_LANES - 1) / LN_LANES)), dim3(64), 0, st, A, B);
     hipLaunchKernelGGL(k_inflate_resolve, dim3((uint32_t)A.ncand), dim3(64), 0, st, A, B);
     if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();
