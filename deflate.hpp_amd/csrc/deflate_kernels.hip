@@ -34,7 +34,9 @@
 namespace dmx {
 
 constexpr int DF_NT = 1024;    // threads per workgroup (16 waves)
-constexpr int DF_CHUNK = 256;  // bytes per parse lane
+constexpr int DF_CHUNK = 258;  // bytes per parse lane: one maximal match per chunk, and not a
+                               // multiple of 256, so the lanes' chunk starts spread over the LDS
+                               // banks (at 256 every lane of a wave hit one bank per matchlen read)
 constexpr int DF_HB = 12;      // hash bits of each of the two match tables
 // Code-length limits of the emitted lit/len and distance codes.  RFC 1951 allows 15; 9 and 6
 // keep every code inside the one-level lookup tables of the lane decoder
@@ -197,7 +199,6 @@ __device__ void wave_build_lengths(const uint32_t* freq, int nsym, int maxbits, 
         if (s < nsym) lens[s] = 0;
     }
     const uint32_t F = wave_sum(fs), nz = wave_sum(nzs);
-    const uint32_t U = 1u << maxbits;
     if (nz <= 1) {
         uint32_t u = used;
 #pragma unroll
@@ -391,7 +392,7 @@ __device__ __forceinline__ RunPlan plan_run(uint32_t v, uint32_t r) {
 // ---------------------------------------------------------------------------------------
 template <int SEG>
 struct DfSmem {
-    static constexpr int NWALK = SEG / DF_CHUNK;
+    static constexpr int NWALK = (SEG + DF_CHUNK - 1) / DF_CHUNK;
     static constexpr int HT = 1 << DF_HB;  // entries per hash table
     static constexpr int UW0 = 2 * HT;
     static constexpr int UW1 = SEG / 4 + 64;
@@ -399,7 +400,8 @@ struct DfSmem {
     uint32_t data32[SEG / 4 + 16];
     uint16_t cand[SEG + 8];
     uint32_t U[UW];  // head[HT] | first[HT] while matching, the output bit image afterwards
-    uint32_t tokmap[SEG / 32];  // token-start bitmap
+    uint32_t mmap[SEG / 32];    // "a verified match of >= 3 starts here" (match rounds)
+    uint32_t tokmap[SEG / 32];  // token-start bitmap (parse walk; chunks share boundary words)
     uint32_t litfreq[288];
     uint32_t distfreq[32];
     uint32_t prefreq[32];
@@ -409,7 +411,7 @@ struct DfSmem {
     uint8_t litlen[288];
     uint8_t distlen[32];
     uint8_t prelen[32];
-    uint32_t scan[2 * DF_NT / 64];
+    uint32_t scan[4 * DF_NT / 64];
     uint64_t runmask[6];
     uint32_t sh[48];
 };
@@ -452,24 +454,74 @@ __device__ void emit_stored(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t*
     if (t == 0) *size_out = total;
 }
 
-// bits of the tokens starting in bitmap word wi (token p: literal if cand[p] == 0, else a
-// match with distance cand[p] and length cand[p + 1])
+// Work units of 8 positions: unit u = byte (u & 3) of token-bitmap word u >> 2.  Thread t owns
+// units t, t + DF_NT, t + 2 DF_NT, ... so a dense stretch of tokens (a literal run) is spread
+// over many threads instead of landing on a few word owners.
 template <int SEG>
-__device__ __forceinline__ uint32_t word_bits(const DfSmem<SEG>& S, uint32_t wi) {
-    uint32_t w = S.tokmap[wi], bits = 0;
-    while (w) {
-        const uint32_t p = wi * 32 + __builtin_ctz(w);
-        w &= w - 1;
-        const uint32_t d = S.cand[p];
-        if (d) {
-            const uint32_t L = S.cand[p + 1];
-            const uint32_t ls = len_sym(L), ds = dist_sym(d);
-            bits += (S.litcode[ls] >> 16) + len_extra(ls) + (S.distcode[ds] >> 16) + dist_extra(ds);
-        } else {
-            bits += S.litcode[data_byte(S.data32, p)] >> 16;
-        }
+struct Units {
+    static constexpr int N = SEG / 8;
+    static constexpr int PER = N / DF_NT;  // units per thread (4 at 32 KiB, 2 at 16 KiB)
+};
+// the thread's units as one 32-bit mask: byte k = unit k * DF_NT + t (UPT <= 4), so a single
+// token loop walks all of them (the wave iterates max-over-lanes of the thread's total tokens,
+// not the sum over units of per-unit maxima)
+template <int SEG>
+__device__ __forceinline__ uint32_t thread_units(const DfSmem<SEG>& S, uint32_t t) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < Units<SEG>::PER; k++) {
+        const uint32_t u = k * DF_NT + t;
+        m |= ((S.tokmap[u >> 2] >> ((u & 3) * 8)) & 0xFFu) << (8 * k);
     }
-    return bits;
+    return m;
+}
+// position of mask bit b of thread t
+__device__ __forceinline__ uint32_t unit_pos(uint32_t t, uint32_t b) {
+    return ((b >> 3) * DF_NT + t) * 8 + (b & 7);
+}
+
+// bits of the token starting at p (literal if cand[p] == 0, else a match with distance
+// cand[p] and length cand[p + 1])
+template <int SEG>
+__device__ __forceinline__ uint32_t token_bits(const DfSmem<SEG>& S, uint32_t p) {
+    const uint32_t d = S.cand[p];
+    if (d) {
+        const uint32_t L = S.cand[p + 1];
+        const uint32_t ls = len_sym(L), ds = dist_sym(d);
+        return (S.litcode[ls] >> 16) + len_extra(ls) + (S.distcode[ds] >> 16) + dist_extra(ds);
+    }
+    return S.litcode[data_byte(S.data32, p)] >> 16;
+}
+
+// exclusive block scan of K values per thread, in the order (k, thread): value k of thread t
+// is element k * DF_NT + t.  scratch holds K * DF_NT / 64 words.
+template <int K>
+__device__ void block_excl_scan_k(const uint32_t (&v)[K], uint32_t (&off)[K], uint32_t* scratch,
+                                  uint32_t* total) {
+    constexpr int NW = DF_NT / 64;
+    const int t = threadIdx.x, w = t >> 6;
+    uint32_t inc[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        inc[k] = wave_incl_scan(v[k]);
+        if ((t & 63) == 63) scratch[k * NW + w] = inc[k];
+    }
+    __syncthreads();
+    uint32_t base = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (int i = 0; i < NW; i++) {
+            const uint32_t x = scratch[k * NW + i];
+            if (i < w) pre += x;
+            tot += x;
+        }
+        off[k] = base + pre + inc[k] - v[k];
+        base += tot;
+    }
+    __syncthreads();
+    *total = base;
 }
 
 // Huffman (dynamic or fixed) block for the tokenized segment; returns false when a stored
@@ -477,7 +529,6 @@ __device__ __forceinline__ uint32_t word_bits(const DfSmem<SEG>& S, uint32_t wi)
 template <int SEG>
 __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t* slot,
                              uint32_t* size_out, uint64_t* dbg, uint64_t seg) {
-    constexpr int NMAP = SEG / 32;
     const int t = threadIdx.x;
 
     // ---- code lengths + canonical codes (wave 0: lit/len, wave 1: distance) -------------
@@ -485,7 +536,6 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t
         uint64_t wst[6] = {0, 0, 0, 0, 0, 0};
         wave_build_lengths(S.litfreq, 286, DF_LIT_MAXBITS, S.litlen, dbg ? wst : nullptr);
         if (dbg && t == 0) dbg[seg * kPhaseSlots + 11] = (wst[0] & 0xFFFF) | ((wst[1] & 0xFFFF) << 16) | ((wst[3] & 0xFFFF) << 32) | ((wst[4] & 0xFFFF) << 48);
-        if (dbg && t == 0) dbg[seg * kPhaseSlots + 15] = (wst[2] & 0xFFFF) | ((wst[5] & 0xFFFF) << 16);
         DMX_PHASE(dbg, seg, 12);
         wave_assign_codes(S.litlen, 286, S.litcode);
         DMX_PHASE(dbg, seg, 13);
@@ -586,10 +636,21 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t
         __syncthreads();
     }
 
-    // ---- token bits per bitmap word, block scan ------------------------------------------
-    const uint32_t mybits = (t < NMAP) ? word_bits(S, t) : 0;
+    // ---- token bits per unit, block scan -------------------------------------------------
+    constexpr int UPT = Units<SEG>::PER;
+    const uint32_t umask = thread_units(S, t);
+    uint32_t ubits[UPT], uoff[UPT];
+#pragma unroll
+    for (int k = 0; k < UPT; k++) ubits[k] = 0;
+    for (uint32_t m = umask; m;) {
+        const uint32_t b = __builtin_ctz(m);
+        m &= m - 1;
+        const uint32_t c = token_bits(S, unit_pos(t, b));
+#pragma unroll
+        for (int k = 0; k < UPT; k++) ubits[k] += (b >> 3) == (uint32_t)k ? c : 0u;
+    }
     uint32_t tok_total;
-    const uint32_t tok_off = block_excl_scan(mybits, S.scan, &tok_total);
+    block_excl_scan_k<UPT>(ubits, uoff, S.scan, &tok_total);
     const uint32_t hdr_end = 3 + (use_dyn ? hdr_bits : 0);
     DMX_PHASE(dbg, seg, 8);
 
@@ -635,13 +696,22 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t
         }
         bw.flush();
     }
-    if (t < NMAP && mybits) {
+    {
         BitOr bw;
-        bw.init(S.U, hdr_end + tok_off);
-        uint32_t w = S.tokmap[t];
-        while (w) {
-            const uint32_t p = t * 32 + __builtin_ctz(w);
-            w &= w - 1;
+        uint32_t cur = 0xFFFFFFFFu;
+        for (uint32_t m = umask; m;) {
+            const uint32_t b = __builtin_ctz(m);
+            m &= m - 1;
+            const uint32_t k = b >> 3;
+            if (k != cur) {  // next unit: its own bit offset
+                if (cur != 0xFFFFFFFFu) bw.flush();
+                uint32_t o = uoff[0];
+#pragma unroll
+                for (int q = 1; q < UPT; q++) o = k == (uint32_t)q ? uoff[q] : o;
+                bw.init(S.U, hdr_end + o);
+                cur = k;
+            }
+            const uint32_t p = unit_pos(t, b);
             const uint32_t d = S.cand[p];
             if (d) {
                 const uint32_t L = S.cand[p + 1];
@@ -659,7 +729,7 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t
                 bw.put(lc & 0xFFFF, lc >> 16);
             }
         }
-        bw.flush();
+        if (cur != 0xFFFFFFFFu) bw.flush();
     }
     // end of block, then (non-final) the byte-aligning empty stored block 000|pad|0000|FFFF
     const uint32_t eob_at = hdr_end + tok_total;
@@ -742,8 +812,16 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                     ok[k] = p[k] + 4 <= nb;
                     key[k] = ok[k] ? ld32u(S.data32, p[k]) : 0;
                     h[k] = ok[k] ? (key[k] * 0x1E35A7BDu) >> (32 - DF_HB) : 0;
-                    if (ok[k]) atomicMax(&first[h[k]], (rr << 16) | (0xFFFFu - p[k]));  // first in round
-                    if (pok[k]) atomicMax(&head[ph[k]], pp[k] + 1);                     // previous round
+                    // skip an update a neighbour position makes redundant (runs of equal keys
+                    // would otherwise serialize on one LDS address): the first occurrence needs
+                    // no write when position p - 1 has the same hash, the latest none when p + 1
+                    // has.  Neighbours come by DPP within rows of 16 lanes; row edges just write.
+                    const uint32_t hx = ok[k] ? h[k] : 0xFFFFFFFFu;
+                    const uint32_t hl = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)hx, 0x111, 0xF, 0xF, false);
+                    const uint32_t phx = pok[k] ? ph[k] : 0xFFFFFFFFu;
+                    const uint32_t phr = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)phx, 0x101, 0xF, 0xF, false);
+                    if (ok[k] && hl != hx) atomicMax(&first[h[k]], (rr << 16) | (0xFFFFu - p[k]));  // first in round
+                    if (pok[k] && phr != phx) atomicMax(&head[ph[k]], pp[k] + 1);                // previous round
                 }
                 __syncthreads();
 #pragma unroll
@@ -768,13 +846,12 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                         }
                     }
                     if (p[k] < nb) S.cand[p[k]] = (uint16_t)c;
-                    // bit p of tokmap = "a match of >= 3 starts at p" until the walk turns it
-                    // into token starts
+                    // bit p of mmap = "a match of >= 3 starts at p"
                     const uint64_t m = __ballot(c != 0);
                     const uint32_t w0 = (r0 + k * DF_NT + wave * 64) >> 5;
                     if (lane == 0 && w0 < NMAP) {
-                        S.tokmap[w0] = (uint32_t)m;
-                        if (w0 + 1 < NMAP) S.tokmap[w0 + 1] = (uint32_t)(m >> 32);
+                        S.mmap[w0] = (uint32_t)m;
+                        if (w0 + 1 < NMAP) S.mmap[w0 + 1] = (uint32_t)(m >> 32);
                     }
                     pok[k] = ok[k];
                     ph[k] = h[k];
@@ -786,31 +863,33 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
         }
         DMX_PHASE(A.dbg, seg, 2);
 
-        // ---- parse walk: one 256-byte chunk per lane; jumps over literal runs with the
-        //      match bitmap, turns it into the token-start bitmap in place ------------------
+        // ---- parse walk: one DF_CHUNK-byte chunk per lane; jumps over literal runs with the
+        //      match bitmap, ORs token starts into tokmap (neighbouring chunks share words) -----
+        if (A.dbg && t < 2) S.sh[40 + t] = 0;
+        __syncthreads();
         if (level >= 2 && t < NWALK) {
+            const uint64_t wt0 = A.dbg ? __builtin_amdgcn_s_memtime() : 0;
+            uint32_t nml = 0;
             const uint32_t lo = t * DF_CHUNK;
             const uint32_t hi = min(lo + DF_CHUNK, nb);
-            const uint32_t wlast = (hi - 1) >> 5;
             auto bits_range = [](uint32_t a, uint32_t b, uint32_t w) -> uint32_t {  // [a, b) in word w
                 const uint32_t e = b - w * 32;
                 return (e >= 32 ? 0xFFFFFFFFu : ((1u << e) - 1u)) & (0xFFFFFFFFu << (a & 31));
             };
             auto full_len = [&](uint32_t q) -> uint32_t {  // >= 3: verified in the rounds
+                nml++;
                 return matchlen(S.data32, q, q - S.cand[q], min(258u, hi - q));
             };
-            uint32_t p = lo, w = lo >> 5, mw = S.tokmap[w], tok = 0;
-            auto mbit = [&](uint32_t q) -> bool {  // original match bit (w or the word after)
-                const uint32_t wq = q >> 5;
-                return ((wq == w ? mw : S.tokmap[wq]) >> (q & 31)) & 1u;
+            uint32_t p = lo, w = lo >> 5, mw = S.mmap[w], tok = 0;
+            auto mbit = [&](uint32_t q) -> bool {
+                return (S.mmap[q >> 5] >> (q & 31)) & 1u;
             };
             while (p < hi) {
                 const uint32_t wi = p >> 5;
                 if (wi != w) {
-                    S.tokmap[w] = tok;
-                    for (uint32_t x = w + 1; x < wi; x++) S.tokmap[x] = 0;
+                    if (tok) atomicOr(&S.tokmap[w], tok);
                     w = wi;
-                    mw = S.tokmap[w];
+                    mw = S.mmap[w];
                     tok = 0;
                 }
                 const uint32_t m = mw & (0xFFFFFFFFu << (p & 31));
@@ -832,12 +911,34 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                         continue;
                     }
                 }
+                if (L >= 32) {
+                    // long match: prefer the smallest distance giving the same length -- a short
+                    // period (1..4) or a divisor c / k of the candidate (periodic data: a table,
+                    // an image row, a repeated record).  Equal distances of consecutive matches
+                    // are what the lane decoder merges into one periodic copy.
+                    const uint32_t c = S.cand[p];
+                    const uint32_t ml = min(258u, hi - p);
+                    uint32_t best = c;
+                    for (uint32_t dd = 1; dd <= 4 && dd < best; dd++)
+                        if (dd <= p && matchlen(S.data32, p, p - dd, ml) >= L) best = dd;
+                    if (best == c) {  // one probe at c / k, k the largest divisor <= 8 (a probe
+                                      // per k would serialize across lanes that differ in k)
+                        uint32_t k = 1;
+#pragma unroll
+                        for (uint32_t q = 2; q <= 8; q++) k = (c % q == 0) ? q : k;
+                        if (k > 1 && matchlen(S.data32, p, p - c / k, ml) >= L) best = c / k;
+                    }
+                    S.cand[p] = (uint16_t)best;
+                }
                 tok |= 1u << (p & 31);
                 S.cand[p + 1] = (uint16_t)L;
                 p += L;
             }
-            S.tokmap[w] = tok;
-            for (uint32_t x = w + 1; x <= wlast; x++) S.tokmap[x] = 0;
+            if (tok) atomicOr(&S.tokmap[w], tok);
+            if (A.dbg) {
+                atomicMax(&S.sh[40], (uint32_t)(__builtin_amdgcn_s_memtime() - wt0));
+                atomicMax(&S.sh[41], nml);
+            }
         }
         if (level < 2) {  // Huffman only: every position is a literal token
             for (uint32_t i = t; i < nb; i += DF_NT) S.cand[i] = 0;
@@ -848,12 +949,12 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
         }
         __syncthreads();
         DMX_PHASE(A.dbg, seg, 3);
+        if (A.dbg && t == 0) A.dbg[seg * kPhaseSlots + 15] = S.sh[40] | ((uint64_t)S.sh[41] << 32);
 
         // ---- histogram over token starts; the output image is zeroed meanwhile ------------
-        if (t < NMAP) {
-            uint32_t w = S.tokmap[t];
-            while (w) {
-                const uint32_t p = t * 32 + __builtin_ctz(w);
+        for (uint32_t w = thread_units(S, t); w;) {
+            {
+                const uint32_t p = unit_pos(t, __builtin_ctz(w));
                 w &= w - 1;
                 const uint32_t d = S.cand[p];
                 if (d) {

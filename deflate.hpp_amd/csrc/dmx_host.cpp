@@ -126,7 +126,7 @@ void phase_dump(dmx_ctx* c, const char* kernel, uint64_t nidx, hipStream_t st) {
         for (uint64_t i = 0; i < nidx; i++) {
             const uint64_t a = h[i * kPhaseSlots + 11], b = h[i * kPhaseSlots + 15];
             w[0] += a & 0xFFFF; w[1] += (a >> 16) & 0xFFFF; w[3] += (a >> 32) & 0xFFFF; w[4] += (a >> 48) & 0xFFFF;
-            w[2] += b & 0xFFFF; w[5] += (b >> 16) & 0xFFFF;
+            w[2] += b & 0xFFFFFFFF; w[5] += b >> 32;  // slot 15: slowest parse lane cycles / full_len calls
         }
         for (int k = 0; k < 6; k++) std::fprintf(f, " wb%d=%.0f", k, nidx ? w[k] / nidx : 0.0);
     }
@@ -185,6 +185,13 @@ int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, 
     A.out = d_out;
     A.cap = cap;
     A.dbg = phase_buf(c, nseg);
+    {
+        static const uint32_t dev_flags = [] {
+            const char* e = std::getenv("DMX_DF_FLAGS");
+            return e ? (uint32_t)std::atoi(e) : 0u;
+        }();
+        A.dev_flags = dev_flags;
+    }
     HIPCHK(launch_deflate(A, c->seg, st, c->timing ? c->ev[1] : nullptr, c->timing ? c->ev[2] : nullptr));
     if (A.dbg) phase_dump(c, "deflate", nseg, st);
     uint64_t total = 0;

@@ -19,6 +19,7 @@ struct DeflateArgs {
     uint8_t* out;
     uint64_t cap;
     uint64_t* dbg;        // optional per-block phase timestamps (DMX_PHASES), else nullptr
+    uint32_t dev_flags;   // developer experiments (DMX_DF_FLAGS), 0 in production
 };
 
 hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t st, hipEvent_t ev0,
