@@ -175,7 +175,8 @@ def main():
     # roofline of the dominant kernel: algorithmic bytes = N read + C written (deflate) or
     # C read + N written (inflate), per launch, over its HIP-event duration
     alg = n + comp_bytes
-    inf_kernel = "k_inflate_pj" if recs[-1][4].path == 3 else "k_inflate_segments"
+    path = recs[-1][4].path
+    inf_kernel = {3: "k_inflate_pj", 4: "k_inflate_lanes+k_inflate_resolve"}.get(path, "k_inflate_segments")
     dom = inf_kernel if k_inf >= k_def else "k_deflate_segments"
     kms = max(k_inf, k_def)
     achieved = alg / (kms * 1e-3) / 1e9

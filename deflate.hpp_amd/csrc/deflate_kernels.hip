@@ -83,34 +83,35 @@ __device__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* tot
 // the code is over-full, then shorten the first (most frequent) members while slack remains.
 // Ends with a complete code (Kraft sum exactly 2^maxbits), as zlib and the reference require.
 __device__ __forceinline__ void fit_classes(uint32_t (&cnt)[17], int maxbits) {
-    const uint32_t U = 1u << maxbits;
-    int64_t K = 0;
+    // Kraft sums in units of 2^-maxbits (<= 288 * 2^8: 32-bit); every class weight is a power
+    // of two, so the divisions are shifts
+    const int32_t U = 1 << maxbits;
+    int32_t K = 0;
 #pragma unroll
-    for (int L = 1; L <= 15; L++) K += (int64_t)cnt[L] * (int64_t)(U >> L);
-    while (K > (int64_t)U) {
+    for (int L = 1; L <= 15; L++) K += L <= maxbits ? (int32_t)cnt[L] << (maxbits - L) : 0;
+    while (K > U) {
 #pragma unroll
         for (int L = 14; L >= 1; L--) {
-            if (L < maxbits && K > (int64_t)U && cnt[L]) {
-                const int64_t gain = U >> (L + 1);
-                const int64_t need = (K - (int64_t)U + gain - 1) / gain;
-                const uint32_t k = (uint32_t)min(need, (int64_t)cnt[L]);
+            if (L < maxbits && K > U && cnt[L]) {
+                const int sh = maxbits - L - 1;  // gain of one lengthening: 2^sh
+                const uint32_t need = (uint32_t)((K - U + (1 << sh) - 1) >> sh);
+                const uint32_t k = min(need, cnt[L]);
                 cnt[L] -= k;
                 cnt[L + 1] += k;
-                K -= (int64_t)k * gain;
+                K -= (int32_t)k << sh;
             }
         }
     }
-    uint32_t R = (uint32_t)((int64_t)U - K);
+    uint32_t R = (uint32_t)(U - K);
     for (int pass = 0; pass < 64 && R; pass++) {
         bool changed = false;
 #pragma unroll
         for (int L = 2; L <= 15; L++) {
-            const uint32_t c = U >> L;
-            if (L <= maxbits && cnt[L] && c <= R) {
-                const uint32_t k = min(cnt[L], R / c);
+            if (L <= maxbits && cnt[L] && (1u << (maxbits - L)) <= R) {
+                const uint32_t k = min(cnt[L], R >> (maxbits - L));
                 cnt[L] -= k;
                 cnt[L - 1] += k;
-                R -= k * c;
+                R -= k << (maxbits - L);
                 changed = true;
             }
         }
@@ -176,81 +177,6 @@ __device__ void wave_build_lengths64(const uint32_t* freq, int nsym, int maxbits
     if (key >> 9) lens[511 - (key & 511)] = (uint8_t)L;
 }
 
-__device__ void wave_build_lengths(const uint32_t* freq, int nsym, int maxbits, uint8_t* lens,
-                                   uint64_t* st = nullptr) {
-    const int lane = lane_id();
-    uint64_t t0 = st ? __builtin_amdgcn_s_memtime() : 0;
-#define WB_STAMP(k)                                       \
-    if (st && lane == 0) {                                \
-        const uint64_t t1 = __builtin_amdgcn_s_memtime(); \
-        st[k] = t1 - t0;                                  \
-        t0 = t1;                                          \
-    }
-    uint32_t key[8];
-    uint32_t fs = 0, nzs = 0, used = 0;
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-        const int s = lane * 8 + r;
-        const uint32_t f = s < nsym ? freq[s] : 0;
-        key[r] = f ? (f << 9) | (511 - s) : 0;
-        fs += f;
-        nzs += f ? 1 : 0;
-        if (f) used = s + 1;
-        if (s < nsym) lens[s] = 0;
-    }
-    const uint32_t F = wave_sum(fs), nz = wave_sum(nzs);
-    if (nz <= 1) {
-        uint32_t u = used;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) u = max(u, __shfl_xor(u, d, 64));
-        if (lane == 0) {
-            if (u == 0) { lens[0] = 1; lens[1] = 1; }
-            else { lens[u - 1] = 1; lens[u - 1 == 0 ? 1 : 0] = 1; }
-        }
-        return;
-    }
-    WB_STAMP(0);
-    wave_sort512_desc(key);
-    WB_STAMP(1);
-    // Initial lengths round(log2(F/f)) clamped to [1, maxbits].  Frequencies are sorted in
-    // descending order by rank (rank = lane * 8 + r), so the lengths are non-decreasing in rank
-    // and every length class is a contiguous rank range.  The Kraft repair (lengthen the least
-    // frequent members of a class) and the slack fill (shorten the most frequent ones) keep
-    // that property, so both run on the 15 class sizes alone, in scalar code.
-    uint32_t len[8];
-#pragma unroll
-    for (int r = 0; r < 8; r++) len[r] = init_len(key[r] >> 9, F, maxbits);
-    WB_STAMP(2);
-    uint32_t cnt[17];
-    cnt[0] = cnt[16] = 0;
-#pragma unroll
-    for (int L = 1; L <= 15; L++) {
-        uint32_t c = 0;
-#pragma unroll
-        for (int r = 0; r < 8; r++) c += __popcll(__ballot(len[r] == (uint32_t)L));
-        cnt[L] = c;
-    }
-    WB_STAMP(3);
-    fit_classes(cnt, maxbits);
-    WB_STAMP(4);
-    // rank q has length = number of classes l in [1, 15] whose first rank S_l <= q
-    uint32_t S[16];
-    S[1] = 0;
-#pragma unroll
-    for (int L = 2; L <= 15; L++) S[L] = S[L - 1] + cnt[L - 1];
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-        if (!(key[r] >> 9)) continue;
-        const uint32_t q = (uint32_t)lane * 8 + r;
-        uint32_t L = 0;
-#pragma unroll
-        for (int l = 1; l <= 15; l++) L += q >= S[l] ? 1u : 0u;
-        lens[511 - (key[r] & 511)] = (uint8_t)L;
-    }
-    WB_STAMP(5);
-#undef WB_STAMP
-}
-
 // Canonical codes (RFC 1951 3.2.2; reference FlatHuffmanTree::construct common.hpp:104-145),
 // stored bit-reversed for the LSB-first bit packer: codes[s] = (len << 16) | rev(code).
 // One wavefront; per-length counts and ranks come from ballots over 64-symbol chunks.
@@ -304,6 +230,49 @@ struct BitOr {
         nacc += n;
         if (nacc >= 32) {
             atomicOr(&out[wi], (uint32_t)acc);
+            wi++;
+            acc >>= 32;
+            nacc -= 32;
+        }
+    }
+    __device__ void flush() {
+        if (nacc) atomicOr(&out[wi], (uint32_t)acc);
+    }
+};
+
+// The same for a thread that owns the bit range it writes: only the first and the last word
+// can be shared with a neighbouring range (atomicOr); the words between are plain stores.
+struct BitSt {
+    uint32_t* out;
+    uint64_t acc;
+    uint32_t nacc, wi;
+    bool shared;  // the current word is the range's first
+    __device__ void init(uint32_t* o, uint32_t bitpos) {
+        out = o;
+        wi = bitpos >> 5;
+        nacc = bitpos & 31;
+        acc = 0;
+        shared = true;
+    }
+    __device__ void put(uint32_t bits, uint32_t n) {  // n <= 32
+        acc |= (uint64_t)bits << nacc;
+        nacc += n;
+        if (nacc >= 32) {
+            if (shared) atomicOr(&out[wi], (uint32_t)acc);
+            else out[wi] = (uint32_t)acc;
+            shared = false;
+            wi++;
+            acc >>= 32;
+            nacc -= 32;
+        }
+    }
+    __device__ void put64(uint64_t bits, uint32_t n) {  // n <= 33 (nacc <= 31 on entry)
+        acc |= bits << nacc;
+        nacc += n;
+        while (nacc >= 32) {
+            if (shared) atomicOr(&out[wi], (uint32_t)acc);
+            else out[wi] = (uint32_t)acc;
+            shared = false;
             wi++;
             acc >>= 32;
             nacc -= 32;
@@ -402,8 +371,8 @@ struct DfSmem {
     uint32_t U[UW];  // head[HT] | first[HT] while matching, the output bit image afterwards
     uint32_t mmap[SEG / 32];    // "a verified match of >= 3 starts here" (match rounds)
     uint32_t tokmap[SEG / 32];  // token-start bitmap (parse walk; chunks share boundary words)
-    uint32_t litfreq[288];
-    uint32_t distfreq[32];
+    alignas(16) uint32_t litfreq[288];  // 16-B aligned: the rank count reads 4 at a time
+    alignas(16) uint32_t distfreq[32];
     uint32_t prefreq[32];
     uint32_t litcode[288];  // (len << 16) | bit-reversed code
     uint32_t distcode[32];
@@ -414,7 +383,168 @@ struct DfSmem {
     uint32_t scan[4 * DF_NT / 64];
     uint64_t runmask[6];
     uint32_t sh[48];
+    // block_build_codes: ranks (lit/len at [0, 286), distance at [320, 350)), per-alphabet
+    // class sizes, class start ranks, next canonical code, per-wave length counts, F / used
+    uint32_t hb_rank[352];
+    uint32_t hb_xbuf[2][512];
+    uint32_t hb_cnt[2][16];
+    uint32_t hb_start[2][16];
+    uint32_t hb_next[2][16];
+    uint32_t hb_wcnt[6][16];
+    uint32_t hb_sum[4];
+    uint32_t hb_used[2];
 };
+
+// Block-parallel code lengths and canonical codes of the lit/len code (286 symbols, threads
+// 0..285) and the distance code (30 symbols, threads 320..349), built side by side.  The
+// lengths are those of the one-wave builder wave_build_lengths64 (and of the 512-key one it
+// replaces): symbols ranked by the key (f << 9 | 511 - s) descending, initial lengths
+// round(log2(F/f)) clamped to [1, maxbits], fit_classes on the class sizes, then lengths by
+// rank (lengths are non-decreasing in rank, so each class is a rank range).  The ranks come
+// from a bitonic sort over 512 threads (one key each) instead of a one-wave sort of 8 keys per
+// lane.  Canonical codes (RFC 1951 3.2.2; reference
+// FlatHuffmanTree::construct common.hpp:104-145) from the final class sizes and per-wave
+// ballots.  Also sums the token cost under the dynamic and the fixed code (sh[32], sh[33]) and
+// finds HLIT / HDIST (sh[34], sh[35]).  Stands in for generateCodeLengths
+// (common.hpp:322-404) and the cost compare of deflate.hpp:739-746.
+template <int SEG>
+__device__ void block_build_codes(DfSmem<SEG>& S, uint64_t* dbg, uint64_t seg) {
+    static_assert(DF_NT == 1024, "thread layout of block_build_codes");
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int a = t >= 320 ? 1 : 0;  // alphabet of the symbol thread: 0 lit/len, 1 distance
+    const uint32_t s = a ? t - 320 : t;
+    const bool sym = a ? (s < 30) : (s < 286);
+    const uint32_t* const freq = a ? S.distfreq : S.litfreq;
+    const uint32_t f = sym ? freq[s] : 0;
+    const int maxbits = a ? DF_DIST_MAXBITS : DF_LIT_MAXBITS;
+    const uint64_t ltmask = (1ull << lane) - 1ull;
+    if (t < 32) S.hb_cnt[t >> 4][t & 15] = 0;
+    if (t < 4) { S.hb_sum[t] = 0; S.sh[32 + t] = 0; }
+    if (t < 2) S.hb_used[t] = 0;
+    __syncthreads();
+    if (t < 384) {  // F, used count and highest used symbol, one atomic per wave
+        const uint32_t Fw = wave_sum(f);
+        const uint64_t nzm = __ballot(f != 0);
+        if (lane == 0 && nzm) {
+            atomicAdd(&S.hb_sum[2 * a], Fw);
+            atomicAdd(&S.hb_sum[2 * a + 1], (uint32_t)__popcll(nzm));
+            atomicMax(&S.hb_used[a], (uint32_t)((w - 5 * a) * 64 + 64 - __clzll(nzm)));
+        }
+    }
+    {   // ranks by a bitonic sort of the keys (f << 9 | 511 - s), descending: lit/len keys on
+        // threads 0..511 (exchanges at strides >= 64 through LDS, one barrier each), distance
+        // keys on wave 8 (strides < 64 only; later stages leave its sorted run as it is)
+        const bool lk = t < 512, dk = t >= 512 && t < 576;
+        const uint32_t i = lk ? (uint32_t)t : (uint32_t)lane;
+        const uint32_t ks = lk ? (uint32_t)t : (uint32_t)lane;
+        const uint32_t kf = lk ? (ks < 286 ? S.litfreq[ks] : 0u) : (dk && ks < 30 ? S.distfreq[ks] : 0u);
+        uint32_t key = kf ? (kf << 9) | (511 - ks) : 0u;
+        int par = 0;
+#pragma unroll
+        for (int size = 2; size <= 512; size <<= 1) {
+#pragma unroll
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                uint32_t o;
+                switch (stride) {
+                    case 1: o = xor_lane<1>(key); break;
+                    case 2: o = xor_lane<2>(key); break;
+                    case 4: o = xor_lane<4>(key); break;
+                    case 8: o = xor_lane<8>(key); break;
+                    case 16: o = xor_lane<16>(key); break;
+                    case 32: o = xor_lane<32>(key); break;
+                    default: {
+                        uint32_t* xb = S.hb_xbuf[par];
+                        par ^= 1;
+                        if (lk) xb[t] = key;
+                        __syncthreads();
+                        o = lk ? xb[t ^ stride] : key;
+                    }
+                }
+                const bool lower = (i & (uint32_t)stride) == 0, desc = (i & (uint32_t)size) == 0;
+                key = (lower == desc) ? max(key, o) : min(key, o);
+            }
+        }
+        if (key && (lk || dk)) S.hb_rank[(lk ? 0u : 320u) + 511 - (key & 511)] = i;
+    }
+    __syncthreads();
+    DMX_PHASE(dbg, seg, 12);
+    const uint32_t nz = S.hb_sum[2 * a + 1];
+    if (t < 384) {  // class sizes of the initial lengths: lane k adds the wave's count of class k
+        const uint32_t L0 = sym ? init_len(f, S.hb_sum[2 * a], maxbits) : 0;
+        uint32_t mine = 0;
+#pragma unroll
+        for (int L = 1; L <= 15; L++) {
+            const uint32_t c = __popcll(__ballot(L0 == (uint32_t)L));
+            mine = lane == L ? c : mine;
+        }
+        if (mine) atomicAdd(&S.hb_cnt[a][lane], mine);
+    }
+    __syncthreads();
+    if (t == 0 || t == 320) {  // Kraft repair / slack fill on the class sizes, class starts,
+                               // next codes (two waves, in parallel)
+        uint32_t cnt[17];
+        cnt[0] = cnt[16] = 0;
+#pragma unroll
+        for (int L = 1; L <= 15; L++) cnt[L] = nz > 1 ? S.hb_cnt[a][L] : (L == 1 ? 2u : 0u);
+        if (nz > 1) fit_classes(cnt, maxbits);
+        uint32_t st = 0, code = 0;
+#pragma unroll
+        for (int L = 1; L <= 15; L++) {
+            S.hb_start[a][L] = st;
+            st += cnt[L];
+            code = (code + cnt[L - 1]) << 1;
+            S.hb_next[a][L] = code;
+        }
+    }
+    __syncthreads();
+    DMX_PHASE(dbg, seg, 13);
+    uint32_t L = 0;
+    if (sym) {
+        if (nz > 1) {
+            if (f) {
+                const uint32_t q = S.hb_rank[t];
+#pragma unroll
+                for (int l = 1; l <= 15; l++) L += q >= S.hb_start[a][l] ? 1u : 0u;
+            }
+        } else {  // zero or one used symbol: two codes of length 1 (a complete code, as zlib)
+            const uint32_t u = S.hb_used[a];
+            L = (s == (u ? u - 1 : 0u) || s == (u <= 1 ? 1u : 0u)) ? 1u : 0u;
+        }
+        (a ? S.distlen : S.litlen)[s] = (uint8_t)L;
+    }
+    uint32_t within = 0;
+    if (t < 384) {  // rank of the symbol among the wave's symbols of the same length
+        uint32_t mine = 0;
+#pragma unroll
+        for (int k = 1; k <= 15; k++) {
+            const uint64_t b = __ballot(L == (uint32_t)k);
+            within = L == (uint32_t)k ? (uint32_t)__popcll(b & ltmask) : within;
+            mine = lane == k ? (uint32_t)__popcll(b) : mine;
+        }
+        if (lane < 16) S.hb_wcnt[w][lane] = mine;
+        // token cost under the dynamic / fixed code, HLIT / HDIST
+        const uint32_t ex = a ? dist_extra(s) : (s > 256 ? len_extra(s) : 0);
+        const uint32_t dyn = sym ? f * (L + ex) : 0;
+        const uint32_t fix = sym ? f * ((a ? 5u : fixed_lit_len(s)) + ex) : 0;
+        const uint32_t dw = wave_sum(dyn), fw = wave_sum(fix);
+        const uint64_t used = __ballot(L != 0);
+        if (lane == 0) {
+            if (dw) atomicAdd(&S.sh[32], dw);
+            if (fw) atomicAdd(&S.sh[33], fw);
+            if (used) atomicMax(&S.sh[34 + a], (uint32_t)((w - 5 * a) * 64 + 64 - __clzll(used)));
+        }
+    }
+    __syncthreads();
+    if (sym) {
+        uint32_t code = 0;
+        if (L) {
+            uint32_t c = S.hb_next[a][L] + within;
+            for (int v = 0; v < w && !a; v++) c += S.hb_wcnt[v][L];
+            code = (L << 16) | bitrev(c, L);
+        }
+        (a ? S.distcode : S.litcode)[s] = code;
+    }
+}
 
 // stored block: [BFINAL|00][LEN][NLEN][data] (+ empty stored block unless final)
 template <int SEG>
@@ -454,116 +584,65 @@ __device__ void emit_stored(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t*
     if (t == 0) *size_out = total;
 }
 
-// Work units of 8 positions: unit u = byte (u & 3) of token-bitmap word u >> 2.  Thread t owns
-// units t, t + DF_NT, t + 2 DF_NT, ... so a dense stretch of tokens (a literal run) is spread
-// over many threads instead of landing on a few word owners.
-template <int SEG>
-struct Units {
-    static constexpr int N = SEG / 8;
-    static constexpr int PER = N / DF_NT;  // units per thread (4 at 32 KiB, 2 at 16 KiB)
+// Token ranges: after the parse, thread t owns tokens [t K, (t + 1) K) of the segment in
+// position order (K = ceil(tokens / DF_NT)), found from per-word token counts of the token-start
+// bitmap.  Every thread then walks the same number of tokens (a wave iterates K times, not the
+// maximum over its lanes of a position range's token count), and its bits form one contiguous
+// range of the block's bitstream.
+struct TokRange {
+    uint32_t w, m, n;  // bitmap word of the first token, its bits from that token on, tokens
 };
-// the thread's units as one 32-bit mask: byte k = unit k * DF_NT + t (UPT <= 4), so a single
-// token loop walks all of them (the wave iterates max-over-lanes of the thread's total tokens,
-// not the sum over units of per-unit maxima)
-template <int SEG>
-__device__ __forceinline__ uint32_t thread_units(const DfSmem<SEG>& S, uint32_t t) {
-    uint32_t m = 0;
-#pragma unroll
-    for (int k = 0; k < Units<SEG>::PER; k++) {
-        const uint32_t u = k * DF_NT + t;
-        m |= ((S.tokmap[u >> 2] >> ((u & 3) * 8)) & 0xFFu) << (8 * k);
-    }
-    return m;
-}
-// position of mask bit b of thread t
-__device__ __forceinline__ uint32_t unit_pos(uint32_t t, uint32_t b) {
-    return ((b >> 3) * DF_NT + t) * 8 + (b & 7);
+__device__ __forceinline__ uint32_t next_tok(const uint32_t* tokmap, uint32_t& w, uint32_t& m) {
+    while (!m) m = tokmap[++w];
+    const uint32_t p = w * 32 + __builtin_ctz(m);
+    m &= m - 1;
+    return p;
 }
 
-// bits of the token starting at p (literal if cand[p] == 0, else a match with distance
-// cand[p] and length cand[p + 1])
+// Encodes the token starting at p (a literal if cand[p] == 0, else a match with distance
+// cand[p] and length cand[p + 1]) under the block's codes and returns its bit count.  The bit
+// pattern replaces the token's candidate entries, for the emission pass:
+//   literal  cand[p]     = 0x8000 | bits << 9 | code           (code <= 9 bits)
+//   match    cand[p]     = pattern bits 0..14                   (bit 15 clear: d < 32768)
+//            cand[p + 1] = pattern bits 15..30
+//            cand[p + 2] = pattern bits 31..32 | bits << 2      (bits <= 9+5+6+13 = 33)
+// cand[p + 2] lies inside the match (L >= 3): no other token reads it.
 template <int SEG>
-__device__ __forceinline__ uint32_t token_bits(const DfSmem<SEG>& S, uint32_t p) {
+__device__ __forceinline__ uint32_t encode_token(DfSmem<SEG>& S, uint32_t p) {
     const uint32_t d = S.cand[p];
     if (d) {
         const uint32_t L = S.cand[p + 1];
         const uint32_t ls = len_sym(L), ds = dist_sym(d);
-        return (S.litcode[ls] >> 16) + len_extra(ls) + (S.distcode[ds] >> 16) + dist_extra(ds);
+        const uint32_t lc = S.litcode[ls], dc = S.distcode[ds];
+        uint64_t pat = lc & 0xFFFF;
+        uint32_t n = lc >> 16;
+        pat |= (uint64_t)(L - len_base(ls)) << n;
+        n += len_extra(ls);
+        pat |= (uint64_t)(dc & 0xFFFF) << n;
+        n += dc >> 16;
+        pat |= (uint64_t)(d - dist_base(ds)) << n;
+        n += dist_extra(ds);
+        S.cand[p] = (uint16_t)(pat & 0x7FFF);
+        S.cand[p + 1] = (uint16_t)(pat >> 15);
+        S.cand[p + 2] = (uint16_t)(((pat >> 31) & 3) | (n << 2));
+        return n;
     }
-    return S.litcode[data_byte(S.data32, p)] >> 16;
-}
-
-// exclusive block scan of K values per thread, in the order (k, thread): value k of thread t
-// is element k * DF_NT + t.  scratch holds K * DF_NT / 64 words.
-template <int K>
-__device__ void block_excl_scan_k(const uint32_t (&v)[K], uint32_t (&off)[K], uint32_t* scratch,
-                                  uint32_t* total) {
-    constexpr int NW = DF_NT / 64;
-    const int t = threadIdx.x, w = t >> 6;
-    uint32_t inc[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        inc[k] = wave_incl_scan(v[k]);
-        if ((t & 63) == 63) scratch[k * NW + w] = inc[k];
-    }
-    __syncthreads();
-    uint32_t base = 0;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        uint32_t pre = 0, tot = 0;
-#pragma unroll
-        for (int i = 0; i < NW; i++) {
-            const uint32_t x = scratch[k * NW + i];
-            if (i < w) pre += x;
-            tot += x;
-        }
-        off[k] = base + pre + inc[k] - v[k];
-        base += tot;
-    }
-    __syncthreads();
-    *total = base;
+    const uint32_t lc = S.litcode[data_byte(S.data32, p)];
+    S.cand[p] = (uint16_t)(0x8000u | ((lc >> 16) << 9) | (lc & 0x1FF));
+    return lc >> 16;
 }
 
 // Huffman (dynamic or fixed) block for the tokenized segment; returns false when a stored
 // block would be smaller (the caller then emits it), true after writing the slot.
 template <int SEG>
-__device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t* slot,
-                             uint32_t* size_out, uint64_t* dbg, uint64_t seg) {
+__device__ bool emit_huffman(DfSmem<SEG>& S, const TokRange tr, uint32_t nb, bool is_final,
+                             uint8_t* slot, uint32_t* size_out, uint64_t* dbg, uint64_t seg) {
     const int t = threadIdx.x;
 
-    // ---- code lengths + canonical codes (wave 0: lit/len, wave 1: distance) -------------
-    if (t < 64) {
-        uint64_t wst[6] = {0, 0, 0, 0, 0, 0};
-        wave_build_lengths(S.litfreq, 286, DF_LIT_MAXBITS, S.litlen, dbg ? wst : nullptr);
-        if (dbg && t == 0) dbg[seg * kPhaseSlots + 11] = (wst[0] & 0xFFFF) | ((wst[1] & 0xFFFF) << 16) | ((wst[3] & 0xFFFF) << 32) | ((wst[4] & 0xFFFF) << 48);
-        DMX_PHASE(dbg, seg, 12);
-        wave_assign_codes(S.litlen, 286, S.litcode);
-        DMX_PHASE(dbg, seg, 13);
-    } else if (t < 128) {
-        wave_build_lengths64(S.distfreq, 30, DF_DIST_MAXBITS, S.distlen);
-        wave_assign_codes(S.distlen, 30, S.distcode);
-    }
-    if (t < 8) S.sh[32 + t] = 0;
+    // ---- code lengths, canonical codes, token cost, HLIT / HDIST (whole block) -----------
+    block_build_codes<SEG>(S, dbg, seg);
     __syncthreads();
     DMX_PHASE(dbg, seg, 4);
-
-    // ---- token cost under the dynamic and the fixed code; HLIT / HDIST ------------------
-    if (t < 286) {
-        const uint32_t s = t;
-        const uint32_t f = S.litfreq[s];
-        const uint32_t ex = s > 256 ? len_extra(s) : 0;
-        uint32_t dyn = f * (S.litlen[s] + ex), fix = f * (fixed_lit_len(s) + ex);
-        if (t < 30) {
-            const uint32_t g = S.distfreq[t];
-            dyn += g * (S.distlen[t] + dist_extra(t));
-            fix += g * (5 + dist_extra(t));
-            if (S.distlen[t]) atomicMax(&S.sh[35], (uint32_t)t + 1);
-        }
-        if (dyn) atomicAdd(&S.sh[32], dyn);
-        if (fix) atomicAdd(&S.sh[33], fix);
-        if (S.litlen[s]) atomicMax(&S.sh[34], s + 1);
-    }
-    __syncthreads();
     DMX_PHASE(dbg, seg, 5);
     const uint32_t dyn_tok = S.sh[32], fix_tok = S.sh[33];
     const uint32_t nlit = max(257u, S.sh[34]), ndist = max(1u, S.sh[35]);
@@ -636,21 +715,14 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t
         __syncthreads();
     }
 
-    // ---- token bits per unit, block scan -------------------------------------------------
-    constexpr int UPT = Units<SEG>::PER;
-    const uint32_t umask = thread_units(S, t);
-    uint32_t ubits[UPT], uoff[UPT];
-#pragma unroll
-    for (int k = 0; k < UPT; k++) ubits[k] = 0;
-    for (uint32_t m = umask; m;) {
-        const uint32_t b = __builtin_ctz(m);
-        m &= m - 1;
-        const uint32_t c = token_bits(S, unit_pos(t, b));
-#pragma unroll
-        for (int k = 0; k < UPT; k++) ubits[k] += (b >> 3) == (uint32_t)k ? c : 0u;
+    // ---- bits of the thread's token range, block scan -------------------------------------
+    uint32_t mybits = 0;
+    {
+        uint32_t w = tr.w, m = tr.m;
+        for (uint32_t i = 0; i < tr.n; i++) mybits += encode_token(S, next_tok(S.tokmap, w, m));
     }
     uint32_t tok_total;
-    block_excl_scan_k<UPT>(ubits, uoff, S.scan, &tok_total);
+    const uint32_t myoff = block_excl_scan(mybits, S.scan, &tok_total);
     const uint32_t hdr_end = 3 + (use_dyn ? hdr_bits : 0);
     DMX_PHASE(dbg, seg, 8);
 
@@ -696,40 +768,17 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t
         }
         bw.flush();
     }
-    {
-        BitOr bw;
-        uint32_t cur = 0xFFFFFFFFu;
-        for (uint32_t m = umask; m;) {
-            const uint32_t b = __builtin_ctz(m);
-            m &= m - 1;
-            const uint32_t k = b >> 3;
-            if (k != cur) {  // next unit: its own bit offset
-                if (cur != 0xFFFFFFFFu) bw.flush();
-                uint32_t o = uoff[0];
-#pragma unroll
-                for (int q = 1; q < UPT; q++) o = k == (uint32_t)q ? uoff[q] : o;
-                bw.init(S.U, hdr_end + o);
-                cur = k;
-            }
-            const uint32_t p = unit_pos(t, b);
-            const uint32_t d = S.cand[p];
-            if (d) {
-                const uint32_t L = S.cand[p + 1];
-                const uint32_t ls = len_sym(L), ds = dist_sym(d);
-                const uint32_t lc = S.litcode[ls];
-                bw.put(lc & 0xFFFF, lc >> 16);
-                const uint32_t le = len_extra(ls);
-                if (le) bw.put(L - len_base(ls), le);
-                const uint32_t dc = S.distcode[ds];
-                bw.put(dc & 0xFFFF, dc >> 16);
-                const uint32_t de = dist_extra(ds);
-                if (de) bw.put(d - dist_base(ds), de);
-            } else {
-                const uint32_t lc = S.litcode[data_byte(S.data32, p)];
-                bw.put(lc & 0xFFFF, lc >> 16);
-            }
+    if (tr.n) {
+        BitSt bw;
+        bw.init(S.U, hdr_end + myoff);
+        uint32_t w = tr.w, m = tr.m;
+        for (uint32_t i = 0; i < tr.n; i++) {
+            const uint32_t p = next_tok(S.tokmap, w, m);
+            const uint32_t v0 = S.cand[p], v1 = S.cand[p + 1], v2 = S.cand[p + 2];
+            if (v0 & 0x8000) bw.put(v0 & 0x1FF, (v0 >> 9) & 15);
+            else bw.put64((uint64_t)v0 | ((uint64_t)v1 << 15) | ((uint64_t)(v2 & 3) << 31), v2 >> 2);
         }
-        if (cur != 0xFFFFFFFFu) bw.flush();
+        bw.flush();
     }
     // end of block, then (non-final) the byte-aligning empty stored block 000|pad|0000|FFFF
     const uint32_t eob_at = hdr_end + tok_total;
@@ -949,13 +998,34 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
         }
         __syncthreads();
         DMX_PHASE(A.dbg, seg, 3);
-        if (A.dbg && t == 0) A.dbg[seg * kPhaseSlots + 15] = S.sh[40] | ((uint64_t)S.sh[41] << 32);
 
-        // ---- histogram over token starts; the output image is zeroed meanwhile ------------
-        for (uint32_t w = thread_units(S, t); w;) {
-            {
-                const uint32_t p = unit_pos(t, __builtin_ctz(w));
-                w &= w - 1;
+        // ---- token ranges (TokRange): per-word token counts, block scan into the match
+        //      bitmap (dead after the parse), binary search for the thread's first token ------
+        TokRange tr;
+        {
+            const uint32_t c = t < NMAP ? (uint32_t)__popc(S.tokmap[t]) : 0u;
+            uint32_t tot;
+            const uint32_t ex = block_excl_scan(c, S.scan, &tot);
+            if (t < NMAP) S.mmap[t] = ex;
+            __syncthreads();
+            const uint32_t K = (tot + DF_NT - 1) / DF_NT;
+            const uint32_t first = min((uint32_t)t * K, tot);
+            tr.n = min(first + K, tot) - first;
+            uint32_t lo = 0, hi = NMAP;  // largest word lo with pre[lo] <= first
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (S.mmap[mid] <= first) lo = mid;
+                else hi = mid;
+            }
+            tr.w = lo;
+            tr.m = S.tokmap[lo];
+            for (uint32_t r = tr.n ? first - S.mmap[lo] : 0u; r; r--) tr.m &= tr.m - 1;
+        }
+        // ---- histogram over the thread's tokens; the output image is zeroed meanwhile ------
+        {
+            uint32_t w = tr.w, m = tr.m;
+            for (uint32_t i = 0; i < tr.n; i++) {
+                const uint32_t p = next_tok(S.tokmap, w, m);
                 const uint32_t d = S.cand[p];
                 if (d) {
                     atomicAdd(&S.litfreq[len_sym(S.cand[p + 1])], 1u);
@@ -968,7 +1038,8 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
         for (int i = t; i < DfSmem<SEG>::UW; i += DF_NT) S.U[i] = 0;
         if (t == 0) atomicAdd(&S.litfreq[256], 1u);  // end-of-block
         __syncthreads();
-        if (emit_huffman<SEG>(S, nb, is_final, slot, &A.sizes[seg], A.dbg, seg)) {
+        DMX_PHASE(A.dbg, seg, 11);
+        if (emit_huffman<SEG>(S, tr, nb, is_final, slot, &A.sizes[seg], A.dbg, seg)) {
             DMX_PHASE(A.dbg, seg, 10);
             return;
         }

@@ -121,14 +121,16 @@ void phase_dump(dmx_ctx* c, const char* kernel, uint64_t nidx, hipStream_t st) {
     if (!f) return;
     std::fprintf(f, "%s %llu", kernel, (unsigned long long)nidx);
     for (int k = 1; k < kPhaseSlots; k++) std::fprintf(f, " p%d=%.0f", k, cnt[k] ? sum[k] / cnt[k] : 0.0);
-    if (!inf) {  // packed wave_build_lengths sub-steps (developer aid)
-        double w[6] = {0};
-        for (uint64_t i = 0; i < nidx; i++) {
-            const uint64_t a = h[i * kPhaseSlots + 11], b = h[i * kPhaseSlots + 15];
-            w[0] += a & 0xFFFF; w[1] += (a >> 16) & 0xFFFF; w[3] += (a >> 32) & 0xFFFF; w[4] += (a >> 48) & 0xFFFF;
-            w[2] += b & 0xFFFFFFFF; w[5] += b >> 32;  // slot 15: slowest parse lane cycles / full_len calls
+    if (!inf) {  // timeline: mean cycles from slot 0 to every recorded slot (developer aid)
+        for (int k = 1; k < kPhaseSlots; k++) {
+            double a = 0;
+            uint64_t m = 0;
+            for (uint64_t i = 0; i < nidx; i++) {
+                const uint64_t* r = &h[i * kPhaseSlots];
+                if (r[k] && r[0] && r[k] >= r[0]) { a += (double)(r[k] - r[0]); m++; }
+            }
+            if (m) std::fprintf(f, " t%d=%.0f", k, a / m);
         }
-        for (int k = 0; k < 6; k++) std::fprintf(f, " wb%d=%.0f", k, nidx ? w[k] / nidx : 0.0);
     }
     if (inf)
         for (int k = 8; k < kPhaseSlots; k++) std::fprintf(f, " x%d=%.1f", k, xcnt[k] ? xsum[k] / xcnt[k] : 0.0);

@@ -10,7 +10,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libdmx.so")
+# DMX_LIB: developer override (A/B runs of two builds); the default is the in-tree build
+LIB_PATH = os.environ.get("DMX_LIB") or os.path.join(HERE, "lib", "libdmx.so")
 
 DMX_OK = 0
 DMX_ERR_ARG = -1
