@@ -315,6 +315,45 @@ __device__ __forceinline__ uint32_t matchlen(const uint32_t* w, uint32_t p, uint
     return min(L, maxl);
 }
 
+// matchlen by the four lanes of a quad (all four call it with the same p, q, maxl): lane
+// `sub` compares bytes [L + 16 sub, L + 16 sub + 16), so one LDS latency covers 64 bytes.
+// Reads up to 84 bytes past p + L: beyond maxl they only meet the segment's zero padding or
+// the next LDS array, and the result is clamped to maxl.  Same value as matchlen().
+__device__ __forceinline__ uint32_t matchlen4(const uint32_t* w, uint32_t p, uint32_t q,
+                                              uint32_t maxl, uint32_t sub) {
+    const int qb = lane_id() & ~3;
+    uint32_t L = 0;
+    while (L < maxl) {
+        const uint32_t o = L + 16 * sub;
+        const uint32_t ip = (p + o) >> 2, sp = (p + o) & 3, iq = (q + o) >> 2, sq = (q + o) & 3;
+        uint32_t a[5], b[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            a[k] = w[ip + k];
+            b[k] = w[iq + k];
+        }
+        uint32_t x = 0, off = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t d = __builtin_amdgcn_alignbyte(a[k + 1], a[k], sp) ^
+                               __builtin_amdgcn_alignbyte(b[k + 1], b[k], sq);
+            if (!x && d) {
+                x = d;
+                off = 4 * k;
+            }
+        }
+        const uint32_t mine = x ? off + ((uint32_t)__builtin_ctz(x) >> 3) : 16u;
+        const uint32_t qbits = (uint32_t)(__ballot(x != 0) >> qb) & 0xFu;
+        if (qbits) {
+            const uint32_t f = (uint32_t)__builtin_ctz(qbits);
+            L += 16 * f + (uint32_t)__shfl((int)mine, qb + (int)f, 64);
+            break;
+        }
+        L += 64;
+    }
+    return min(L, maxl);
+}
+
 __device__ __forceinline__ uint8_t data_byte(const uint32_t* w, uint32_t p) {
     return (uint8_t)(w[p >> 2] >> ((p & 3) * 8));
 }
@@ -366,7 +405,7 @@ struct DfSmem {
     static constexpr int UW0 = 2 * HT;
     static constexpr int UW1 = SEG / 4 + 64;
     static constexpr int UW = UW0 > UW1 ? UW0 : UW1;
-    uint32_t data32[SEG / 4 + 16];
+    uint32_t data32[SEG / 4 + 32];  // + 128 B: matchlen4 reads up to 84 B past a match end
     uint16_t cand[SEG + 8];
     uint32_t U[UW];  // head[HT] | first[HT] while matching, the output bit image afterwards
     uint32_t mmap[SEG / 32];    // "a verified match of >= 3 starts here" (match rounds)
@@ -912,22 +951,20 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
         }
         DMX_PHASE(A.dbg, seg, 2);
 
-        // ---- parse walk: one DF_CHUNK-byte chunk per lane; jumps over literal runs with the
+        // ---- parse walk: one DF_CHUNK-byte chunk per quad of lanes (the four walk in step and
+        //      share the match-length compares, matchlen4); jumps over literal runs with the
         //      match bitmap, ORs token starts into tokmap (neighbouring chunks share words) -----
-        if (A.dbg && t < 2) S.sh[40 + t] = 0;
-        __syncthreads();
-        if (level >= 2 && t < NWALK) {
-            const uint64_t wt0 = A.dbg ? __builtin_amdgcn_s_memtime() : 0;
-            uint32_t nml = 0;
-            const uint32_t lo = t * DF_CHUNK;
+        if (level >= 2 && t < 4 * NWALK) {
+            const uint32_t sub = t & 3;
+            const bool lead = sub == 0;
+            const uint32_t lo = (t >> 2) * DF_CHUNK;
             const uint32_t hi = min(lo + DF_CHUNK, nb);
             auto bits_range = [](uint32_t a, uint32_t b, uint32_t w) -> uint32_t {  // [a, b) in word w
                 const uint32_t e = b - w * 32;
                 return (e >= 32 ? 0xFFFFFFFFu : ((1u << e) - 1u)) & (0xFFFFFFFFu << (a & 31));
             };
             auto full_len = [&](uint32_t q) -> uint32_t {  // >= 3: verified in the rounds
-                nml++;
-                return matchlen(S.data32, q, q - S.cand[q], min(258u, hi - q));
+                return matchlen4(S.data32, q, q - S.cand[q], min(258u, hi - q), sub);
             };
             uint32_t p = lo, w = lo >> 5, mw = S.mmap[w], tok = 0;
             auto mbit = [&](uint32_t q) -> bool {
@@ -936,7 +973,7 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
             while (p < hi) {
                 const uint32_t wi = p >> 5;
                 if (wi != w) {
-                    if (tok) atomicOr(&S.tokmap[w], tok);
+                    if (tok && lead) atomicOr(&S.tokmap[w], tok);
                     w = wi;
                     mw = S.mmap[w];
                     tok = 0;
@@ -955,7 +992,7 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                 if (level == 3 && L < 258 && p + 1 < hi && mbit(p + 1)) {
                     if (full_len(p + 1) > L) {  // lazy: literal here, the longer match next
                         tok |= 1u << (p & 31);
-                        S.cand[p] = 0;
+                        if (lead) S.cand[p] = 0;
                         p++;
                         continue;
                     }
@@ -969,25 +1006,21 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                     const uint32_t ml = min(258u, hi - p);
                     uint32_t best = c;
                     for (uint32_t dd = 1; dd <= 4 && dd < best; dd++)
-                        if (dd <= p && matchlen(S.data32, p, p - dd, ml) >= L) best = dd;
+                        if (dd <= p && matchlen4(S.data32, p, p - dd, ml, sub) >= L) best = dd;
                     if (best == c) {  // one probe at c / k, k the largest divisor <= 8 (a probe
                                       // per k would serialize across lanes that differ in k)
                         uint32_t k = 1;
 #pragma unroll
                         for (uint32_t q = 2; q <= 8; q++) k = (c % q == 0) ? q : k;
-                        if (k > 1 && matchlen(S.data32, p, p - c / k, ml) >= L) best = c / k;
+                        if (k > 1 && matchlen4(S.data32, p, p - c / k, ml, sub) >= L) best = c / k;
                     }
-                    S.cand[p] = (uint16_t)best;
+                    if (lead) S.cand[p] = (uint16_t)best;
                 }
                 tok |= 1u << (p & 31);
-                S.cand[p + 1] = (uint16_t)L;
+                if (lead) S.cand[p + 1] = (uint16_t)L;
                 p += L;
             }
-            if (tok) atomicOr(&S.tokmap[w], tok);
-            if (A.dbg) {
-                atomicMax(&S.sh[40], (uint32_t)(__builtin_amdgcn_s_memtime() - wt0));
-                atomicMax(&S.sh[41], nml);
-            }
+            if (tok && lead) atomicOr(&S.tokmap[w], tok);
         }
         if (level < 2) {  // Huffman only: every position is a literal token
             for (uint32_t i = t; i < nb; i += DF_NT) S.cand[i] = 0;
