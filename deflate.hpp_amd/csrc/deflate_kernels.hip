@@ -891,14 +891,19 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
             bool pok[DF_PPT] = {};
             uint32_t ph[DF_PPT] = {}, pp[DF_PPT] = {};
             const uint32_t wave = t >> 6, lane = t & 63;
+            // Straight-line rounds: every LDS read is issued unconditionally (addresses stay in
+            // bounds: p < SEG, c <= p), so both positions' reads share one wait per step.
             for (uint32_t r0 = 0, rr = 0; r0 < nb; r0 += DF_PPT * DF_NT, rr++) {
                 uint32_t h[DF_PPT], p[DF_PPT], key[DF_PPT];
                 bool ok[DF_PPT];
 #pragma unroll
                 for (int k = 0; k < DF_PPT; k++) {
                     p[k] = r0 + k * DF_NT + t;
+                    key[k] = ld32u(S.data32, p[k]);
+                }
+#pragma unroll
+                for (int k = 0; k < DF_PPT; k++) {
                     ok[k] = p[k] + 4 <= nb;
-                    key[k] = ok[k] ? ld32u(S.data32, p[k]) : 0;
                     h[k] = ok[k] ? (key[k] * 0x1E35A7BDu) >> (32 - DF_HB) : 0;
                     // skip an update a neighbour position makes redundant (runs of equal keys
                     // would otherwise serialize on one LDS address): the first occurrence needs
@@ -912,30 +917,29 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                     if (pok[k] && phr != phx) atomicMax(&head[ph[k]], pp[k] + 1);                // previous round
                 }
                 __syncthreads();
+                uint32_t f[DF_PPT], hd[DF_PPT], c[DF_PPT], v[DF_PPT];
 #pragma unroll
                 for (int k = 0; k < DF_PPT; k++) {
-                    uint32_t c = 0;
-                    if (ok[k]) {
-                        const uint32_t f = first[h[k]];
-                        if ((f >> 16) == rr) {
-                            const uint32_t q = 0xFFFFu - (f & 0xFFFF);
-                            if (q < p[k]) c = p[k] - q;
-                        }
-                        if (!c) {
-                            const uint32_t q = head[h[k]];
-                            if (q) c = p[k] - (q - 1);
-                        }
-                        if (c > 32768) c = 0;
-                        // keep only matches of >= 3 bytes inside this 256-byte chunk (matches
-                        // never cross a chunk, so the parse lanes stay independent)
-                        if (c) {
-                            const uint32_t cend = min(p[k] / DF_CHUNK * DF_CHUNK + DF_CHUNK, nb);
-                            if (cend - p[k] < 3 || ((key[k] ^ ld32u(S.data32, p[k] - c)) & 0xFFFFFFu)) c = 0;
-                        }
-                    }
-                    if (p[k] < nb) S.cand[p[k]] = (uint16_t)c;
+                    f[k] = first[h[k]];
+                    hd[k] = head[h[k]];
+                }
+#pragma unroll
+                for (int k = 0; k < DF_PPT; k++) {
+                    const uint32_t q = 0xFFFFu - (f[k] & 0xFFFF);
+                    uint32_t ck = ((f[k] >> 16) == rr && q < p[k]) ? p[k] - q : 0u;
+                    if (!ck && hd[k]) ck = p[k] - (hd[k] - 1);
+                    c[k] = (ok[k] && ck <= 32768) ? ck : 0u;
+                    v[k] = ld32u(S.data32, p[k] - c[k]);
+                }
+#pragma unroll
+                for (int k = 0; k < DF_PPT; k++) {
+                    // keep only matches of >= 3 bytes inside this chunk (matches never cross a
+                    // chunk, so the parse lanes stay independent)
+                    const uint32_t cend = min(p[k] / DF_CHUNK * DF_CHUNK + DF_CHUNK, nb);
+                    if (c[k] && (cend - p[k] < 3 || ((key[k] ^ v[k]) & 0xFFFFFFu))) c[k] = 0;
+                    if (p[k] < nb) S.cand[p[k]] = (uint16_t)c[k];
                     // bit p of mmap = "a match of >= 3 starts at p"
-                    const uint64_t m = __ballot(c != 0);
+                    const uint64_t m = __ballot(c[k] != 0);
                     const uint32_t w0 = (r0 + k * DF_NT + wave * 64) >> 5;
                     if (lane == 0 && w0 < NMAP) {
                         S.mmap[w0] = (uint32_t)m;
