@@ -575,55 +575,62 @@ __global__ void k_lane_caps(const uint64_t* cands, uint64_t ncand, uint64_t n, u
     caps[j] = (uint32_t)((c + 3) & ~3ull);
 }
 
-// wave-cooperative periodic copy out[o + i] = out[o - d + (i mod d)], i < L.  Every source
-// byte precedes o, so all lanes copy independently.  The body is written as aligned dwords
-// (one per lane per 256-byte step): a dword whose 4 source bytes do not wrap the period is
-// one unaligned LDS read (two aligned words + alignbyte); the unaligned head / tail bytes and
-// the wrapping dwords go byte by byte.
-__device__ __forceinline__ uint32_t ln_mod_small(uint32_t x, uint32_t d) {  // x < d + 3
-    if (x >= d) x -= d;
-    if (x >= d) x -= d;
-    if (x >= d) x -= d;
-    return x;
-}
-__device__ __forceinline__ void ln_copy_wave(uint8_t* win, uint32_t o, uint32_t L, uint32_t d) {
+// Wave-cooperative copies inside the 32 KiB window.  ln_copy_plain moves n bytes from s to o
+// with s + n <= o (source wholly before the destination, so every lane copies independently):
+// unaligned head and tail bytes one per lane, the body as 16-byte aligned stores, each lane
+// building its quad from five source words with alignbyte (1 KiB per wave-step).
+constexpr uint32_t LN_WIN_WORDS = LN_OUT_CAP / 4;
+__device__ __forceinline__ void ln_copy_plain(uint8_t* win, uint32_t o, uint32_t s, uint32_t n) {
     const uint32_t lane = lane_id();
-    uint32_t* const W = reinterpret_cast<uint32_t*>(win);
-    const uint32_t src = o - d, end = o + L;
-    const uint32_t a0 = min((o + 3) & ~3u, end);  // first aligned body byte
-    const uint32_t a1 = max(a0, end & ~3u);       // first tail byte
-    const uint32_t nw = (a1 - a0) >> 2;
-    if (d >= L) {  // plain copy (i mod d == i): no division, no wrap
-        if (lane < a0 - o) win[o + lane] = win[src + lane];
-        if (lane < end - a1) win[a1 + lane] = win[src + (a1 - o) + lane];
-        for (uint32_t k = lane; k < nw; k += 64) W[(a0 >> 2) + k] = ld32u(W, src + (a0 - o) + 4 * k);
+    const uint32_t* const W = reinterpret_cast<const uint32_t*>(win);
+    const uint32_t end = o + n;
+    const uint32_t a0 = min((o + 15) & ~15u, end);  // first 16-byte aligned body byte
+    const uint32_t a1 = max(a0, end & ~15u);        // first tail byte
+    if (lane < a0 - o) win[o + lane] = win[s + lane];
+    else if (lane >= 16 && lane - 16 < end - a1) win[a1 + lane - 16] = win[s + (a1 - o) + lane - 16];
+    const uint32_t nq = (a1 - a0) >> 4;
+    const uint32_t sb = s + (a0 - o), sh = sb & 3;
+    for (uint32_t k = lane; k < nq; k += 64) {
+        const uint32_t i = (sb >> 2) + 4 * k;
+        // the fifth word is needed only when sh != 0, and then i + 4 < LN_WIN_WORDS (the source
+        // ends before the destination): the clamp only keeps the sh == 0 read in the window
+        const uint32_t w0 = W[i], w1 = W[i + 1], w2 = W[i + 2], w3 = W[i + 3];
+        const uint32_t w4 = W[min(i + 4, LN_WIN_WORDS - 1)];
+        *reinterpret_cast<uint4*>(win + a0 + 16 * k) =
+            make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                       __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+    }
+}
+
+// periodic copy out[o + i] = out[o - d + (i mod d)], i < L (the reference's byte-serial
+// overlapping copy, inflate.hpp:268-270): the first period (or, for d < 64, the largest
+// multiple of d that fits one byte per lane) is built directly; after that the P bytes already
+// at o are the pattern for the next P (P stays a multiple of d), so each further round is a
+// plain copy of the doubled prefix -- log2(L / d) rounds, no division, no wrapping reads.
+__device__ __forceinline__ void ln_copy_wave(uint8_t* win, uint32_t o, uint32_t L, uint32_t d) {
+    if (d >= L) {
+        ln_copy_plain(win, o, o - d, L);
         return;
     }
-    if (lane < a0 - o) win[o + lane] = win[src + ln_mod_small(lane, d)];
-    if (lane < end - a1) {
-        const uint32_t i = a1 - o + lane;
-        win[a1 + lane] = win[src + i % d];
+    uint32_t P;
+    if (d >= 64) {
+        ln_copy_plain(win, o, o - d, d);
+        P = d;
+    } else {
+        const uint32_t lane = lane_id();
+        P = d * (64 / d);  // 33..64 bytes, a multiple of d
+        if (lane < min(P, L)) win[o + lane] = win[o - d + lane % d];
     }
-    if (nw == 0) return;
-    uint32_t r = (a0 - o + 4 * lane) % d;  // (i mod d) of this lane's first dword
-    const uint32_t st = 256 % d;
-    for (uint32_t k = lane; k < nw; k += 64) {
-        uint32_t v;
-        if (r + 4 <= d) {
-            v = ld32u(W, src + r);
-        } else {
-            v = (uint32_t)win[src + r] | ((uint32_t)win[src + ln_mod_small(r + 1, d)] << 8) |
-                ((uint32_t)win[src + ln_mod_small(r + 2, d)] << 16) |
-                ((uint32_t)win[src + ln_mod_small(r + 3, d)] << 24);
-        }
-        W[(a0 >> 2) + k] = v;
-        r += st;
-        if (r >= d) r -= d;
+    while (P < L) {
+        wave_sync();
+        const uint32_t n = min(P, L - P);
+        ln_copy_plain(win, o + P, o, n);
+        P += n;
     }
 }
 
 __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs B) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[LN_OUT_CAP + 64];
+    __shared__ __attribute__((aligned(16))) uint8_t win[LN_OUT_CAP];  // exactly 32 KiB: five per CU
     const uint32_t lane = threadIdx.x;
     const uint64_t j = blockIdx.x;
     const SegRecord rec = A.recs[j];
@@ -637,24 +644,23 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
     const uint32_t* const tk = B.tok + B.tokoff[j];
     if (n == 0) return;
     const uint32_t w0 = tk[0];
-    if ((w0 >> 24) == 0) {  // stored segment: 16-byte loads into LDS, 16-byte stores out
+    if ((w0 >> 24) == 0) {  // stored segment: straight from the stream, 16-byte stores
         const uint8_t* src = reinterpret_cast<const uint8_t*>(A.in_words) + A.misalign + A.cands[j] + tk[1];
-        const uintptr_t s16 = reinterpret_cast<uintptr_t>(src) & ~(uintptr_t)15;
-        const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(src) - s16);
-        const uint32_t nblk = (sh + nb + 15) / 16;  // <= 2049 blocks: fits the window + pad
-        const uint4* g = reinterpret_cast<const uint4*>(s16);
-        uint4* w4 = reinterpret_cast<uint4*>(win);
-        for (uint32_t i = lane; i < nblk; i += 64) w4[i] = g[i];
-        wave_sync();
-        const uint32_t* W = reinterpret_cast<const uint32_t*>(win);
         if ((((uintptr_t)dst) & 15) == 0) {
+            // word-aligned source base; the words read stay inside the stream (its last word
+            // holds the last data byte) except the fifth at sh == 0, which is not used then
+            const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3);
+            const uint32_t* sw = reinterpret_cast<const uint32_t*>(src - sh);
             uint4* d4 = reinterpret_cast<uint4*>(dst);
-            for (uint32_t i = lane; i < nb / 16; i += 64)
-                d4[i] = make_uint4(ld32u(W, sh + 16 * i), ld32u(W, sh + 16 * i + 4),
-                                   ld32u(W, sh + 16 * i + 8), ld32u(W, sh + 16 * i + 12));
-            for (uint32_t i = (nb & ~15u) + lane; i < nb; i += 64) dst[i] = win[sh + i];
+            for (uint32_t i = lane; i < nb / 16; i += 64) {
+                const uint32_t w0 = sw[4 * i], w1 = sw[4 * i + 1], w2 = sw[4 * i + 2], w3 = sw[4 * i + 3];
+                const uint32_t w4 = sh ? sw[4 * i + 4] : 0u;
+                d4[i] = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                   __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+            }
+            for (uint32_t i = (nb & ~15u) + lane; i < nb; i += 64) dst[i] = src[i];
         } else {
-            for (uint32_t i = lane; i < nb; i += 64) dst[i] = win[sh + i];
+            for (uint32_t i = lane; i < nb; i += 64) dst[i] = src[i];
         }
         return;
     }
