@@ -37,7 +37,9 @@ constexpr int DF_NT = 1024;    // threads per workgroup (16 waves)
 constexpr int DF_CHUNK = 258;  // bytes per parse lane: one maximal match per chunk, and not a
                                // multiple of 256, so the lanes' chunk starts spread over the LDS
                                // banks (at 256 every lane of a wave hit one bank per matchlen read)
-constexpr int DF_HB = 12;      // hash bits of each of the two match tables
+constexpr int df_hash_bits(int seg) {  // hash bits of each of the two match tables: 11 at 16 KiB
+    return seg >= 32768 ? 12 : 11;     // keeps that variant at <= 80 KiB of LDS (two per CU)
+}
 // Code-length limits of the emitted lit/len and distance codes.  RFC 1951 allows 15; 9 and 6
 // keep every code inside the one-level lookup tables of the lane decoder
 // (inflate_lanes.hip: 512 + 64 entries per segment in LDS) at < 1% ratio cost.
@@ -401,7 +403,8 @@ __device__ __forceinline__ RunPlan plan_run(uint32_t v, uint32_t r) {
 template <int SEG>
 struct DfSmem {
     static constexpr int NWALK = (SEG + DF_CHUNK - 1) / DF_CHUNK;
-    static constexpr int HT = 1 << DF_HB;  // entries per hash table
+    static constexpr int HB = df_hash_bits(SEG);
+    static constexpr int HT = 1 << HB;  // entries per hash table
     static constexpr int UW0 = 2 * HT;
     static constexpr int UW1 = SEG / 4 + 64;
     static constexpr int UW = UW0 > UW1 ? UW0 : UW1;
@@ -904,7 +907,7 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
 #pragma unroll
                 for (int k = 0; k < DF_PPT; k++) {
                     ok[k] = p[k] + 4 <= nb;
-                    h[k] = ok[k] ? (key[k] * 0x1E35A7BDu) >> (32 - DF_HB) : 0;
+                    h[k] = ok[k] ? (key[k] * 0x1E35A7BDu) >> (32 - DfSmem<SEG>::HB) : 0;
                     // skip an update a neighbour position makes redundant (runs of equal keys
                     // would otherwise serialize on one LDS address): the first occurrence needs
                     // no write when position p - 1 has the same hash, the latest none when p + 1
