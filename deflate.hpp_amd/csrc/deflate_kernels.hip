@@ -410,7 +410,9 @@ struct DfSmem {
     static constexpr int UW = UW0 > UW1 ? UW0 : UW1;
     uint32_t data32[SEG / 4 + 32];  // + 128 B: matchlen4 reads up to 84 B past a match end
     uint16_t cand[SEG + 8];
-    uint32_t U[UW];  // head[HT] | first[HT] while matching, the output bit image afterwards
+    // while matching: HT pairs {head, first} (one ds_read_b64 per lookup); the output bit image
+    // afterwards
+    alignas(16) uint32_t U[UW];
     uint32_t mmap[SEG / 32];    // "a verified match of >= 3 starts here" (match rounds)
     uint32_t tokmap[SEG / 32];  // token-start bitmap (parse walk; chunks share boundary words)
     alignas(16) uint32_t litfreq[288];  // 16-B aligned: the rank count reads 4 at a time
@@ -861,8 +863,6 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
     const int level = A.level;
     uint8_t* const slot = A.slots + seg * (uint64_t)A.slot_bytes;
     uint8_t* const dbytes = reinterpret_cast<uint8_t*>(S.data32);
-    uint32_t* const head = S.U;
-    uint32_t* const first = S.U + HT;
     DMX_PHASE(A.dbg, seg, 0);
 
     // ---- load the segment into LDS (16 B per lane when aligned) ------------------------
@@ -891,23 +891,33 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
     if (level != 0) {
         // ---- match candidates: rounds of 2*DF_NT positions, two per thread ---------------
         if (level >= 2) {
+            // Table entries carry a fingerprint of the 4-byte key (product bits below the hash
+            // bits), so a lookup verifies its candidate without reading the candidate's bytes:
+            //   first = round(4) | 0x7FFF - p (15) | fp13      (atomicMax: earliest p in round)
+            //   head  = p + 1 (16) | fp16                       (atomicMax: latest p, 0 = none)
+            // stored as {head, first} pairs, one ds_read_b64 per lookup.  A fingerprint match
+            // that is not a key match is rare; the parse walk then finds a match length < 3
+            // and emits a literal.
+            static_assert(SEG / (DF_PPT * DF_NT) <= 16, "round number is 4 bits");
+            constexpr uint32_t HB = DfSmem<SEG>::HB;
             bool pok[DF_PPT] = {};
-            uint32_t ph[DF_PPT] = {}, pp[DF_PPT] = {};
+            uint32_t ph[DF_PPT] = {}, pp[DF_PPT] = {}, pt[DF_PPT] = {};
             const uint32_t wave = t >> 6, lane = t & 63;
+            const uint2* const tab = reinterpret_cast<const uint2*>(S.U);
             // Straight-line rounds: every LDS read is issued unconditionally (addresses stay in
-            // bounds: p < SEG, c <= p), so both positions' reads share one wait per step.
+            // bounds: p < SEG), so both positions' reads share one wait per step.
             for (uint32_t r0 = 0, rr = 0; r0 < nb; r0 += DF_PPT * DF_NT, rr++) {
-                uint32_t h[DF_PPT], p[DF_PPT], key[DF_PPT];
+                uint32_t h[DF_PPT], p[DF_PPT], prod[DF_PPT];
                 bool ok[DF_PPT];
 #pragma unroll
                 for (int k = 0; k < DF_PPT; k++) {
                     p[k] = r0 + k * DF_NT + t;
-                    key[k] = ld32u(S.data32, p[k]);
+                    prod[k] = ld32u(S.data32, p[k]) * 0x1E35A7BDu;
                 }
 #pragma unroll
                 for (int k = 0; k < DF_PPT; k++) {
                     ok[k] = p[k] + 4 <= nb;
-                    h[k] = ok[k] ? (key[k] * 0x1E35A7BDu) >> (32 - DfSmem<SEG>::HB) : 0;
+                    h[k] = ok[k] ? prod[k] >> (32 - HB) : 0;
                     // skip an update a neighbour position makes redundant (runs of equal keys
                     // would otherwise serialize on one LDS address): the first occurrence needs
                     // no write when position p - 1 has the same hash, the latest none when p + 1
@@ -916,33 +926,29 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                     const uint32_t hl = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)hx, 0x111, 0xF, 0xF, false);
                     const uint32_t phx = pok[k] ? ph[k] : 0xFFFFFFFFu;
                     const uint32_t phr = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)phx, 0x101, 0xF, 0xF, false);
-                    if (ok[k] && hl != hx) atomicMax(&first[h[k]], (rr << 16) | (0xFFFFu - p[k]));  // first in round
-                    if (pok[k] && phr != phx) atomicMax(&head[ph[k]], pp[k] + 1);                // previous round
+                    if (ok[k] && hl != hx)  // first in round
+                        atomicMax(&S.U[2 * h[k] + 1], (rr << 28) | ((0x7FFFu - p[k]) << 13) |
+                                                          ((prod[k] >> (32 - HB - 13)) & 0x1FFFu));
+                    if (pok[k] && phr != phx) atomicMax(&S.U[2 * ph[k]], ((pp[k] + 1) << 16) | pt[k]);  // previous round
                 }
                 __syncthreads();
-                uint32_t f[DF_PPT], hd[DF_PPT], c[DF_PPT], v[DF_PPT];
+                uint2 e[DF_PPT];
+#pragma unroll
+                for (int k = 0; k < DF_PPT; k++) e[k] = tab[h[k]];
 #pragma unroll
                 for (int k = 0; k < DF_PPT; k++) {
-                    f[k] = first[h[k]];
-                    hd[k] = head[h[k]];
-                }
-#pragma unroll
-                for (int k = 0; k < DF_PPT; k++) {
-                    const uint32_t q = 0xFFFFu - (f[k] & 0xFFFF);
-                    uint32_t ck = ((f[k] >> 16) == rr && q < p[k]) ? p[k] - q : 0u;
-                    if (!ck && hd[k]) ck = p[k] - (hd[k] - 1);
-                    c[k] = (ok[k] && ck <= 32768) ? ck : 0u;
-                    v[k] = ld32u(S.data32, p[k] - c[k]);
-                }
-#pragma unroll
-                for (int k = 0; k < DF_PPT; k++) {
-                    // keep only matches of >= 3 bytes inside this chunk (matches never cross a
-                    // chunk, so the parse lanes stay independent)
+                    const uint32_t f = e[k].y, hd = e[k].x;
+                    const uint32_t fp16 = (prod[k] >> (32 - HB - 16)) & 0xFFFFu;
+                    const uint32_t q = 0x7FFFu - ((f >> 13) & 0x7FFFu);
+                    uint32_t c = ((f >> 28) == rr && q < p[k] && (f & 0x1FFFu) == (fp16 >> 3)) ? p[k] - q : 0u;
+                    if (!c && hd && (hd & 0xFFFFu) == fp16) c = p[k] - ((hd >> 16) - 1);
+                    // keep only matches that can reach 3 bytes inside this chunk (matches never
+                    // cross a chunk, so the parse lanes stay independent)
                     const uint32_t cend = min(p[k] / DF_CHUNK * DF_CHUNK + DF_CHUNK, nb);
-                    if (c[k] && (cend - p[k] < 3 || ((key[k] ^ v[k]) & 0xFFFFFFu))) c[k] = 0;
-                    if (p[k] < nb) S.cand[p[k]] = (uint16_t)c[k];
-                    // bit p of mmap = "a match of >= 3 starts at p"
-                    const uint64_t m = __ballot(c[k] != 0);
+                    if (!ok[k] || cend - p[k] < 3) c = 0;
+                    if (p[k] < nb) S.cand[p[k]] = (uint16_t)c;
+                    // bit p of mmap = "a candidate (4-byte fingerprint match) starts at p"
+                    const uint64_t m = __ballot(c != 0);
                     const uint32_t w0 = (r0 + k * DF_NT + wave * 64) >> 5;
                     if (lane == 0 && w0 < NMAP) {
                         S.mmap[w0] = (uint32_t)m;
@@ -951,6 +957,7 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                     pok[k] = ok[k];
                     ph[k] = h[k];
                     pp[k] = p[k];
+                    pt[k] = fp16;
                 }
                 __syncthreads();
             }
@@ -970,7 +977,7 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                 const uint32_t e = b - w * 32;
                 return (e >= 32 ? 0xFFFFFFFFu : ((1u << e) - 1u)) & (0xFFFFFFFFu << (a & 31));
             };
-            auto full_len = [&](uint32_t q) -> uint32_t {  // >= 3: verified in the rounds
+            auto full_len = [&](uint32_t q) -> uint32_t {  // < 3 only on a fingerprint collision
                 return matchlen4(S.data32, q, q - S.cand[q], min(258u, hi - q), sub);
             };
             uint32_t p = lo, w = lo >> 5, mw = S.mmap[w], tok = 0;
@@ -996,6 +1003,12 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                 tok |= bits_range(p, q, w);  // literals before the match
                 p = q;
                 uint32_t L = full_len(p);
+                if (L < 3) {  // fingerprint collision, not a match: a literal
+                    tok |= 1u << (p & 31);
+                    if (lead) S.cand[p] = 0;
+                    p++;
+                    continue;
+                }
                 if (level == 3 && L < 258 && p + 1 < hi && mbit(p + 1)) {
                     if (full_len(p + 1) > L) {  // lazy: literal here, the longer match next
                         tok |= 1u << (p & 31);
