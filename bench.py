@@ -164,6 +164,18 @@ def main():
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok = bool(okt.item())
 
+    # practical HBM ceiling: a device-to-device copy of the shard, after the timed
+    # region, on torch's current stream where its events are recorded; bytes = N read + N written
+    copy_ms = 1e9
+    for _ in range(3):
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record()
+        d_out[:n].copy_(d_in)
+        c1.record()
+        c1.synchronize()
+        copy_ms = min(copy_ms, c0.elapsed_time(c1))
+    d2d_gbps = 2 * n / (copy_ms * 1e-3) / 1e9
+
     ms_step = elapsed / a.steps * 1e3
     t_def = sum(r[0][0].elapsed_time(r[0][1]) for r in recs) / len(recs)
     t_gat = sum(r[0][1].elapsed_time(r[0][2]) for r in recs) / len(recs)
@@ -219,7 +231,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                          "traffic": traffic, "kernel": dom,
-                         "alg_bytes_per_launch": alg},
+                         "alg_bytes_per_launch": alg,
+                         "d2d_copy_GBps": round(d2d_gbps, 1)},
             "cpu_baseline": None,
         }
         if world == 1 and not a.no_cpu_baseline:

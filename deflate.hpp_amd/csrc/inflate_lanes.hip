@@ -42,7 +42,10 @@ constexpr uint32_t LN_REGION = 1280;
 constexpr uint32_t LN_DIST = 1024;
 constexpr uint32_t LN_PRE = 1152;
 constexpr uint32_t LN_OUT_CAP = 32768;
-constexpr uint32_t LN_LANES = 16;  // segments per 64-thread workgroup: 16 x 1280 B = 20 KiB of LDS,
+#ifndef DMX_LN_LANES
+#define DMX_LN_LANES 16
+#endif
+constexpr uint32_t LN_LANES = DMX_LN_LANES;  // segments per 64-thread workgroup: 16 x 1280 B = 20 KiB of LDS,
                                    // eight workgroups per CU, two decoding waves on every SIMD
                                    // (the decode is issue-bound: lanes per wave cost nothing,
                                    // waves per SIMD double the issue rate)
@@ -59,7 +62,10 @@ __constant__ const uint8_t kLnPerm[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5,
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 GUint4;  // global, not flat: a flat
                                                                // load also counts in lgkmcnt
-constexpr uint32_t LN_RING_LOW = 16;  // top up when fewer words than this are buffered
+#ifndef DMX_LN_RING_LOW
+#define DMX_LN_RING_LOW 16
+#endif
+constexpr uint32_t LN_RING_LOW = DMX_LN_RING_LOW;  // top up when fewer words than this are buffered
 
 struct LaneIn {
     GUint4* blk;
