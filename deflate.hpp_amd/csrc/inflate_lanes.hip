@@ -474,6 +474,9 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
                         if (j != 0) {
                             flags |= SEGF_XREF;
                             going = false;
+                        } else if (br.bitpos() > 8 * br.E) {  // the one branch that does not
+                            flags |= SEGF_EXOTIC;             // advance outpos: bound it here
+                            going = false;
                         }  // stream start: the reference copies nothing
                     } else if (outpos + L > LN_OUT_CAP) {
                         flags |= SEGF_EXOTIC;
@@ -513,10 +516,8 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
                         going = false;
                     }
                 }
-                if (br.bitpos() > 8 * br.E) {
-                    flags |= SEGF_EXOTIC;  // over-read: the exact decoder decides
-                    going = false;
-                }
+                // over-read is checked after the loop (and in the branch above): every other
+                // iteration advances outpos or ends the loop, so LN_OUT_CAP bounds it
             }
         }
         if (dbg) dbg[3] = __builtin_amdgcn_s_memtime();
