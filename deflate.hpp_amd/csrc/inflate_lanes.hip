@@ -68,16 +68,16 @@ typedef __attribute__((address_space(1))) const u32x4 GUint4;  // global, not fl
 constexpr uint32_t LN_RING_LOW = DMX_LN_RING_LOW;  // top up when fewer words than this are buffered
 
 struct LaneIn {
-    GUint4* blk;
-    uint64_t nblk, E;
+    GUint4* blk;     // the candidate's first 16-byte quad: all positions below are 32-bit,
+    uint32_t nblk, E;  // relative to it (E clamped to 2^26 bytes, far beyond any accepted segment)
     u32x4 Q0, Q1, Q2, Q3, Q4, Q5, Q6, Q7;
-    uint64_t fq;  // quads [.., fq) are in the ring
-    uint64_t wi;  // absolute index of the next word to shift into bb
+    uint32_t fq;  // quads [.., fq) are in the ring
+    uint32_t wi;  // index of the next word to shift into bb
     uint32_t nb;  // valid bits in bb
     uint64_t bb;
     // clamped to the last block (refill() zeroes bytes past E), so the load is unconditional
     // within the lanes that issue it
-    __device__ __forceinline__ u32x4 fetch(uint64_t b) const { return blk[min(b, nblk - 1)]; }
+    __device__ __forceinline__ u32x4 fetch(uint32_t b) const { return blk[min(b, nblk - 1)]; }
     __device__ __forceinline__ bool low() const { return fq * 4 < wi + LN_RING_LOW; }
     // load quads [fq, wi/4 + 8): slot k gets the quad q == k (mod 8) in that range, or --
     // when there is none -- its current quad again (same bytes), so all eight loads are
@@ -85,11 +85,11 @@ struct LaneIn {
     // load: computed inside the loads' registers, each would first wait for the previous
     // top-up's load there (vmcnt(0), which also drains the loads just issued).
     __device__ __forceinline__ void topup() {
-        const uint64_t lim = (wi >> 2) + 8, last = nblk - 1;
+        const uint32_t lim = (wi >> 2) + 8, last = nblk - 1;
         uint64_t a[8];
 #pragma unroll
         for (uint32_t k = 0; k < 8; k++) {
-            uint64_t q = fq + ((uint64_t)(k - (uint32_t)fq) & 7u);
+            uint32_t q = fq + ((k - fq) & 7u);
             if (q >= lim) q -= 8;
             a[k] = reinterpret_cast<uint64_t>(blk + min(q, last));
         }
@@ -106,7 +106,7 @@ struct LaneIn {
         fq = lim;
     }
     __device__ __forceinline__ uint32_t word() const {
-        const uint32_t qs = (uint32_t)(wi >> 2) & 7, ws = (uint32_t)wi & 3;
+        const uint32_t qs = (wi >> 2) & 7, ws = wi & 3;
         const bool b0 = qs & 1, b1 = qs & 2, b2 = qs & 4;
         const u32x4 p01 = b0 ? Q1 : Q0, p23 = b0 ? Q3 : Q2, p45 = b0 ? Q5 : Q4, p67 = b0 ? Q7 : Q6;
         const u32x4 p03 = b1 ? p23 : p01, p47 = b1 ? p67 : p45;
@@ -115,13 +115,13 @@ struct LaneIn {
     }
     __device__ __forceinline__ void refill() {  // requires nb <= 32 and a word in the ring
         uint32_t w = word();
-        const uint64_t wb = wi * 4;
-        if (wb + 4 > E) w = wb >= E ? 0u : (w & ((1u << (8 * (uint32_t)(E - wb))) - 1u));
+        const uint32_t wb = wi * 4;
+        if (wb + 4 > E) w = wb >= E ? 0u : (w & ((1u << (8 * (E - wb))) - 1u));
         bb |= (uint64_t)w << nb;
         nb += 32;
         wi++;
     }
-    __device__ void seek(uint64_t abyte) {
+    __device__ void seek(uint32_t abyte) {
         wi = abyte >> 2;
         fq = wi >> 2;
         topup();
@@ -129,7 +129,7 @@ struct LaneIn {
         nb = 0;
         refill();
         refill();
-        const uint32_t sk = (uint32_t)(abyte & 3) * 8;
+        const uint32_t sk = (abyte & 3) * 8;
         bb >>= sk;
         nb -= sk;
     }
@@ -146,7 +146,7 @@ struct LaneIn {
         bb >>= n;
         nb -= n;
     }
-    __device__ __forceinline__ uint64_t bitpos() const { return wi * 32 - nb; }
+    __device__ __forceinline__ uint32_t bitpos() const { return wi * 32 - nb; }
     __device__ __forceinline__ void align() { consume((uint32_t)(-bitpos()) & 7u); }  // next byte
 };
 
@@ -183,14 +183,16 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
     const uintptr_t base16 = base4 & ~(uintptr_t)15;
     const uint64_t off0 = (uint64_t)(base4 - base16) + A.misalign;  // stream byte 0
     LaneIn br;
-    br.blk = (GUint4*)base16;
-    br.E = off0 + A.n;
-    br.nblk = (br.E + 15) / 16;
     const uint64_t start = A.cands[j];
+    uint64_t cb = (off0 + start) & ~(uint64_t)15;  // stream byte of relative position 0
+    if (cb >= 16 && cb >= off0 + A.n) cb -= 16;  // a candidate at the stream end: keep a quad in bounds
+    br.blk = (GUint4*)(base16 + cb);
+    br.E = (uint32_t)min(off0 + A.n - cb, (uint64_t)1 << 26);
+    br.nblk = (br.E + 15) / 16;
     uint64_t* const dbg = A.dbg ? A.dbg + j * kPhaseSlots : nullptr;  // DMX_PHASES developer aid
     uint32_t n_iter = 0, n_top = 0;
     if (dbg) dbg[0] = __builtin_amdgcn_s_memtime();
-    br.seek(off0 + start);
+    br.seek((uint32_t)(off0 + start - cb));
 
     uint32_t flags = 0, outpos = 0;
     bool fin = false;
@@ -229,19 +231,19 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
         br.align();
         br.ensure(32);
         const uint32_t len = br.bits(16), nlen = br.bits(16);
-        const uint64_t b0 = br.bitpos() >> 3;  // absolute byte of the data
+        const uint32_t b0 = br.bitpos() >> 3;  // byte of the data (relative)
         if (!bfinal && len == 0 && nlen == 0xFFFF) {
-            end_byte = b0 - off0;  // empty segment: the candidate is itself a marker
+            end_byte = b0 + cb - off0;  // empty segment: the candidate is itself a marker
         } else if (b0 + len > br.E || len > LN_OUT_CAP) {
             flags |= SEGF_EXOTIC;
         } else {
             push(len);
-            push((uint32_t)(b0 - off0 - start));
+            push((uint32_t)(b0 + cb - off0 - start));
             outpos = len;
             br.seek(b0 + len);
             if (bfinal) {
                 fin = true;
-                end_byte = b0 + len - off0;
+                end_byte = b0 + len + cb - off0;
             } else {
                 br.ensure(3);
                 const uint32_t f2 = br.bits(1), t2 = br.bits(2);
@@ -249,7 +251,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
                 br.ensure(32);
                 const uint32_t l2 = br.bits(16), n2 = br.bits(16);
                 if (f2 || t2 != 0 || l2 != 0 || n2 != 0xFFFF) flags |= SEGF_EXOTIC;
-                end_byte = (br.bitpos() >> 3) - off0;
+                end_byte = (br.bitpos() >> 3) + cb - off0;
             }
         }
     } else if (btype == 3) {
@@ -525,7 +527,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
         if (!flags) {
             if (bfinal) {
                 fin = true;
-                end_byte = ((br.bitpos() + 7) >> 3) - off0;
+                end_byte = ((br.bitpos() + 7) >> 3) + cb - off0;
             } else {
                 br.ensure(3);
                 const uint32_t f2 = br.bits(1), t2 = br.bits(2);
@@ -533,7 +535,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
                 br.ensure(32);
                 const uint32_t l2 = br.bits(16), n2 = br.bits(16);
                 if (f2 || t2 != 0 || l2 != 0 || n2 != 0xFFFF) flags |= SEGF_EXOTIC;
-                end_byte = (br.bitpos() >> 3) - off0;
+                end_byte = (br.bitpos() >> 3) + cb - off0;
             }
         }
     }
