@@ -235,10 +235,23 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
                                c->cands.as<uint64_t>(), nullptr, st));
 
     uint8_t* out = fixed_out;
+    // The segment-parallel passes place candidate j at j * 32 KiB.  Every 00 00 FF FF inside
+    // stored data is a candidate too, so a marker-dense stream can ask for more HBM than exists:
+    // then the parallel plan is skipped and the serial decoder (sized by its count pass) runs.
+    bool parallel_ok = true;
     if (!out) {
-        if (!c->out.ensure(ncand * (size_t)kSegCap)) return DMX_ERR_NOMEM;
-        out = c->out.as<uint8_t>();
-        cap = c->out.cap;
+        size_t freeb = 0, totb = 0;
+        if (hipMemGetInfo(&freeb, &totb) != hipSuccess) freeb = 0;
+        const size_t want = ncand * (size_t)kSegCap;
+        if ((want <= c->out.cap || want <= freeb / 2) && c->out.ensure(want)) {
+            out = c->out.as<uint8_t>();
+            cap = c->out.cap;
+        } else {
+            parallel_ok = false;
+            if (!c->out.ensure(1)) return DMX_ERR_NOMEM;
+            out = c->out.as<uint8_t>();
+            cap = 0;
+        }
     }
     InflateArgs A;
     A.in_words = words;
@@ -267,6 +280,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     const bool few_bits = n / ncand < 4096;
     uint32_t plan[8][2];
     int np = 0;
+    r.status = 2;
     if (path_env == -1 || path_env == 4) {
         const uint64_t words = std::min<uint64_t>(ncand * 32788ull, 8ull * n + 20ull * ncand);
         if (c->ltok.ensure(words * 4) && c->ltokoff.ensure((ncand + 1) * 8) &&
@@ -288,6 +302,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     }
     if (path_env != 1 && path_env != 4) plan[np][0] = 1, plan[np][1] = 0, np++;
     uint32_t lead_mode = 0;
+    if (!parallel_ok) np = 0;
     for (int pi = 0; pi < np; pi++) {
         const uint32_t mode = plan[pi][0];
         if (mode == 3 && (r.exotic == 0 || r.exotic > ncand / 8)) continue;  // nothing / too many
@@ -362,6 +377,22 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     return r.status;
 }
 
+// Restores the calling thread's current HIP device on scope exit: an entry point switches to
+// its context's device, and a caller driving several GPUs from one thread must not see its
+// current device move.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = prev == dev || hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
 bool is_gfx950(int dev) {
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, dev) != hipSuccess) return false;
@@ -390,7 +421,8 @@ int dmx_create(dmx_ctx** out, const dmx_config* cfg) {
     int dev = cfg->device;
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return DMX_ERR_DEVICE;
     if (dev >= ndev || !is_gfx950(dev)) return DMX_ERR_DEVICE;
-    if (hipSetDevice(dev) != hipSuccess) return DMX_ERR_DEVICE;
+    DeviceGuard dg(dev);
+    if (!dg.ok) return DMX_ERR_DEVICE;
     dmx_ctx* c = new (std::nothrow) dmx_ctx();
     if (!c) return DMX_ERR_NOMEM;
     c->device = dev;
@@ -407,10 +439,11 @@ int dmx_create(dmx_ctx** out, const dmx_config* cfg) {
 
 void dmx_destroy(dmx_ctx* c) {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    DeviceGuard dg(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->in, &c->out, &c->slots, &c->sizes, &c->offs, &c->scal, &c->cands,
-                      &c->tiles, &c->tileoffs, &c->recs, &c->status, &c->dbg})
+                      &c->tiles, &c->tileoffs, &c->recs, &c->status, &c->dbg, &c->ltok,
+                      &c->ltokoff, &c->lntok, &c->lcaps})
         b->release();
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -433,7 +466,8 @@ int dmx_deflate_device(dmx_ctx* c, const void* d_in, size_t n, int level, uint32
                        void* d_out, size_t cap, size_t* out_len, void* stream) {
     if (!c || (!d_in && n) || !d_out || !out_len) return DMX_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    if (hipSetDevice(c->device) != hipSuccess) return DMX_ERR_DEVICE;
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     return deflate_device_locked(c, (const uint8_t*)d_in, n, level, flags, (uint8_t*)d_out, cap,
                                  out_len, st);
@@ -443,7 +477,8 @@ int dmx_inflate_device(dmx_ctx* c, const void* d_in, size_t n, void* d_out, size
                        size_t* out_len, void* stream) {
     if (!c || (!d_in && n) || !d_out || !out_len) return DMX_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    if (hipSetDevice(c->device) != hipSuccess) return DMX_ERR_DEVICE;
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     return inflate_device_locked(c, (const uint8_t*)d_in, n, (uint8_t*)d_out, cap, out_len,
                                  nullptr, st);
@@ -455,7 +490,8 @@ int dmx_deflate(dmx_ctx* c, const uint8_t* in, size_t n, int level, uint8_t* out
     if (!c) return DMX_ERR_DEVICE;
     if ((!in && n) || !out_len || (!out && cap)) return DMX_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    if (hipSetDevice(c->device) != hipSuccess) return DMX_ERR_DEVICE;
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
     const size_t bound = dmx_deflate_bound(n);
     if (!c->in.ensure(n + 16) || !c->out.ensure(bound)) return DMX_ERR_NOMEM;
     if (n) HIPCHK(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
@@ -482,7 +518,8 @@ int dmx_inflate(dmx_ctx* c, const uint8_t* in, size_t n, uint8_t* out, size_t ca
     if (!c) return DMX_ERR_DEVICE;
     if ((!in && n) || (!out && cap) || !written) return DMX_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    if (hipSetDevice(c->device) != hipSuccess) return DMX_ERR_DEVICE;
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
     uint8_t* dev = nullptr;
     size_t tot = 0;
     *written = 0;
@@ -502,7 +539,8 @@ int dmx_inflate_alloc(dmx_ctx* c, const uint8_t* in, size_t n, uint8_t** out, si
     if (!c) return DMX_ERR_DEVICE;
     if ((!in && n) || !out || !len) return DMX_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    if (hipSetDevice(c->device) != hipSuccess) return DMX_ERR_DEVICE;
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
     *out = nullptr;
     *len = 0;
     uint8_t* dev = nullptr;

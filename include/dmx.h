@@ -108,7 +108,10 @@ typedef struct dmx_stats {
     uint64_t out_bytes;
     uint32_t path;          /* inflate: 0 = segment-parallel (speculative offsets),
                                1 = segment-parallel (look-back offsets), 2 = serial path,
-                               3 = workgroup-per-segment decoder (32 KiB slots)             */
+                               3 = workgroup-per-segment decoder (32 KiB slots),
+                               4 = lane decoder + wave resolve (the default for libdmx
+                                   streams: one lane decodes a segment's tokens, one
+                                   wavefront rebuilds its bytes)                            */
     uint32_t reserved;
 } dmx_stats;
 

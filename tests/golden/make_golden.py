@@ -135,7 +135,41 @@ def main():
     outc = ref.decompress_cap(s, 1000)
     man["cap_case"] = {"stream": "streams/zlib_test.bmp_l1_default.deflate", "cap": 1000,
                        "written": len(outc), "sha256": sha(outc)}
-    # 7. corpus checksums for the generator
+    # 7. the reference's own MULTI-CHUNK streams (32 KiB chunks glued at bit offsets,
+    #    deflate.hpp:689-697, 791-793): fixed-Huffman fallback blocks (A-4), the trailing pad
+    #    byte (A-7), the extra empty final block when N % 32 KiB == 0 (D2), the lossy L2 tail
+    #    (A-1) and the misaligned stored fallback (A-3, the reference's inflate then fails).
+    #    Expected = what the reference inflate makes of them (SHA-256 + size, or its error).
+    multi = [("text", 1 << 20, 2), ("repeat", 1 << 20, 2), ("zeros", 1 << 20, 2), ("text", 256 << 10, 3),
+             ("mixed", 1 << 20, 2)]
+    for kind, n, lvl in multi:
+        d = dmx.corpus(kind, n)
+        s = ref.compress(d, lvl)
+        add(f"refmulti_L{lvl}_{kind}{n >> 10}k", s, f"reference deflate::compress level {lvl} of {n} B of "
+            f"corpus '{kind}' (offset 0)", original=d)
+    # 8. multi-block zlib streams of 1 MiB slices (cross-block back-references: the streams a
+    #    marker-based decoder cannot split) and a Z_FULL_FLUSH stream (00 00 FF FF every 64 KiB
+    #    with 15-bit codes)
+    for kind, lvl in (("text", 1), ("text", 6), ("bmp", 1), ("mixed", 1), ("repeat", 6), ("zeros", 1)):
+        d = dmx.corpus(kind, 1 << 20, offset=(1 << 20) * 5)
+        add(f"zmulti_{kind}1M_l{lvl}", raw(d, lvl, 0), f"zlib raw level {lvl} of 1 MiB '{kind}' at offset 5 MiB",
+            original=d)
+    d = dmx.corpus("text", 1 << 20, offset=(1 << 20) * 7)
+    z = zlib.compressobj(6, zlib.DEFLATED, -15, 9, 0)
+    fs = b"".join(z.compress(d[i:i + 65536]) + z.flush(zlib.Z_FULL_FLUSH) for i in range(0, len(d), 65536)) + z.flush()
+    add("zfullflush_text1M_l6", fs, "zlib raw level 6, Z_FULL_FLUSH every 64 KiB, 1 MiB 'text' at offset 7 MiB",
+        original=d)
+    # 9. config C3: the zlib level-1 raw stream of the full large.bmp stand-in.
+    #    Too large to commit (6.2 MB): tests regenerate it with zlib and check its SHA-256 first.
+    bmp = dmx.corpus("bmp", 25165962)
+    z = zlib.compressobj(1, zlib.DEFLATED, -15)  # zlib's default memLevel 8, as SURVEY 8(d) C3
+    c3 = z.compress(bmp) + z.flush()
+    c3out = ref.decompress(c3)
+    man["c3_bmp_zlib1"] = {"corpus": "bmp", "n": len(bmp), "zlib_level": 1, "stream_len": len(c3),
+                           "stream_sha256": sha(c3), "out_len": len(c3out), "out_sha256": sha(c3out),
+                           "equals_original": c3out == bmp, "how": "reference inflate::decompress of "
+                           "zlib.compressobj(1, DEFLATED, -15) of dmx.corpus('bmp', 25165962)"}
+    # 10. corpus checksums for the generator
     man["corpus_sha256_1MiB"] = {k: sha(dmx.corpus(k, 1 << 20)) for k in ("zeros", "repeat", "random", "text", "mixed")}
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(man, f, indent=1)

@@ -70,8 +70,41 @@ def test_inflate_foreign_stream_serial_path(ctx, oracle, kind):
     for lvl, st in ((1, 0), (6, 0), (9, zlib.Z_FIXED), (6, zlib.Z_RLE)):
         s = zraw(d, lvl, st)
         out = ctx.decompress(s)
-        assert out == d
+        assert out == d, (lvl, st)
+        assert oracle.inflate(s) == out, (lvl, st)
+
+
+def test_inflate_c3_large_bmp_zlib1(ctx):
+    """Config C3: the zlib level-1 raw stream of the full 25,165,962-B large.bmp
+    stand-in (6.2 MB, hundreds of dynamic blocks with cross-block references), bit-exact with
+    the reference inflate's output (SHA-256 recorded by make_golden.py from oracle/_ref)."""
+    c3 = MAN["c3_bmp_zlib1"]
+    d = dmx.corpus("bmp", c3["n"])
+    z = zlib.compressobj(c3["zlib_level"], zlib.DEFLATED, -15)
+    s = z.compress(d) + z.flush()
+    assert len(s) == c3["stream_len"] and sha(s) == c3["stream_sha256"], "zlib produced another stream"
+    out = ctx.decompress(s)
+    assert len(out) == c3["out_len"] and sha(out) == c3["out_sha256"]
+
+
+def test_inflate_zlib_full_flush_stream(ctx, oracle):
+    """A third-party stream with full-flush points (00 00 FF FF every 64 KiB, 15-bit codes):
+    bit-exact whichever decoder takes it."""
+    d = dmx.corpus("text", 1 << 20, offset=999)
+    z = zlib.compressobj(6, zlib.DEFLATED, -15, 9, 0)
+    s = b"".join(z.compress(d[i:i + 65536]) + z.flush(zlib.Z_FULL_FLUSH) for i in range(0, len(d), 65536)) + z.flush()
+    assert ctx.decompress(s) == d
     assert oracle.inflate(s) == d
+
+
+def test_inflate_marker_dense_stored_stream_host_api(ctx, oracle):
+    """every 00 00 FF FF inside stored data is a segment candidate.  A level-0
+    stream of marker-dense data must still decode through the host API (the parallel plan is
+    skipped when its candidate slots do not fit, the serial decoder runs)."""
+    blob = b"\x00\x00\xff\xff" * (3 << 18)  # 3 MiB, a candidate every 4 bytes
+    s = ctx.compress(blob, 0)
+    assert ctx.decompress(s) == blob
+    assert ctx.decompress(s, cap=1000) == blob[:1000]
 
 
 def test_inflate_empty_input_errors(ctx):
@@ -132,8 +165,8 @@ def test_deflate_roundtrip_oracle_zlib_gpu(oracle, seg, level):
 @pytest.mark.skipif(not Reference.available(), reason="oracle/_ref not shipped")
 def test_deflate_decodes_with_compiled_reference(ctx):
     ref = Reference()
-    for name, d in INPUTS[:8]:
-        for level in (1, 2, 3):
+    for name, d in INPUTS:
+        for level in (0, 1, 2, 3):
             s = ctx.compress(d, level)
             assert ref.decompress(s) == d, (name, level)
 

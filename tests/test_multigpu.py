@@ -74,4 +74,4 @@ def test_shard_ranges_cover_and_align():
             rs = [shard.shard_range(total, r, world, SEG) for r in range(world)]
             assert rs[0][0] == 0 and rs[-1][1] == total
             for (b0, e0), (b1, e1) in zip(rs, rs[1:]):
-                assert e0 == b1 and b1 % SEG == 0 or b1 == total
+                assert e0 == b1 and (b1 % SEG == 0 or b1 == total)
