@@ -60,6 +60,9 @@ struct dmx_ctx {
     std::mutex mu;
     DevBuf in, out, slots, sizes, offs, scal, cands, tiles, tileoffs, recs, status, dbg;
     DevBuf ltok, ltokoff, lntok, lcaps;  // lane decoder token lists (mode 4)
+    // block-parallel path (path 5): scan counts / hits / offsets, hit list, unit starts, token
+    // offsets and words, unit records, chain (unit index, offset, size), 16-bit image
+    DevBuf fbc, fbh, fbo, fbl, fbs, fbt, fbk, fbu, fbch, fbco, fbcs, fbimg;
     bool timing = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     dmx_stats stats{};
@@ -76,7 +79,7 @@ struct Scal {  // small device-side scalars, one allocation
     uint64_t total;
     uint64_t nmarkers;
     uint32_t ticket;
-    uint32_t pad;
+    uint32_t fb_err;  // block-parallel path: a copy reached before the stream start
     InflateResult res;
 };
 
@@ -207,6 +210,108 @@ int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, 
     return total > cap ? DMX_ERR_CAPACITY : DMX_OK;
 }
 
+// Block-parallel inflate of an arbitrary stream (inflate_blocks.hip): header scan, unit decode,
+// chain walk here on the host, replay / window hand-off / resolve.  *handled = false sends the
+// stream to the serial decoder (no chain from bit 0 to a BFINAL block, a unit that errors or
+// runs out of token space, a copy from before the stream start): results and error codes are
+// then the serial decoder's, i.e. the reference's.
+int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_out, size_t cap,
+                      size_t* total_out, uint8_t** dev_out, hipStream_t st, bool* handled) {
+    *handled = false;
+    Scal* ds = c->scal.as<Scal>();
+    if (c->timing) (void)hipEventRecord(c->ev[1], st);
+    const uint64_t misalign = (uintptr_t)d_in & 3;
+    const uint32_t* words = reinterpret_cast<const uint32_t*>(d_in - misalign);
+    const uint64_t nc = fb_scan_chunks(n);
+    if (!c->fbc.ensure(nc * 4) || !c->fbh.ensure(nc * fb_hits_per_chunk() * 8) || !c->fbo.ensure(nc * 8 + 8))
+        return DMX_OK;
+    HIPCHK(launch_fb_scan(words, misalign, n, c->fbc.as<uint32_t>(), c->fbh.as<uint64_t>(),
+                          c->fbo.as<uint64_t>(), &ds->nmarkers, st));
+    uint64_t nhits = 0;
+    HIPCHK(hipMemcpyAsync(&nhits, &ds->nmarkers, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<uint64_t> hits(nhits);
+    if (nhits) {
+        if (!c->fbl.ensure(nhits * 8)) return DMX_OK;
+        HIPCHK(launch_fb_compact(c->fbc.as<uint32_t>(), c->fbo.as<uint64_t>(), c->fbh.as<uint64_t>(), nc,
+                                 c->fbl.as<uint64_t>(), st));
+        HIPCHK(hipMemcpyAsync(hits.data(), c->fbl.p, nhits * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    // units: bit 0, then every hit (sorted: chunks in order, lanes in order within a chunk)
+    std::vector<uint64_t> starts{0};
+    for (uint64_t h : hits)
+        if (h > starts.back()) starts.push_back(h);
+    const uint64_t K = starts.size();
+    // token words per unit: at most one per bit of its span (every token costs >= 1 bit), plus
+    // room for the block that crosses the next start when that start is false; 16-B groups
+    std::vector<uint64_t> tokoff(K + 1);
+    const uint64_t nbits = 8ull * n;
+    tokoff[0] = 0;
+    for (uint64_t k = 0; k < K; k++) {
+        const uint64_t span = (k + 1 < K ? starts[k + 1] : nbits) - starts[k];
+        tokoff[k + 1] = tokoff[k] + ((span + 4096 + 63) & ~63ull);
+    }
+    if (!c->fbs.ensure(K * 8) || !c->fbt.ensure((K + 1) * 8) || !c->fbk.ensure(tokoff[K] * 4) ||
+        !c->fbu.ensure(K * sizeof(FbUnit)))
+        return DMX_OK;
+    HIPCHK(hipMemcpyAsync(c->fbs.p, starts.data(), K * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->fbt.p, tokoff.data(), (K + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(launch_fb_decode(words, misalign, n, c->fbs.as<uint64_t>(), K, c->fbt.as<uint64_t>(),
+                            c->fbk.as<uint32_t>(), c->fbu.as<FbUnit>(), c->flags, st));
+    std::vector<FbUnit> units(K);
+    HIPCHK(hipMemcpyAsync(units.data(), c->fbu.p, K * sizeof(FbUnit), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    // chain from bit 0: each unit must end where the next one on the chain starts
+    std::vector<uint32_t> chain;
+    std::vector<uint64_t> coffs, csizes;
+    uint64_t total = 0, k = 0;
+    for (;;) {
+        const FbUnit& u = units[k];
+        if (u.flags & ~SEGF_FINAL) return DMX_OK;
+        chain.push_back((uint32_t)k);
+        coffs.push_back(total);
+        csizes.push_back(u.size);
+        total += u.size;
+        if (u.flags & SEGF_FINAL) break;
+        const auto it = std::lower_bound(starts.begin() + k + 1, starts.end(), u.end);
+        if (it == starts.end() || *it != u.end) return DMX_OK;  // chain leaves the unit starts
+        k = (uint64_t)(it - starts.begin());
+    }
+    *handled = true;
+    *total_out = total;
+    uint8_t* out = fixed_out;
+    if (!out) {
+        if (!c->out.ensure(total ? total : 1)) return DMX_ERR_NOMEM;
+        out = c->out.as<uint8_t>();
+    } else if (total > cap) {
+        return DMX_ERR_CAPACITY;
+    }
+    const uint64_t nch = chain.size();
+    if (!c->fbch.ensure(nch * 4) || !c->fbco.ensure(nch * 8) || !c->fbcs.ensure(nch * 8) ||
+        !c->fbimg.ensure(total * 2 + 16))
+        return DMX_ERR_NOMEM;
+    HIPCHK(hipMemcpyAsync(c->fbch.p, chain.data(), nch * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->fbco.p, coffs.data(), nch * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->fbcs.p, csizes.data(), nch * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(&ds->fb_err, 0, 4, st));
+    HIPCHK(launch_fb_resolve(d_in, c->fbs.as<uint64_t>(), c->fbch.as<uint32_t>(), c->fbco.as<uint64_t>(),
+                             c->fbcs.as<uint64_t>(), nch, c->fbt.as<uint64_t>(), c->fbk.as<uint32_t>(),
+                             c->fbu.as<FbUnit>(), c->fbimg.as<uint16_t>(), total, out, &ds->fb_err, st));
+    if (c->timing) (void)hipEventRecord(c->ev[2], st);
+    uint32_t ferr = 0;
+    HIPCHK(hipMemcpyAsync(&ferr, &ds->fb_err, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (ferr) {
+        *handled = false;
+        *total_out = 0;
+        return DMX_OK;
+    }
+    c->stats.segments = nch;
+    if (dev_out) *dev_out = out;
+    return DMX_OK;
+}
+
 // Shared inflate driver.  fixed_out != nullptr: decode into the caller's device buffer of
 // `cap` bytes.  Otherwise decode into c->out, grown as needed (*dev_out receives it).
 int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_out,
@@ -303,6 +408,9 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     if (path_env != 1 && path_env != 4) plan[np][0] = 1, plan[np][1] = 0, np++;
     uint32_t lead_mode = 0;
     if (!parallel_ok) np = 0;
+    // no marker in a large stream: not libdmx's segment layout, the block-parallel path next
+    if (ncand == 1 && n > 65536 && path_env == -1) np = 0;
+    if (path_env == 5) np = 0;
     for (int pi = 0; pi < np; pi++) {
         const uint32_t mode = plan[pi][0];
         if (mode == 3 && (r.exotic == 0 || r.exotic > ncand / 8)) continue;  // nothing / too many
@@ -354,6 +462,17 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
         return r.total > cap ? DMX_ERR_CAPACITY : DMX_OK;
     }
 
+    if (path_env == -1 || path_env == 5) {
+        bool handled = false;
+        const int rc = inflate_fb_locked(c, d_in, n, fixed_out, cap, total_out, dev_out, st, &handled);
+        if (handled) {
+            end_timing(c, st);
+            c->stats.path = 5;
+            c->stats.in_bytes = n;
+            c->stats.out_bytes = *total_out;
+            return rc;
+        }
+    }
     // serial path: size pass, then write pass
     c->stats.path = 2;
     HIPCHK(launch_inflate_serial(A, 1, &ds->res, st));
@@ -443,7 +562,8 @@ void dmx_destroy(dmx_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->in, &c->out, &c->slots, &c->sizes, &c->offs, &c->scal, &c->cands,
                       &c->tiles, &c->tileoffs, &c->recs, &c->status, &c->dbg, &c->ltok,
-                      &c->ltokoff, &c->lntok, &c->lcaps})
+                      &c->ltokoff, &c->lntok, &c->lcaps, &c->fbc, &c->fbh, &c->fbo, &c->fbl,
+                      &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg})
         b->release();
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);

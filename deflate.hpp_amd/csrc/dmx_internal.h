@@ -99,6 +99,34 @@ hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* t
                                 uint32_t* ntok, uint32_t* caps, hipStream_t st, hipEvent_t ev0,
                                 hipEvent_t ev1);
 hipError_t launch_inflate_validate(const InflateArgs& A, InflateResult* res, hipStream_t st);
+
+// block-parallel inflate of arbitrary streams (inflate_blocks.hip, path 5)
+struct FbUnit {         // per-unit record written by k_fb_decode
+    uint64_t start;     // stream bit of the unit's first block
+    uint64_t end;       // stream bit just past its last block
+    uint64_t size;      // output bytes
+    uint32_t ntok;      // token words
+    uint32_t flags;     // SEGF_*
+};
+uint64_t fb_scan_chunks(uint64_t n);
+uint32_t fb_hits_per_chunk();
+// header scan of every bit offset: counts[nchunks], hits[nchunks * fb_hits_per_chunk()],
+// offs = exclusive scan of counts, *nhits = total
+hipError_t launch_fb_scan(const uint32_t* in_words, uint64_t misalign, uint64_t n,
+                          uint32_t* counts, uint64_t* hits, uint64_t* offs, uint64_t* nhits,
+                          hipStream_t st);
+hipError_t launch_fb_compact(const uint32_t* counts, const uint64_t* offs, const uint64_t* hits,
+                             uint64_t nchunks, uint64_t* list, hipStream_t st);
+hipError_t launch_fb_decode(const uint32_t* in_words, uint64_t misalign, uint64_t n,
+                            const uint64_t* starts, uint64_t nunits, const uint64_t* tokoff,
+                            uint32_t* tok, FbUnit* units, uint32_t flags, hipStream_t st);
+// replay + serial window hand-off + final resolve; *err (zeroed by the caller) becomes nonzero
+// when a copy reaches before the stream start
+hipError_t launch_fb_resolve(const uint8_t* stream, const uint64_t* starts, const uint32_t* chain,
+                             const uint64_t* offs, const uint64_t* sizes, uint64_t nchain,
+                             const uint64_t* tokoff, const uint32_t* tok, const FbUnit* units,
+                             uint16_t* img, uint64_t total, uint8_t* out, uint32_t* err,
+                             hipStream_t st);
 hipError_t launch_inflate_serial(const InflateArgs& A, int count_only, InflateResult* res,
                                  hipStream_t st);
 

@@ -35,6 +35,7 @@
 #include "../../include/dmx.h"
 #include "dmx_device.h"
 #include "dmx_internal.h"
+#include "inflate_common.h"
 
 namespace dmx {
 
@@ -52,103 +53,6 @@ constexpr uint32_t LN_LANES = DMX_LN_LANES;  // segments per 64-thread workgroup
 
 __constant__ const uint8_t kLnPerm[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5,
                                           11, 4,  12, 3, 13, 2, 14, 1, 15};
-
-// per-lane LSB-first bit reader over the stream in HBM: a 64-bit bit buffer fed from a ring
-// of eight 16-byte quads held in VGPRs (quad q of the stream lives in Q[q & 7]).  Loads are
-// issued only in wave-wide top-ups (every lane refills all its consumed quads at once, one
-// memory latency for the wave), never one lane at a time: s_waitcnt is per wave, so a lane's
-// lone reload would stall all 64.  Positions are bytes from blk (the 16-byte aligned base);
-// bytes at or past E read as zero.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) const u32x4 GUint4;  // global, not flat: a flat
-                                                               // load also counts in lgkmcnt
-#ifndef DMX_LN_RING_LOW
-#define DMX_LN_RING_LOW 16
-#endif
-constexpr uint32_t LN_RING_LOW = DMX_LN_RING_LOW;  // top up when fewer words than this are buffered
-
-struct LaneIn {
-    GUint4* blk;     // the candidate's first 16-byte quad: all positions below are 32-bit,
-    uint32_t nblk, E;  // relative to it (E clamped to 2^26 bytes, far beyond any accepted segment)
-    u32x4 Q0, Q1, Q2, Q3, Q4, Q5, Q6, Q7;
-    uint32_t fq;  // quads [.., fq) are in the ring
-    uint32_t wi;  // index of the next word to shift into bb
-    uint32_t nb;  // valid bits in bb
-    uint64_t bb;
-    // clamped to the last block (refill() zeroes bytes past E), so the load is unconditional
-    // within the lanes that issue it
-    __device__ __forceinline__ u32x4 fetch(uint32_t b) const { return blk[min(b, nblk - 1)]; }
-    __device__ __forceinline__ bool low() const { return fq * 4 < wi + LN_RING_LOW; }
-    // load quads [fq, wi/4 + 8): slot k gets the quad q == k (mod 8) in that range, or --
-    // when there is none -- its current quad again (same bytes), so all eight loads are
-    // unconditional.  The addresses are pinned in registers of their own before the first
-    // load: computed inside the loads' registers, each would first wait for the previous
-    // top-up's load there (vmcnt(0), which also drains the loads just issued).
-    __device__ __forceinline__ void topup() {
-        const uint32_t lim = (wi >> 2) + 8, last = nblk - 1;
-        uint64_t a[8];
-#pragma unroll
-        for (uint32_t k = 0; k < 8; k++) {
-            uint32_t q = fq + ((k - fq) & 7u);
-            if (q >= lim) q -= 8;
-            a[k] = reinterpret_cast<uint64_t>(blk + min(q, last));
-        }
-        asm volatile("" : : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]),
-                     "v"(a[6]), "v"(a[7]));
-        Q0 = *reinterpret_cast<GUint4*>(a[0]);
-        Q1 = *reinterpret_cast<GUint4*>(a[1]);
-        Q2 = *reinterpret_cast<GUint4*>(a[2]);
-        Q3 = *reinterpret_cast<GUint4*>(a[3]);
-        Q4 = *reinterpret_cast<GUint4*>(a[4]);
-        Q5 = *reinterpret_cast<GUint4*>(a[5]);
-        Q6 = *reinterpret_cast<GUint4*>(a[6]);
-        Q7 = *reinterpret_cast<GUint4*>(a[7]);
-        fq = lim;
-    }
-    __device__ __forceinline__ uint32_t word() const {
-        const uint32_t qs = (wi >> 2) & 7, ws = wi & 3;
-        const bool b0 = qs & 1, b1 = qs & 2, b2 = qs & 4;
-        const u32x4 p01 = b0 ? Q1 : Q0, p23 = b0 ? Q3 : Q2, p45 = b0 ? Q5 : Q4, p67 = b0 ? Q7 : Q6;
-        const u32x4 p03 = b1 ? p23 : p01, p47 = b1 ? p67 : p45;
-        const u32x4 q = b2 ? p47 : p03;
-        return (ws & 2) ? ((ws & 1) ? q.w : q.z) : ((ws & 1) ? q.y : q.x);
-    }
-    __device__ __forceinline__ void refill() {  // requires nb <= 32 and a word in the ring
-        uint32_t w = word();
-        const uint32_t wb = wi * 4;
-        if (wb + 4 > E) w = wb >= E ? 0u : (w & ((1u << (8 * (E - wb))) - 1u));
-        bb |= (uint64_t)w << nb;
-        nb += 32;
-        wi++;
-    }
-    __device__ void seek(uint32_t abyte) {
-        wi = abyte >> 2;
-        fq = wi >> 2;
-        topup();
-        bb = 0;
-        nb = 0;
-        refill();
-        refill();
-        const uint32_t sk = (abyte & 3) * 8;
-        bb >>= sk;
-        nb -= sk;
-    }
-    __device__ __forceinline__ void ensure(uint32_t k) {  // k <= 32
-        if (nb < k) refill();
-    }
-    __device__ __forceinline__ uint32_t bits(uint32_t n) {  // n <= 32, after ensure(n)
-        const uint32_t v = n ? (uint32_t)(bb & ((1ull << n) - 1ull)) : 0u;
-        bb >>= n;
-        nb -= n;
-        return v;
-    }
-    __device__ __forceinline__ void consume(uint32_t n) {
-        bb >>= n;
-        nb -= n;
-    }
-    __device__ __forceinline__ uint32_t bitpos() const { return wi * 32 - nb; }
-    __device__ __forceinline__ void align() { consume((uint32_t)(-bitpos()) & 7u); }  // next byte
-};
 
 struct LaneArgs {
     uint32_t* tok;          // token words

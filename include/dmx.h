@@ -111,7 +111,11 @@ typedef struct dmx_stats {
                                3 = workgroup-per-segment decoder (32 KiB slots),
                                4 = lane decoder + wave resolve (the default for libdmx
                                    streams: one lane decodes a segment's tokens, one
-                                   wavefront rebuilds its bytes)                            */
+                                   wavefront rebuilds its bytes),
+                               5 = block-parallel decoder for streams without segment
+                                   markers (zlib's, libdeflate's, the reference's own):
+                                   header scan, one wavefront per unit of blocks, window
+                                   hand-off                                                  */
     uint32_t reserved;
 } dmx_stats;
 
