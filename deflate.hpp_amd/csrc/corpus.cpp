@@ -59,10 +59,29 @@ struct TextGen {
             vocab[w] = s;
         }
     }
-    // stream text from position 0, copying only [off, off+n)
+    // Stream text from position 0, copying only [off, off+n).  The word stream is sequential
+    // (variable-length words), so a per-thread cursor remembers where the last call stopped:
+    // ascending windows (the mixed corpus takes text slices in offset order, a bench rank
+    // takes its shard) resume there instead of regenerating the prefix, and words before
+    // `off` are skipped without touching bytes.
+    struct Cursor {
+        uint64_t st = 0x5EED0004ull, pos = 0;
+    };
     void gen(uint64_t off, size_t n, uint8_t* out) const {
-        uint64_t st = 0x5EED0004ull;
-        uint64_t pos = 0, end = off + n;
+        thread_local Cursor cur;
+        Cursor c = cur.pos <= off ? cur : Cursor{};
+        const uint64_t end = off + n;
+        for (;;) {  // skip whole words that end at or before off
+            uint64_t s = c.st;
+            const uint64_t r = sm(s);
+            const unsigned k = (unsigned)(r % 13);
+            const uint64_t L = vocab[(r >> 8) & ((1ull << k) - 1)].size() + 1;
+            if (c.pos + L > off) break;
+            c.st = s;
+            c.pos += L;
+        }
+        cur = c;  // a word boundary at or before off
+        uint64_t st = c.st, pos = c.pos;
         while (pos < end) {
             uint64_t r = sm(st);
             unsigned k = (unsigned)(r % 13);
@@ -70,12 +89,11 @@ struct TextGen {
             const std::string& w = vocab[rank];
             char sep = ((r >> 60) == 0) ? '\n' : ' ';
             uint64_t L = w.size() + 1;
-            if (pos + L > off) {
-                for (uint64_t j = 0; j < L; j++) {
-                    uint64_t p = pos + j;
-                    if (p >= off && p < end) out[p - off] = (uint8_t)(j < w.size() ? w[j] : sep);
-                }
+            for (uint64_t j = 0; j < L; j++) {
+                uint64_t p = pos + j;
+                if (p >= off && p < end) out[p - off] = (uint8_t)(j < w.size() ? w[j] : sep);
             }
+            if (pos + L <= end) { cur.st = st; cur.pos = pos + L; }
             pos += L;
         }
     }
