@@ -8,19 +8,29 @@ inflate of the produced stream back into HBM; with N > 1 GPUs the compressed sha
 gathered to rank 0 over RCCL (the north_star's "final bitstream gather").  value = total
 uncompressed bytes of all ranks / max-over-ranks step time.
 
-  python bench.py                          # N=1, defaults
-  torchrun --nproc-per-node N bench.py --gpus N
+  python bench.py                          # N=1, defaults (+ the per-config sub-records)
+  torchrun --nproc-per-node N bench.py --gpus N [--strong]
 
-Prints ONE JSON line on rank 0.  Extra fields: per-phase GB/s, compression ratio next to the
-reference's ratio on the same corpus, the roofline of the dominant kernel (HIP-event timed
-on the stream it runs on), and the reference CPU baseline timed on this host (rank 0, N=1).
+Prints ONE JSON line on rank 0.  Besides the contract fields it carries, at N = 1:
+  corpora      the same round trip on the other Appendix-B corpora (1 GiB each): GB/s per
+               direction, ratio next to the reference's level-2 ratio and zlib-1's, the
+               roofline fraction of each direction's kernels
+  c3_inflate   config C3: inflate of the zlib level-1 stream of the 25,165,962-B large.bmp
+               stand-in (block-parallel path for marker-less streams) and of libdmx's own
+               stream of it, bit-exact checked
+  c5_level3    config C5: level 3 on the 1 GiB text corpus, ratio next to the reference L3's
+               and zlib-6's
+  cpu_baseline the reference compiled from its headers (oracle/_ref), 1 core and `nproc`
+               processes on disjoint slices, with the host CPU model
 """
 import argparse
-import ctypes
+import hashlib
 import json
 import os
+import subprocess
 import sys
 import time
+import zlib
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "deflate.hpp_amd"))
@@ -30,12 +40,14 @@ import shard  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 GiB = 1 << 30
+C3_N = 25165962  # large.bmp stand-in
 # reference ratios measured in the survey container
 REF_RATIO_L2 = {"zeros": 96.0938, "repeat": 19.6319, "text": 2.0892, "random": 0.9998,
                 "mixed": 2.4723, "bmp": 3.315}
 REF_NOTES = {"text": "reference L2 stream is lossy (SURVEY A-1)",
              "mixed": "reference L2 stream is invalid (SURVEY A-3)",
              "bmp": "reference L2 stream is invalid (SURVEY A-3)"}
+REF_RATIO_L3_TEXT = 2.5741  # reference L3 on the 1 MiB text prefix
 
 
 def parse():
@@ -44,46 +56,200 @@ def parse():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--corpus", default="repeat", choices=sorted(dmx.CORPUS))
-    p.add_argument("--bytes", type=int, default=GiB, help="uncompressed bytes per GPU")
+    p.add_argument("--bytes", type=int, default=GiB,
+                   help="uncompressed bytes per GPU (weak scaling) or in total (--strong)")
+    p.add_argument("--strong", action="store_true", help="fixed total size split over the ranks")
     p.add_argument("--level", type=int, default=2)
     p.add_argument("--segment", type=int, default=32768)
     p.add_argument("--cpu-sample", type=int, default=64 << 20,
-                   help="bytes of the same corpus the reference CPU baseline compresses")
+                   help="bytes of the same corpus the single-core reference baseline compresses")
+    p.add_argument("--cpu-slice", type=int, default=16 << 20,
+                   help="bytes per process of the nproc-process reference baseline")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extras", action="store_true", help="skip the per-config sub-records")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return p.parse_args()
 
 
-def cpu_baseline(kind_corpus, nbytes, level):
-    """Reference deflate::compress + inflate::decompress on one host core (oracle/_ref)."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(kind, nbytes, level, slice_bytes):
+    """Reference deflate::compress + inflate::decompress on the host cores (oracle/_ref):
+    (a) one thread on `nbytes`; (b) P processes on disjoint `slice_bytes` slices, started
+    together, wall-clock aggregate (SURVEY 8(d) "Timing method (CPU reference)")."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from oracle_bind import Reference, Oracle
-    data = dmx.corpus(kind_corpus, nbytes)
-    if Reference.available():
-        ref = Reference()
-        t0 = time.perf_counter()
-        comp = ref.compress(data, level)
-        t1 = time.perf_counter()
-        try:
-            ref.decompress(comp)
-            t2 = time.perf_counter()
-        except Exception:
-            t2 = t1 + float("nan")
-        secs = (t1 - t0) + (t2 - t1)
-        return {"value": round(nbytes / secs / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "reference",
-                "sample": f"{nbytes >> 20} MiB of the {kind_corpus} corpus, reference deflate::compress "
-                          f"level {level} + inflate::decompress (oracle/_ref, g++ -O2), single thread",
-                "deflate_GBps": round(nbytes / (t1 - t0) / 1e9, 6),
-                "inflate_GBps": round(nbytes / (t2 - t1) / 1e9, 6),
-                "ratio": round(nbytes / len(comp), 4)}
-    # restatement: only the inflate is restated in C (oracle/inflate_oracle.c)
-    orc = Oracle()
-    comp = dmx.compress(data, level)
+    from oracle_bind import Reference
+    if not Reference.available():
+        return {"error": "oracle/_ref/libdeflate_ref.so absent (built only where /root/reference exists)"}
+    data = dmx.corpus(kind, nbytes)
+    ref = Reference()
     t0 = time.perf_counter()
-    orc.inflate(comp)
-    secs = time.perf_counter() - t0
-    return {"value": round(nbytes / secs / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"{nbytes >> 20} MiB {kind_corpus}: oracle inflate only (oracle/_ref absent)"}
+    comp = ref.compress(data, level)
+    t1 = time.perf_counter()
+    try:
+        ref.decompress(comp)
+        t2 = time.perf_counter()
+    except Exception:
+        t2 = t1 + float("nan")
+    secs = t2 - t0
+    res = {"value": round(nbytes / secs / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "reference",
+           "sample": f"{nbytes >> 20} MiB of the {kind} corpus, reference deflate::compress level {level} "
+                     f"+ inflate::decompress (oracle/_ref, g++ -O2), single thread",
+           "deflate_GBps": round(nbytes / (t1 - t0) / 1e9, 6),
+           "inflate_GBps": round(nbytes / (t2 - t1) / 1e9, 6),
+           "ratio": round(nbytes / len(comp), 4), "cpu_model": cpu_model()}
+    # (b) P processes on disjoint slices; the box's CPU share is 16 per GPU
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    P = max(1, min(16, ncpu))
+    worker = os.path.join(ROOT, "tests", "cpu_ref_worker.py")
+    procs = [subprocess.Popen([sys.executable, worker, kind, str(i * slice_bytes), str(slice_bytes), str(level)],
+                              stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True) for i in range(P)]
+    for pr in procs:
+        if pr.stdout.readline().strip() != "ready":
+            raise RuntimeError("cpu worker failed to start")
+    w0 = time.perf_counter()
+    for pr in procs:
+        pr.stdin.write("go\n")
+        pr.stdin.flush()
+    outs = [json.loads(pr.stdout.readline()) for pr in procs]
+    wall = time.perf_counter() - w0
+    for pr in procs:
+        pr.wait(timeout=60)
+    tot = P * slice_bytes
+    res["nproc"] = {"value": round(tot / wall / 1e9, 6), "unit": "GB/s", "cores": P,
+                    "sample": f"{P} processes x {slice_bytes >> 20} MiB disjoint slices of the {kind} corpus, "
+                              f"deflate level {level} + inflate each, wall clock from a common start",
+                    "deflate_s_max": round(max(o["deflate_s"] for o in outs), 3),
+                    "inflate_s_max": round(max(o["inflate_s"] for o in outs), 3)}
+    return res
+
+
+class Runner:
+    """Device-resident deflate + inflate of one shard on one GPU (buffers reused across corpora)."""
+
+    def __init__(self, torch, ctx, dev, n, stream):
+        self.torch, self.ctx, self.dev, self.n, self.stream = torch, ctx, dev, n, stream
+        self.bound = dmx.deflate_bound(n) + 64
+        self.d_in = torch.empty(n + 64, dtype=torch.uint8, device=dev)
+        self.d_comp = torch.empty(self.bound, dtype=torch.uint8, device=dev)
+        self.d_out = torch.empty(n + 64, dtype=torch.uint8, device=dev)
+
+    def load(self, kind, offset):
+        torch = self.torch
+        host = torch.empty(self.n, dtype=torch.uint8).pin_memory()
+        dmx.corpus_into(kind, self.n, host.data_ptr(), offset=offset)
+        self.d_in[: self.n].copy_(host)
+        del host
+
+    def step(self, level, not_final=False, gather=None):
+        """One round trip; returns (events, clen, olen, deflate stats, inflate stats)."""
+        torch, n, sh = self.torch, self.n, self.stream.cuda_stream
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record(self.stream)
+        clen = self.ctx.deflate_device(self.d_in.data_ptr(), n, level, self.d_comp.data_ptr(), self.bound,
+                                       stream=sh, not_final=not_final)
+        ks_d = self.ctx.stats()
+        ev[1].record(self.stream)
+        if gather is not None:
+            gather(self.d_comp, clen)
+        ev[2].record(self.stream)
+        ilen = clen
+        if not_final:  # make the shard a complete stream for the local round trip
+            self.d_comp[clen: clen + 2].copy_(torch.tensor([0x03, 0x00], dtype=torch.uint8, device=self.dev))
+            ilen = clen + 2
+        olen = self.ctx.inflate_device(self.d_comp.data_ptr(), ilen, self.d_out.data_ptr(), n + 64, stream=sh)
+        ks_i = self.ctx.stats()
+        ev[3].record(self.stream)
+        return ev, clen, olen, ks_d, ks_i
+
+    def verify(self, olen):
+        return olen == self.n and bool(self.torch.equal(self.d_out[: self.n], self.d_in[: self.n]))
+
+
+def summarize(recs, n):
+    t_def = sum(r[0][0].elapsed_time(r[0][1]) for r in recs) / len(recs)
+    t_gat = sum(r[0][1].elapsed_time(r[0][2]) for r in recs) / len(recs)
+    t_inf = sum(r[0][2].elapsed_time(r[0][3]) for r in recs) / len(recs)
+    k_def = sum(r[3].ms_main_kernel for r in recs) / len(recs)
+    k_inf = sum(r[4].ms_main_kernel for r in recs) / len(recs)
+    clen = recs[-1][1]
+    alg = n + clen
+    return {"t_def": t_def, "t_gat": t_gat, "t_inf": t_inf, "k_def": k_def, "k_inf": k_inf,
+            "clen": clen, "alg": alg, "path": int(recs[-1][4].path),
+            "frac_def": alg / (k_def * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "frac_inf": alg / (k_inf * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+
+
+INF_KERNEL = {3: "k_inflate_pj", 4: "k_inflate_lanes+k_inflate_resolve",
+              5: "k_fb_decode+k_fb_resolve (block-parallel)", 2: "k_inflate_serial"}
+
+
+def zlib_ratio(kind, level, nbytes=16 << 20):
+    d = dmx.corpus(kind, nbytes)
+    z = zlib.compressobj(level, zlib.DEFLATED, -15)
+    return round(len(d) / len(z.compress(d) + z.flush()), 4)
+
+
+def corpus_record(run, kind, level, steps):
+    run.load(kind, 0)
+    run.step(level)
+    ev, clen, olen, _, _ = run.step(level)
+    ok = run.verify(olen)
+    recs = [run.step(level) for _ in range(steps)]
+    run.torch.cuda.synchronize(run.dev)
+    s = summarize(recs, run.n)
+    n = run.n
+    return {"bytes": n, "level": level, "roundtrip_ok": ok,
+            "roundtrip_GBps": round(n / ((s["t_def"] + s["t_inf"]) * 1e-3) / 1e9, 3),
+            "deflate_GBps": round(n / (s["t_def"] * 1e-3) / 1e9, 3),
+            "inflate_GBps": round(n / (s["t_inf"] * 1e-3) / 1e9, 3),
+            "ratio": round(n / s["clen"], 4),
+            "ref_ratio_L2": REF_RATIO_L2.get(kind), "ref_note": REF_NOTES.get(kind, "reference L2 round-trips"),
+            "zlib1_ratio_16MiB": zlib_ratio(kind, 1),
+            "kernel_ms": {"k_deflate_segments": round(s["k_def"], 4),
+                          INF_KERNEL.get(s["path"], "k_inflate_segments"): round(s["k_inf"], 4)},
+            "inflate_path": s["path"],
+            "roofline_frac": {"deflate": round(s["frac_def"], 5), "inflate": round(s["frac_inf"], 5)}}
+
+
+def c3_record(torch, ctx, dev, stream):
+    """Config C3: inflate of large.bmp's zlib-1 raw stream and of libdmx's
+    own level-2 stream of it (C3 (ii)); output bit-exact to the original (= the reference's
+    inflate output, tests/golden/manifest.json c3_bmp_zlib1)."""
+    data = dmx.corpus("bmp", C3_N)
+    z = zlib.compressobj(1, zlib.DEFLATED, -15)
+    s = z.compress(data) + z.flush()
+    ref = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    out = torch.empty(C3_N + 64, dtype=torch.uint8, device=dev)
+    res = {"n": C3_N, "sha256_out_expected": hashlib.sha256(data).hexdigest()[:16]}
+    streams = {"zlib1": s, "libdmx_L2": ctx.compress(data, 2)}
+    for name, st in streams.items():
+        d_s = torch.frombuffer(bytearray(st), dtype=torch.uint8).to(dev)
+        ms = []
+        for it in range(8):
+            olen = ctx.inflate_device(d_s.data_ptr(), len(st), out.data_ptr(), C3_N + 64,
+                                      stream=stream.cuda_stream)
+            if it >= 3:
+                ms.append(ctx.stats().ms_device_total)
+        ms.sort()
+        med = ms[len(ms) // 2]
+        ok = olen == C3_N and bool(torch.equal(out[:C3_N], ref))
+        res[name] = {"stream_bytes": len(st), "inflate_ms": round(med, 3),
+                     "inflate_GBps": round(C3_N / (med * 1e-3) / 1e9, 3), "path": int(ctx.stats().path),
+                     "roofline_frac": round((C3_N + len(st)) / (med * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
+                     "bit_exact": ok}
+    return res
 
 
 def main():
@@ -100,50 +266,25 @@ def main():
     dev = torch.device("cuda", local)
     ctx = dmx.Context(device=local, segment_bytes=a.segment)
     ctx.set_timing(True)
-    n = a.bytes
-
-    # input shard r = bytes [r*n, (r+1)*n) of the corpus, generated on the host, copied to HBM
-    host = torch.empty(n, dtype=torch.uint8).pin_memory()
-    dmx.corpus_into(a.corpus, n, host.data_ptr(), offset=rank * n)
-    d_in = host.to(dev, non_blocking=False)
-    del host
-    bound = dmx.deflate_bound(n) + 64
-    d_comp = torch.empty(bound, dtype=torch.uint8, device=dev)
-    d_out = torch.empty(n + 64, dtype=torch.uint8, device=dev)
-    last = rank == world - 1
+    if a.strong:  # fixed total: rank r takes its segment-aligned share
+        b, e = shard.shard_range(a.bytes, rank, world, a.segment)
+        n, offset = max(e - b, 0), b
+    else:
+        n, offset = a.bytes, rank * a.bytes
     stream = torch.cuda.current_stream(dev)
-    sh = stream.cuda_stream
-    tail = torch.tensor([0x03, 0x00], dtype=torch.uint8, device=dev)  # final empty fixed block
+    run = Runner(torch, ctx, dev, n, stream)
+    run.load(a.corpus, offset)
+    last = rank == world - 1
     gathered = None
     if world > 1 and rank == 0:
-        gathered = torch.empty(world * bound, dtype=torch.uint8, device=dev)
-
-    def step(record):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-        ev[0].record(stream)
-        clen = ctx.deflate_device(d_in.data_ptr(), n, a.level, d_comp.data_ptr(), bound, stream=sh,
-                                  not_final=not last)
-        ks_d = ctx.stats()
-        ev[1].record(stream)
-        if world > 1:  # RCCL gather of the compressed shards to rank 0 (xGMI P2P)
-            shard.gather_stream(d_comp, clen, gathered)
-        ev[2].record(stream)
-        ilen = clen
-        if not last:  # make the shard a complete stream for the local round trip
-            d_comp[clen: clen + 2].copy_(tail)
-            ilen = clen + 2
-        olen = ctx.inflate_device(d_comp.data_ptr(), ilen, d_out.data_ptr(), n + 64, stream=sh)
-        ks_i = ctx.stats()
-        ev[3].record(stream)
-        if record is not None:
-            record.append((ev, clen, olen, ks_d, ks_i))
-        return clen, olen
+        gathered = torch.empty(world * run.bound, dtype=torch.uint8, device=dev)
+    gather = (lambda buf, clen: shard.gather_stream(buf, clen, gathered)) if world > 1 else None
 
     for _ in range(a.warmup):
-        step(None)
+        run.step(a.level, not_final=not last, gather=gather)
     # correctness of the round trip (outside the timed region)
-    clen, olen = step(None)
-    ok = olen == n and torch.equal(d_out[:n], d_in)
+    _, clen, olen, _, _ = run.step(a.level, not_final=not last, gather=gather)
+    ok = run.verify(olen)
 
     recs = []
     if world > 1:
@@ -151,11 +292,12 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        step(recs)
+        recs.append(run.step(a.level, not_final=not last, gather=gather))
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    total_bytes = a.bytes if a.strong else world * n
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -170,74 +312,79 @@ def main():
     for _ in range(3):
         c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         c0.record()
-        d_out[:n].copy_(d_in)
+        run.d_out[:n].copy_(run.d_in[:n])
         c1.record()
         c1.synchronize()
         copy_ms = min(copy_ms, c0.elapsed_time(c1))
     d2d_gbps = 2 * n / (copy_ms * 1e-3) / 1e9
 
     ms_step = elapsed / a.steps * 1e3
-    t_def = sum(r[0][0].elapsed_time(r[0][1]) for r in recs) / len(recs)
-    t_gat = sum(r[0][1].elapsed_time(r[0][2]) for r in recs) / len(recs)
-    t_inf = sum(r[0][2].elapsed_time(r[0][3]) for r in recs) / len(recs)
-    k_def = sum(r[3].ms_main_kernel for r in recs) / len(recs)
-    k_inf = sum(r[4].ms_main_kernel for r in recs) / len(recs)
-    comp_bytes = recs[-1][1]
-    ratio = n / comp_bytes
+    s = summarize(recs, n)
+    ratio = n / s["clen"]
     # roofline of the dominant kernel: algorithmic bytes = N read + C written (deflate) or
     # C read + N written (inflate), per launch, over its HIP-event duration
-    alg = n + comp_bytes
-    path = recs[-1][4].path
-    inf_kernel = {3: "k_inflate_pj", 4: "k_inflate_lanes+k_inflate_resolve"}.get(path, "k_inflate_segments")
-    dom = inf_kernel if k_inf >= k_def else "k_deflate_segments"
-    kms = max(k_inf, k_def)
-    achieved = alg / (kms * 1e-3) / 1e9
+    inf_kernel = INF_KERNEL.get(s["path"], "k_inflate_segments")
+    dom = inf_kernel if s["k_inf"] >= s["k_def"] else "k_deflate_segments"
+    kms = max(s["k_inf"], s["k_def"])
+    achieved = s["alg"] / (kms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(a.traffic_json):
         try:
-            tj = json.load(open(a.traffic_json))
-            key = f"{a.corpus}:{n}:{a.level}:{dom}"
-            traffic = tj.get(key)
+            traffic = json.load(open(a.traffic_json)).get(f"{a.corpus}:{n}:{a.level}:{dom}")
         except Exception:
             traffic = None
 
+    res = None
     if rank == 0:
         res = {
             "metric": "GB/s deflate+inflate on 1 GiB buffer at 1/2/4/8 MI355X; ratio vs reference",
-            "value": round(world * n / (ms_step * 1e-3) / 1e9, 4),
+            "value": round(total_bytes / (ms_step * 1e-3) / 1e9, 4),
             "unit": "GB/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": f"deflate level {a.level} + inflate round trip of a {n >> 30} GiB "
-                                   f"'{a.corpus}' corpus shard per GPU (SURVEY App. B), device-resident",
+            "config": {"workload": f"deflate level {a.level} + inflate round trip of a "
+                                   f"{'total' if a.strong else 'per-GPU'} {a.bytes / GiB:g} GiB '{a.corpus}' "
+                                   f"corpus (SURVEY App. B), device-resident",
                        "corpus": a.corpus, "bytes_per_gpu": n, "level": a.level,
                        "segment_bytes": a.segment, "parallelism": f"shard{world}"},
             "roundtrip_ok": ok,
-            "deflate_GBps": round(world * n / (t_def * 1e-3) / 1e9, 4),
-            "inflate_GBps": round(world * n / (t_inf * 1e-3) / 1e9, 4),
-            "gather_ms": round(t_gat, 4),
+            "deflate_GBps": round(total_bytes / (s["t_def"] * 1e-3) / 1e9, 4),
+            "inflate_GBps": round(total_bytes / (s["t_inf"] * 1e-3) / 1e9, 4),
+            "gather_ms": round(s["t_gat"], 4),
             "ratio": round(ratio, 4),
             "ref_ratio": REF_RATIO_L2.get(a.corpus) if a.level == 2 else None,
             "ref_ratio_note": REF_NOTES.get(a.corpus, "reference L2 stream round-trips"),
-            "kernel_ms": {"k_deflate_segments": round(k_def, 4), inf_kernel: round(k_inf, 4)},
-            "inflate_path": int(recs[-1][4].path),
+            "kernel_ms": {"k_deflate_segments": round(s["k_def"], 4), inf_kernel: round(s["k_inf"], 4)},
+            "inflate_path": s["path"],
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                          "traffic": traffic, "kernel": dom,
-                         "alg_bytes_per_launch": alg,
+                         "alg_bytes_per_launch": s["alg"],
+                         "frac_deflate": round(s["frac_def"], 5), "frac_inflate": round(s["frac_inf"], 5),
                          "d2d_copy_GBps": round(d2d_gbps, 1)},
             "cpu_baseline": None,
         }
+    if world == 1 and not a.no_extras:
+        # sub-records (outside the timed region): the other corpora, C3 and C5
+        extras = {}
+        for kind in ("text", "mixed", "random", "zeros"):
+            if kind != a.corpus:
+                extras[kind] = corpus_record(run, kind, a.level, 3)
+        res["corpora"] = extras
+        res["c5_level3"] = corpus_record(run, "text", 3, 3)
+        res["c5_level3"].update({"ref_ratio_L3_1MiB": REF_RATIO_L3_TEXT, "zlib6_ratio_16MiB": zlib_ratio("text", 6)})
+        res["c3_inflate"] = c3_record(torch, ctx, dev, stream)
+    if rank == 0:
         if world == 1 and not a.no_cpu_baseline:
             try:
-                res["cpu_baseline"] = cpu_baseline(a.corpus, min(a.cpu_sample, n), a.level)
+                res["cpu_baseline"] = cpu_baseline(a.corpus, min(a.cpu_sample, n), a.level, a.cpu_slice)
             except Exception as e:  # the baseline is informative, never fatal
                 res["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(res), flush=True)

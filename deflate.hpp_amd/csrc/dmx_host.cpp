@@ -8,7 +8,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <thread>
 #include <cstdlib>
 #include <vector>
 #include <cstring>
@@ -63,6 +65,7 @@ struct dmx_ctx {
     // block-parallel path (path 5): scan counts / hits / offsets, hit list, unit starts, token
     // offsets and words, unit records, chain (unit index, offset, size), 16-bit image
     DevBuf fbc, fbh, fbo, fbl, fbs, fbt, fbk, fbu, fbch, fbco, fbcs, fbimg;
+    DevBuf ck;  // checksum scratch (checksum.hip) + the 4-byte result at its start
     bool timing = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     dmx_stats stats{};
@@ -496,6 +499,63 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     return r.status;
 }
 
+// Adler-32 / CRC-32 of a device buffer, computed on the GPU (checksum.hip); the value is
+// returned to the host (the call synchronizes the stream).
+int checksum_locked(dmx_ctx* c, bool crc, const uint8_t* d, size_t n, uint32_t init, uint32_t* out,
+                    hipStream_t st) {
+    if (!c->ck.ensure(256 + checksum_scratch_bytes(n))) return DMX_ERR_NOMEM;
+    uint32_t* d_res = c->ck.as<uint32_t>();
+    void* scratch = c->ck.as<uint8_t>() + 256;
+    if (crc) HIPCHK(launch_crc32_raw(d, n, scratch, d_res, st));
+    else HIPCHK(launch_adler32(d, n, init, scratch, d_res, st));
+    uint32_t v = 0;
+    HIPCHK(hipMemcpyAsync(&v, d_res, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *out = crc ? crc32_finish(v, n, init) : v;
+    return DMX_OK;
+}
+
+// zlib (RFC 1950) / gzip (RFC 1952) framing around libdmx's raw stream; the checksum of the
+// input is computed on the GPU from the device copy the deflate reads.
+int deflate_framed(dmx_ctx* c, bool gz, const uint8_t* in, size_t n, int level, uint8_t* out, size_t cap,
+                   size_t* out_len) {
+    const size_t head = gz ? 10 : 2, tail = gz ? 8 : 4;
+    *out_len = 0;
+    const size_t bound = dmx_deflate_bound(n);
+    if (!c->in.ensure(n + 16) || !c->out.ensure(bound)) return DMX_ERR_NOMEM;
+    if (n) HIPCHK(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
+    size_t total = 0;
+    int rc = deflate_device_locked(c, c->in.as<uint8_t>(), n, level, 0, c->out.as<uint8_t>(), c->out.cap,
+                                   &total, c->stream);
+    if (rc != DMX_OK) return rc;
+    uint32_t ck = 0;
+    rc = checksum_locked(c, gz, c->in.as<uint8_t>(), n, gz ? 0u : 1u, &ck, c->stream);
+    if (rc != DMX_OK) return rc;
+    *out_len = head + total + tail;
+    if (head + total + tail > cap) return DMX_ERR_CAPACITY;
+    const int lv = (level < 0 || level > 3) ? 1 : level;
+    if (gz) {
+        const uint8_t h[10] = {0x1F, 0x8B, 8, 0, 0, 0, 0, 0, (uint8_t)(lv == 3 ? 2 : lv <= 1 ? 4 : 0), 255};
+        std::memcpy(out, h, 10);
+    } else {
+        const uint32_t flevel = lv <= 1 ? 0 : lv == 2 ? 1 : 3;  // RFC 1950 FLEVEL
+        const uint32_t cmf = 0x78, flg0 = flevel << 6;
+        const uint32_t flg = flg0 + (31 - (cmf * 256 + flg0) % 31) % 31;
+        out[0] = (uint8_t)cmf;
+        out[1] = (uint8_t)flg;
+    }
+    if (total) HIPCHK(hipMemcpyAsync(out + head, c->out.p, total, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    uint8_t* t = out + head + total;
+    if (gz) {
+        for (int b = 0; b < 4; b++) t[b] = (uint8_t)(ck >> (8 * b));
+        for (int b = 0; b < 4; b++) t[4 + b] = (uint8_t)((uint64_t)n >> (8 * b));
+    } else {
+        for (int b = 0; b < 4; b++) t[b] = (uint8_t)(ck >> (24 - 8 * b));
+    }
+    return DMX_OK;
+}
+
 // Restores the calling thread's current HIP device on scope exit: an entry point switches to
 // its context's device, and a caller driving several GPUs from one thread must not see its
 // current device move.
@@ -563,7 +623,8 @@ void dmx_destroy(dmx_ctx* c) {
     for (DevBuf* b : {&c->in, &c->out, &c->slots, &c->sizes, &c->offs, &c->scal, &c->cands,
                       &c->tiles, &c->tileoffs, &c->recs, &c->status, &c->dbg, &c->ltok,
                       &c->ltokoff, &c->lntok, &c->lcaps, &c->fbc, &c->fbh, &c->fbo, &c->fbl,
-                      &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg})
+                      &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg,
+                      &c->ck})
         b->release();
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -682,6 +743,405 @@ int dmx_inflate_alloc(dmx_ctx* c, const uint8_t* in, size_t n, uint8_t** out, si
     return DMX_OK;
 }
 
+// ---- segment index for multi-GPU inflate ------------------------------------
+int dmx_segment_starts_device(dmx_ctx* c, const void* d_in, size_t n, uint64_t* starts, size_t cap,
+                              size_t* count, void* stream) {
+    if (!c || (!d_in && n) || !count || (!starts && cap)) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    *count = 0;
+    if (n == 0) return DMX_OK;
+    if (!c->scal.ensure(sizeof(Scal))) return DMX_ERR_NOMEM;
+    Scal* ds = c->scal.as<Scal>();
+    const uint8_t* in = static_cast<const uint8_t*>(d_in);
+    const uint64_t misalign = (uintptr_t)in & 3;
+    const uint32_t* words = reinterpret_cast<const uint32_t*>(in - misalign);
+    const uint64_t ntiles = marker_tiles(n, misalign);
+    if (!c->tiles.ensure(ntiles * 4) || !c->tileoffs.ensure(ntiles * 8)) return DMX_ERR_NOMEM;
+    HIPCHK(launch_marker_count(words, misalign, n, c->tiles.as<uint32_t>(), ntiles, st));
+    HIPCHK(launch_scan_u32(c->tiles.as<uint32_t>(), c->tileoffs.as<uint64_t>(), ntiles, &ds->nmarkers, st));
+    uint64_t nm = 0;
+    HIPCHK(hipMemcpyAsync(&nm, &ds->nmarkers, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (!c->cands.ensure((nm + 1) * 8)) return DMX_ERR_NOMEM;
+    HIPCHK(launch_marker_write(words, misalign, n, c->tileoffs.as<uint64_t>(), ntiles, c->cands.as<uint64_t>(),
+                               nullptr, st));
+    // cands[0] is the stream start; markers follow
+    const size_t k = std::min<size_t>(cap, nm);
+    if (k) HIPCHK(hipMemcpyAsync(starts, c->cands.as<uint64_t>() + 1, k * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *count = nm;
+    return DMX_OK;
+}
+
+// ---- checksums and zlib / gzip containers ------------------------------
+int dmx_adler32_device(dmx_ctx* c, const void* d, size_t n, uint32_t init, uint32_t* out, void* stream) {
+    if (!c || (!d && n) || !out) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
+    return checksum_locked(c, false, (const uint8_t*)d, n, init, out, stream ? (hipStream_t)stream : c->stream);
+}
+
+int dmx_crc32_device(dmx_ctx* c, const void* d, size_t n, uint32_t init, uint32_t* out, void* stream) {
+    if (!c || (!d && n) || !out) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
+    return checksum_locked(c, true, (const uint8_t*)d, n, init, out, stream ? (hipStream_t)stream : c->stream);
+}
+
+static int checksum_host(dmx_ctx* c, bool crc, const uint8_t* in, size_t n, uint32_t init, uint32_t* out) {
+    if (!c) c = dmx_default_ctx();
+    if (!c) return DMX_ERR_DEVICE;
+    if ((!in && n) || !out) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
+    if (!c->in.ensure(n + 16)) return DMX_ERR_NOMEM;
+    if (n) HIPCHK(hipMemcpyAsync(c->in.p, in, n, hipMemcpyHostToDevice, c->stream));
+    return checksum_locked(c, crc, c->in.as<uint8_t>(), n, init, out, c->stream);
+}
+
+int dmx_adler32(dmx_ctx* c, const uint8_t* in, size_t n, uint32_t init, uint32_t* out) {
+    return checksum_host(c, false, in, n, init, out);
+}
+
+int dmx_crc32(dmx_ctx* c, const uint8_t* in, size_t n, uint32_t init, uint32_t* out) {
+    return checksum_host(c, true, in, n, init, out);
+}
+
+size_t dmx_framed_bound(size_t n) { return dmx_deflate_bound(n) + 18; }
+
+static int deflate_framed_entry(dmx_ctx* c, bool gz, const uint8_t* in, size_t n, int level, uint8_t* out,
+                                size_t cap, size_t* out_len) {
+    if (!c) c = dmx_default_ctx();
+    if (!c) return DMX_ERR_DEVICE;
+    if ((!in && n) || !out_len || !out) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
+    return deflate_framed(c, gz, in, n, level, out, cap, out_len);
+}
+
+int dmx_deflate_zlib(dmx_ctx* c, const uint8_t* in, size_t n, int level, uint8_t* out, size_t cap,
+                     size_t* out_len) {
+    return deflate_framed_entry(c, false, in, n, level, out, cap, out_len);
+}
+
+int dmx_deflate_gzip(dmx_ctx* c, const uint8_t* in, size_t n, int level, uint8_t* out, size_t cap,
+                     size_t* out_len) {
+    return deflate_framed_entry(c, true, in, n, level, out, cap, out_len);
+}
+
+// Parses the container header, inflates the raw stream on the GPU and (DMX_VERIFY) checks the
+// trailer against the GPU checksum of the decoded bytes.  The trailer is taken from the last
+// 4 (zlib) / 8 (gzip) bytes of the input.
+static int inflate_framed(dmx_ctx* c, bool gz, const uint8_t* in, size_t n, uint32_t flags, uint8_t** out,
+                          size_t* len) {
+    if (!c) c = dmx_default_ctx();
+    if (!c) return DMX_ERR_DEVICE;
+    if ((!in && n) || !out || !len) return DMX_ERR_ARG;
+    *out = nullptr;
+    *len = 0;
+    size_t head = 0;
+    if (gz) {
+        if (n < 18) return DMX_ERR_OVERREAD;
+        if (in[0] != 0x1F || in[1] != 0x8B || in[2] != 8) return DMX_ERR_DATA;
+        const uint8_t flg = in[3];
+        head = 10;
+        if (flg & 4) {  // FEXTRA
+            if (head + 2 > n) return DMX_ERR_OVERREAD;
+            head += 2 + (size_t)(in[head] | (in[head + 1] << 8));
+        }
+        for (int z = 0; z < 2; z++) {  // FNAME, FCOMMENT: zero-terminated
+            if (flg & (8 << z)) {
+                while (head < n && in[head]) head++;
+                head++;
+            }
+        }
+        if (flg & 2) head += 2;  // FHCRC
+        if (head + 8 > n) return DMX_ERR_OVERREAD;
+    } else {
+        if (n < 6) return DMX_ERR_OVERREAD;
+        const uint32_t cmf = in[0], flg = in[1];
+        if ((cmf & 15) != 8 || (cmf >> 4) > 7 || (cmf * 256 + flg) % 31 != 0) return DMX_ERR_DATA;
+        if (flg & 0x20) return DMX_ERR_DATA;  // preset dictionary: not supported
+        head = 2;
+    }
+    std::lock_guard<std::mutex> g(c->mu);
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
+    uint8_t* dev = nullptr;
+    size_t tot = 0;
+    int rc = inflate_host(c, in + head, n - head, &dev, &tot);
+    if (rc != DMX_OK) return rc;
+    if (flags & DMX_VERIFY) {
+        uint32_t ck = 0;
+        rc = checksum_locked(c, gz, dev, tot, gz ? 0u : 1u, &ck, c->stream);
+        if (rc != DMX_OK) return rc;
+        const uint8_t* t = in + n - (gz ? 8 : 4);
+        uint32_t want = 0;
+        if (gz) {
+            want = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
+            const uint32_t isize = (uint32_t)t[4] | ((uint32_t)t[5] << 8) | ((uint32_t)t[6] << 16) |
+                                   ((uint32_t)t[7] << 24);
+            if (isize != (uint32_t)tot) return DMX_ERR_CHECKSUM;
+        } else {
+            want = ((uint32_t)t[0] << 24) | ((uint32_t)t[1] << 16) | ((uint32_t)t[2] << 8) | (uint32_t)t[3];
+        }
+        if (ck != want) return DMX_ERR_CHECKSUM;
+    }
+    uint8_t* h = static_cast<uint8_t*>(std::malloc(tot ? tot : 1));
+    if (!h) return DMX_ERR_NOMEM;
+    if (tot && hipMemcpyAsync(h, dev, tot, hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
+        std::free(h);
+        return DMX_ERR_DEVICE;
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess) {
+        std::free(h);
+        return DMX_ERR_DEVICE;
+    }
+    *out = h;
+    *len = tot;
+    return DMX_OK;
+}
+
+int dmx_inflate_zlib(dmx_ctx* c, const uint8_t* in, size_t n, uint32_t flags, uint8_t** out, size_t* len) {
+    return inflate_framed(c, false, in, n, flags, out, len);
+}
+
+int dmx_inflate_gzip(dmx_ctx* c, const uint8_t* in, size_t n, uint32_t flags, uint8_t** out, size_t* len) {
+    return inflate_framed(c, true, in, n, flags, out, len);
+}
+
+// ---- file-path overloads with streaming I/O ----------------------------
+namespace {
+
+struct Pinned {
+    void* p = nullptr;
+    explicit Pinned(size_t n) {
+        if (hipHostMalloc(&p, n ? n : 1, hipHostMallocDefault) != hipSuccess) p = nullptr;
+    }
+    ~Pinned() {
+        if (p) (void)hipHostFree(p);
+    }
+    uint8_t* u8() const { return static_cast<uint8_t*>(p); }
+};
+
+struct File {
+    FILE* f = nullptr;
+    File(const char* path, const char* mode) : f(std::fopen(path, mode)) {}
+    ~File() {
+        if (f) std::fclose(f);
+    }
+};
+
+// A reader thread fills two pinned buffers in turn from a file (chunk k into buffer k % 2);
+// the consumer takes chunk k, and releases its buffer once the H2D copy from it has finished.
+struct ChunkReader {
+    FILE* f;
+    size_t chunk, total, nchunks;
+    uint8_t* buf[2];
+    size_t len[2] = {0, 0};
+    bool ready[2] = {false, false};
+    bool failed = false, stop = false;
+    std::mutex m;
+    std::condition_variable cv;
+    std::thread th;
+    ChunkReader(FILE* f_, size_t total_, size_t chunk_, uint8_t* b0, uint8_t* b1)
+        : f(f_), chunk(chunk_), total(total_), nchunks((total_ + chunk_ - 1) / chunk_), buf{b0, b1} {
+        th = std::thread([this] { run(); });
+    }
+    ~ChunkReader() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            stop = true;
+        }
+        cv.notify_all();
+        th.join();
+    }
+    void run() {
+        for (size_t k = 0; k < nchunks; k++) {
+            const int b = (int)(k & 1);
+            {
+                std::unique_lock<std::mutex> g(m);
+                cv.wait(g, [&] { return !ready[b] || stop; });
+                if (stop) return;
+            }
+            const size_t want = std::min(chunk, total - k * chunk);
+            const size_t got = std::fread(buf[b], 1, want, f);
+            std::lock_guard<std::mutex> g(m);
+            len[b] = want;
+            ready[b] = true;
+            if (got != want) failed = true;
+            cv.notify_all();
+        }
+    }
+    // waits for chunk k; returns its buffer and length (nullptr on a read error)
+    uint8_t* take(size_t k, size_t* n) {
+        const int b = (int)(k & 1);
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [&] { return ready[b] || failed; });
+        if (failed) return nullptr;
+        *n = len[b];
+        return buf[b];
+    }
+    void release(size_t k) {
+        std::lock_guard<std::mutex> g(m);
+        ready[k & 1] = false;
+        cv.notify_all();
+    }
+};
+
+int64_t file_size(FILE* f) {
+    if (std::fseek(f, 0, SEEK_END) != 0) return -1;
+    const long long n = ftello(f);
+    if (std::fseek(f, 0, SEEK_SET) != 0) return -1;
+    return n;
+}
+
+constexpr size_t kFileChunk = 64ull << 20;  // bytes per streamed chunk (a multiple of 32 KiB)
+
+}  // namespace
+
+int dmx_deflate_file(dmx_ctx* c, const char* in_path, const char* out_path, int level, size_t* in_bytes,
+                     size_t* out_bytes) {
+    if (!c) c = dmx_default_ctx();
+    if (!c) return DMX_ERR_DEVICE;
+    if (!in_path || !out_path) return DMX_ERR_ARG;
+    File fi(in_path, "rb");
+    if (!fi.f) return DMX_ERR_ARG;
+    const int64_t N = file_size(fi.f);
+    if (N < 0) return DMX_ERR_ARG;
+    File fo(out_path, "wb");
+    if (!fo.f) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
+    const size_t K = kFileChunk;
+    const size_t bound = dmx_deflate_bound(K);
+    Pinned hin0(K), hin1(K), hout(bound);
+    DevBuf din[2], dout;
+    if (!hin0.p || !hin1.p || !hout.p || !din[0].ensure(K) || !din[1].ensure(K) || !dout.ensure(bound)) {
+        for (auto& d : din) d.release();
+        dout.release();
+        return DMX_ERR_NOMEM;
+    }
+    hipStream_t cs = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    int rc = DMX_OK;
+    if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) rc = DMX_ERR_DEVICE;
+    for (auto& e : ev)
+        if (rc == DMX_OK && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = DMX_ERR_DEVICE;
+    size_t written = 0;
+    if (rc == DMX_OK && N == 0) {  // empty file: one empty final block, as dmx_deflate
+        size_t len = 0;
+        rc = deflate_device_locked(c, nullptr, 0, level, 0, dout.as<uint8_t>(), bound, &len, c->stream);
+        if (rc == DMX_OK && hipMemcpy(hout.p, dout.p, len, hipMemcpyDeviceToHost) != hipSuccess) rc = DMX_ERR_DEVICE;
+        if (rc == DMX_OK && std::fwrite(hout.p, 1, len, fo.f) != len) rc = DMX_ERR_ARG;
+        written = len;
+    } else if (rc == DMX_OK) {
+        ChunkReader rd(fi.f, (size_t)N, K, hin0.u8(), hin1.u8());
+        const size_t nch = rd.nchunks;
+        // copy chunk k + 1 in on the copy stream while chunk k compresses on the context stream
+        auto h2d = [&](size_t k) -> int {
+            size_t n = 0;
+            uint8_t* h = rd.take(k, &n);
+            if (!h) return DMX_ERR_ARG;
+            if (hipMemcpyAsync(din[k & 1].p, h, n, hipMemcpyHostToDevice, cs) != hipSuccess) return DMX_ERR_DEVICE;
+            if (hipEventRecord(ev[k & 1], cs) != hipSuccess) return DMX_ERR_DEVICE;
+            return DMX_OK;
+        };
+        rc = h2d(0);
+        for (size_t k = 0; k < nch && rc == DMX_OK; k++) {
+            if (k + 1 < nch && (rc = h2d(k + 1)) != DMX_OK) break;
+            if (hipStreamWaitEvent(c->stream, ev[k & 1], 0) != hipSuccess) { rc = DMX_ERR_DEVICE; break; }
+            const size_t n = std::min(K, (size_t)N - k * K);
+            size_t len = 0;
+            rc = deflate_device_locked(c, din[k & 1].as<uint8_t>(), n, level, k + 1 < nch ? DMX_DEFLATE_NOT_FINAL : 0,
+                                       dout.as<uint8_t>(), bound, &len, c->stream);
+            if (rc != DMX_OK) break;
+            rd.release(k);  // the H2D of chunk k is complete (the deflate waited for it)
+            if (hipMemcpyAsync(hout.p, dout.p, len, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                hipStreamSynchronize(c->stream) != hipSuccess) { rc = DMX_ERR_DEVICE; break; }
+            if (std::fwrite(hout.p, 1, len, fo.f) != len) { rc = DMX_ERR_ARG; break; }
+            written += len;
+        }
+        (void)hipStreamSynchronize(cs);
+    }
+    for (auto& e : ev)
+        if (e) (void)hipEventDestroy(e);
+    if (cs) (void)hipStreamDestroy(cs);
+    for (auto& d : din) d.release();
+    dout.release();
+    if (in_bytes) *in_bytes = (size_t)N;
+    if (out_bytes) *out_bytes = written;
+    return rc;
+}
+
+int dmx_inflate_file(dmx_ctx* c, const char* in_path, const char* out_path, size_t* out_bytes) {
+    if (!c) c = dmx_default_ctx();
+    if (!c) return DMX_ERR_DEVICE;
+    if (!in_path || !out_path) return DMX_ERR_ARG;
+    if (out_bytes) *out_bytes = 0;
+    File fi(in_path, "rb");
+    if (!fi.f) return DMX_ERR_ARG;
+    const int64_t C = file_size(fi.f);
+    if (C < 0) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
+    const size_t K = kFileChunk;
+    if (!c->in.ensure((size_t)C + 16)) return DMX_ERR_NOMEM;
+    Pinned hb0(K), hb1(K);
+    if (!hb0.p || !hb1.p) return DMX_ERR_NOMEM;
+    int rc = DMX_OK;
+    {   // stream the compressed file in: disk reads overlap the H2D copies of earlier chunks
+        ChunkReader rd(fi.f, (size_t)C, K, hb0.u8(), hb1.u8());
+        for (size_t k = 0; k < rd.nchunks && rc == DMX_OK; k++) {
+            size_t n = 0;
+            uint8_t* h = rd.take(k, &n);
+            if (!h) { rc = DMX_ERR_ARG; break; }
+            if (hipMemcpyAsync(c->in.as<uint8_t>() + k * K, h, n, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+                hipStreamSynchronize(c->stream) != hipSuccess) { rc = DMX_ERR_DEVICE; break; }
+            rd.release(k);
+        }
+    }
+    if (rc != DMX_OK) return rc;
+    uint8_t* dev = nullptr;
+    size_t tot = 0;
+    rc = inflate_device_locked(c, c->in.as<uint8_t>(), (size_t)C, nullptr, 0, &tot, &dev, c->stream);
+    if (rc != DMX_OK) return rc;
+    File fo(out_path, "wb");
+    if (!fo.f) return DMX_ERR_ARG;
+    // stream the output back: the D2H of chunk k + 1 overlaps the file write of chunk k
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    for (auto& e : ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = DMX_ERR_DEVICE;
+    uint8_t* hb[2] = {hb0.u8(), hb1.u8()};
+    const size_t nch = (tot + K - 1) / K;
+    auto d2h = [&](size_t k) -> bool {
+        const size_t n = std::min(K, tot - k * K);
+        return hipMemcpyAsync(hb[k & 1], dev + k * K, n, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+               hipEventRecord(ev[k & 1], c->stream) == hipSuccess;
+    };
+    if (rc == DMX_OK && nch && !d2h(0)) rc = DMX_ERR_DEVICE;
+    for (size_t k = 0; k < nch && rc == DMX_OK; k++) {
+        if (hipEventSynchronize(ev[k & 1]) != hipSuccess) { rc = DMX_ERR_DEVICE; break; }
+        if (k + 1 < nch && !d2h(k + 1)) { rc = DMX_ERR_DEVICE; break; }
+        const size_t n = std::min(K, tot - k * K);
+        if (std::fwrite(hb[k & 1], 1, n, fo.f) != n) rc = DMX_ERR_ARG;
+    }
+    (void)hipStreamSynchronize(c->stream);
+    for (auto& e : ev)
+        if (e) (void)hipEventDestroy(e);
+    if (out_bytes && rc == DMX_OK) *out_bytes = tot;
+    return rc;
+}
+
 void dmx_free(void* p) { std::free(p); }
 
 const char* dmx_strerror(int code) {
@@ -694,6 +1154,7 @@ const char* dmx_strerror(int code) {
         case DMX_ERR_OVERREAD: return "Reading bits beyond the alloted buffer size!";
         case DMX_ERR_CAPACITY: return "output buffer too small";
         case DMX_ERR_INTERNAL: return "internal error";
+        case DMX_ERR_CHECKSUM: return "container checksum or length mismatch";
         default: return "unknown error";
     }
 }

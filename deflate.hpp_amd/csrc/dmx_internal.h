@@ -127,6 +127,14 @@ hipError_t launch_fb_resolve(const uint8_t* stream, const uint64_t* starts, cons
                              const uint64_t* tokoff, const uint32_t* tok, const FbUnit* units,
                              uint16_t* img, uint64_t total, uint8_t* out, uint32_t* err,
                              hipStream_t st);
+// checksums (checksum.hip): scratch of checksum_scratch_bytes(n) bytes; results land in device
+// memory (*d_out).  CRC-32: the zero-start register; crc32_finish applies start value and xor.
+uint64_t checksum_scratch_bytes(uint64_t n);
+hipError_t launch_adler32(const uint8_t* d, uint64_t n, uint32_t init, void* scratch, uint32_t* d_out,
+                          hipStream_t st);
+hipError_t launch_crc32_raw(const uint8_t* d, uint64_t n, void* scratch, uint32_t* d_out, hipStream_t st);
+uint32_t crc32_finish(uint32_t raw, uint64_t n, uint32_t init);
+
 hipError_t launch_inflate_serial(const InflateArgs& A, int count_only, InflateResult* res,
                                  hipStream_t st);
 

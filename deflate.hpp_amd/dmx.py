@@ -20,7 +20,9 @@ DMX_ERR_DEVICE = -3
 DMX_ERR_DATA = -4
 DMX_ERR_OVERREAD = -5
 DMX_ERR_CAPACITY = -6
+DMX_ERR_CHECKSUM = -8
 DMX_CFG_RFC_STRICT = 1
+DMX_VERIFY = 1
 DMX_DEFLATE_NOT_FINAL = 1
 
 CORPUS = {"zeros": 0, "repeat": 1, "random": 2, "text": 3, "mixed": 4, "bmp": 5}
@@ -30,7 +32,9 @@ EXPORTS = [
     "dmx_config_default", "dmx_create", "dmx_destroy", "dmx_default_ctx", "dmx_deflate_bound",
     "dmx_deflate", "dmx_inflate", "dmx_inflate_alloc", "dmx_free", "dmx_strerror",
     "dmx_deflate_device", "dmx_inflate_device", "dmx_set_timing", "dmx_last_stats",
-    "dmx_corpus_generate",
+    "dmx_corpus_generate", "dmx_adler32_device", "dmx_crc32_device", "dmx_adler32", "dmx_crc32",
+    "dmx_framed_bound", "dmx_deflate_zlib", "dmx_deflate_gzip", "dmx_inflate_zlib", "dmx_inflate_gzip",
+    "dmx_deflate_file", "dmx_inflate_file", "dmx_segment_starts_device",
 ]
 
 
@@ -86,6 +90,21 @@ def lib():
     L.dmx_set_timing.argtypes = [vp, ctypes.c_int]
     L.dmx_last_stats.argtypes = [vp, ctypes.POINTER(Stats)]
     L.dmx_corpus_generate.argtypes = [ctypes.c_int, ctypes.c_uint64, sz, vp]
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    for f in ("dmx_adler32_device", "dmx_crc32_device"):
+        getattr(L, f).argtypes = [vp, vp, sz, ctypes.c_uint32, u32p, vp]
+    for f in ("dmx_adler32", "dmx_crc32"):
+        getattr(L, f).argtypes = [vp, vp, sz, ctypes.c_uint32, u32p]
+    L.dmx_deflate_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(sz),
+                                   ctypes.POINTER(sz)]
+    L.dmx_inflate_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(sz)]
+    L.dmx_segment_starts_device.argtypes = [vp, vp, sz, ctypes.POINTER(ctypes.c_uint64), sz, ctypes.POINTER(sz), vp]
+    L.dmx_framed_bound.argtypes = [sz]
+    L.dmx_framed_bound.restype = sz
+    for f in ("dmx_deflate_zlib", "dmx_deflate_gzip"):
+        getattr(L, f).argtypes = [vp, vp, sz, ctypes.c_int, vp, sz, ctypes.POINTER(sz)]
+    for f in ("dmx_inflate_zlib", "dmx_inflate_gzip"):
+        getattr(L, f).argtypes = [vp, vp, sz, ctypes.c_uint32, ctypes.POINTER(u8p), ctypes.POINTER(sz)]
     _lib = L
     return L
 
@@ -177,6 +196,81 @@ class Context:
             raise DmxError(DMX_ERR_OVERREAD, "inflate_zlib")
         return self.decompress(data[2:])
 
+    # ---- file-path overloads (streaming, deflate.hpp:755-777 / inflate.hpp:390-408) ------
+    def compress_file(self, in_path, out_path, level=2):
+        """deflate::compress(std::string, std::string, int); returns (input, output) sizes."""
+        a, b = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(lib().dmx_deflate_file(self.h, os.fsencode(in_path), os.fsencode(out_path), level,
+                                      ctypes.byref(a), ctypes.byref(b)), "deflate_file")
+        return a.value, b.value
+
+    def decompress_file(self, in_path, out_path):
+        """inflate::decompress(std::string, std::string); returns the decoded size."""
+        n = ctypes.c_size_t()
+        _check(lib().dmx_inflate_file(self.h, os.fsencode(in_path), os.fsencode(out_path), ctypes.byref(n)),
+               "inflate_file")
+        return n.value
+
+    # ---- containers and checksums (SURVEY 8(f) row 4; extensions, not in the reference) -----
+    def _framed(self, fn, data, level):
+        data = bytes(data)
+        cap = lib().dmx_framed_bound(len(data))
+        out = ctypes.create_string_buffer(max(1, cap))
+        n = ctypes.c_size_t()
+        _check(getattr(lib(), fn)(self.h, data, len(data), level, out, cap, ctypes.byref(n)), fn)
+        return out.raw[: n.value]
+
+    def compress_zlib(self, data, level=2):
+        """RFC 1950 zlib stream (Adler-32 computed on the GPU)."""
+        return self._framed("dmx_deflate_zlib", data, level)
+
+    def compress_gzip(self, data, level=2):
+        """RFC 1952 gzip member (CRC-32 computed on the GPU)."""
+        return self._framed("dmx_deflate_gzip", data, level)
+
+    def _unframed(self, fn, data, verify):
+        data = bytes(data)
+        p = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t()
+        _check(getattr(lib(), fn)(self.h, data, len(data), DMX_VERIFY if verify else 0, ctypes.byref(p),
+                                  ctypes.byref(n)), fn)
+        try:
+            return ctypes.string_at(p, n.value)
+        finally:
+            lib().dmx_free(p)
+
+    def inflate_zlib(self, data, verify=True):
+        """zlib stream -> bytes; header checked, Adler-32 verified on the GPU (DMX_ERR_CHECKSUM)."""
+        return self._unframed("dmx_inflate_zlib", data, verify)
+
+    def inflate_gzip(self, data, verify=True):
+        """gzip member -> bytes; CRC-32 and ISIZE verified on the GPU."""
+        return self._unframed("dmx_inflate_gzip", data, verify)
+
+    def _ck(self, fn, data, init):
+        data = bytes(data)
+        v = ctypes.c_uint32()
+        _check(getattr(lib(), fn)(self.h, data, len(data), init, ctypes.byref(v)), fn)
+        return v.value
+
+    def adler32(self, data, init=1):
+        return self._ck("dmx_adler32", data, init)
+
+    def crc32(self, data, init=0):
+        return self._ck("dmx_crc32", data, init)
+
+    def adler32_device(self, d, n, init=1, stream=None):
+        v = ctypes.c_uint32()
+        _check(lib().dmx_adler32_device(self.h, ctypes.c_void_p(d), n, init, ctypes.byref(v),
+                                        ctypes.c_void_p(stream) if stream else None), "adler32_device")
+        return v.value
+
+    def crc32_device(self, d, n, init=0, stream=None):
+        v = ctypes.c_uint32()
+        _check(lib().dmx_crc32_device(self.h, ctypes.c_void_p(d), n, init, ctypes.byref(v),
+                                      ctypes.c_void_p(stream) if stream else None), "crc32_device")
+        return v.value
+
     # ---- device-resident API --------------------------------------------------------------
     def deflate_device(self, d_in, n, level, d_out, cap, stream=None, not_final=False):
         out_len = ctypes.c_size_t()
@@ -193,6 +287,17 @@ class Context:
                                       ctypes.byref(out_len), ctypes.c_void_p(stream) if stream else None)
         _check(rc, "inflate_device")
         return out_len.value
+
+    def segment_starts_device(self, d_in, n, stream=None):
+        """Candidate segment starts (bytes after each 00 00 FF FF) of a device-resident stream."""
+        cnt = ctypes.c_size_t()
+        sp = ctypes.c_void_p(stream) if stream else None
+        _check(lib().dmx_segment_starts_device(self.h, ctypes.c_void_p(d_in), n, None, 0, ctypes.byref(cnt), sp),
+               "segment_starts")
+        buf = (ctypes.c_uint64 * max(1, cnt.value))()
+        _check(lib().dmx_segment_starts_device(self.h, ctypes.c_void_p(d_in), n, buf, cnt.value, ctypes.byref(cnt),
+                                               sp), "segment_starts")
+        return list(buf[: cnt.value])
 
     def set_timing(self, on=True):
         _check(lib().dmx_set_timing(self.h, 1 if on else 0), "set_timing")

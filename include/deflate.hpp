@@ -12,8 +12,6 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
-#include <fstream>
-#include <iterator>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -33,14 +31,12 @@ class deflate {
     }
 
     // deflate::compress(std::string, std::string, int)  -- reference deflate.hpp:755-777.
-    // Reads the whole file, writes the stream; returns 0 as the reference does (its out_size
-    // is never updated, deflate.hpp:760, 776).
+    // Streams the file through the GPU in 64 MiB chunks (dmx_deflate_file); returns 0 as the
+    // reference does (its out_size is never updated, deflate.hpp:760, 776).
     static size_t compress(std::string file_path, std::string new_file, int compression_level) {
-        std::ifstream f(file_path, std::ios::binary);
-        std::vector<uint8_t> in((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-        std::vector<uint8_t> out = run(in.data(), in.size(), compression_level);
-        std::ofstream o(new_file, std::ios::binary);
-        o.write(reinterpret_cast<const char*>(out.data()), (std::streamsize)out.size());
+        int rc = dmx_deflate_file(dmx_default_ctx(), file_path.c_str(), new_file.c_str(), compression_level,
+                                  nullptr, nullptr);
+        if (rc != DMX_OK) throw std::runtime_error(dmx_strerror(rc));
         return 0;
     }
 

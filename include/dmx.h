@@ -31,6 +31,7 @@ extern "C" {
                                  (inflate.hpp:81-82, 97-99, 106-108)                          */
 #define DMX_ERR_CAPACITY (-6) /* caller's output buffer too small (device API only)           */
 #define DMX_ERR_INTERNAL (-7)
+#define DMX_ERR_CHECKSUM (-8) /* zlib Adler-32 / gzip CRC-32 or ISIZE mismatch (DMX_VERIFY)      */
 
 /* ---- context --------------------------------------------------------------------------- */
 typedef struct dmx_ctx dmx_ctx;
@@ -81,6 +82,19 @@ int dmx_inflate(dmx_ctx* ctx, const uint8_t* in, size_t n, uint8_t* out, size_t 
 int dmx_inflate_alloc(dmx_ctx* ctx, const uint8_t* in, size_t n, uint8_t** out, size_t* len);
 
 void dmx_free(void* p);
+
+/* Replaces deflate::compress(std::string, std::string, int)      deflate.hpp:755-777
+ *          inflate::decompress(std::string, std::string)          inflate.hpp:390-408
+ * Streaming file I/O: 64 MiB chunks through two pinned buffers; a reader thread overlaps the
+ * disk reads with the H2D copies, and (deflate) the H2D of chunk k + 1 with the compression of
+ * chunk k (each chunk a NOT_FINAL shard, the last one final; the concatenation is one stream).
+ * Inflate streams the compressed file into HBM, decodes it as one stream, and overlaps the
+ * D2H of each output chunk with the file write of the previous one.  Unlike the reference
+ * (correct only for files <= 32 KiB, SURVEY A-8) any size works.  Sizes are reported through
+ * the optional out-parameters. */
+int dmx_deflate_file(dmx_ctx* ctx, const char* in_path, const char* out_path, int level,
+                     size_t* in_bytes, size_t* out_bytes);
+int dmx_inflate_file(dmx_ctx* ctx, const char* in_path, const char* out_path, size_t* out_bytes);
 const char* dmx_strerror(int code);
 
 /* ---- device-resident API (HBM in, HBM out; used by bench.py and multi-GPU sharding) ------ */
@@ -98,6 +112,44 @@ int dmx_deflate_device(dmx_ctx* ctx, const void* d_in, size_t n, int level, uint
  * the decoded stream does not fit in cap. */
 int dmx_inflate_device(dmx_ctx* ctx, const void* d_in, size_t n, void* d_out, size_t cap,
                        size_t* out_len, void* stream);
+
+/* Byte offsets just past every "00 00 FF FF" (empty stored block) in a device-resident stream:
+ * the candidate segment starts of libdmx's layout, in order (at most cap written, *count = all).
+ * Multi-GPU inflate splits a stream at these (deflate.hpp_amd/shard.py scatter_inflate); a
+ * false candidate inside stored data makes the piece before it fail to decode, and the caller
+ * then decodes the stream whole. */
+int dmx_segment_starts_device(dmx_ctx* ctx, const void* d_in, size_t n, uint64_t* starts, size_t cap,
+                              size_t* count, void* stream);
+
+/* ---- checksums and containers (not in the reference) -------------------
+ * The reference's decompressZlib (inflate.hpp:326-361) skips the 2-byte header and ignores the
+ * Adler-32 (SURVEY A-9); inflate.hpp's decompressZlib keeps exactly that.  These entry points
+ * add what a zlib/gzip user needs on top: framing on the deflate side and a verified inflate,
+ * with Adler-32 / CRC-32 computed block-parallel on the GPU (checksum.hip). */
+
+/* zlib's adler32(init, buf, n) / crc32(init, buf, n) of a device buffer (init 1 / 0 to start). */
+int dmx_adler32_device(dmx_ctx* ctx, const void* d, size_t n, uint32_t init, uint32_t* out, void* stream);
+int dmx_crc32_device(dmx_ctx* ctx, const void* d, size_t n, uint32_t init, uint32_t* out, void* stream);
+/* the same for a host buffer (copied to the device first) */
+int dmx_adler32(dmx_ctx* ctx, const uint8_t* in, size_t n, uint32_t init, uint32_t* out);
+int dmx_crc32(dmx_ctx* ctx, const uint8_t* in, size_t n, uint32_t init, uint32_t* out);
+
+/* Upper bound of a zlib- or gzip-framed stream for n input bytes. */
+size_t dmx_framed_bound(size_t n);
+/* RFC 1950 zlib stream (CMF 0x78, FLEVEL from the level, Adler-32 trailer) / RFC 1952 gzip
+ * member (no name, MTIME 0, OS 255, CRC-32 + ISIZE trailer) around dmx_deflate's raw stream. */
+int dmx_deflate_zlib(dmx_ctx* ctx, const uint8_t* in, size_t n, int level, uint8_t* out, size_t cap,
+                     size_t* out_len);
+int dmx_deflate_gzip(dmx_ctx* ctx, const uint8_t* in, size_t n, int level, uint8_t* out, size_t cap,
+                     size_t* out_len);
+
+/* Check the container trailer against the decoded bytes (DMX_ERR_CHECKSUM on mismatch). */
+#define DMX_VERIFY 1u
+/* Inflate of a zlib stream (header checked; preset dictionaries are DMX_ERR_DATA) / a
+ * single-member gzip stream (FEXTRA, FNAME, FCOMMENT, FHCRC skipped); the trailer is the last
+ * 4 / 8 input bytes.  *out is allocated by the library (dmx_free). */
+int dmx_inflate_zlib(dmx_ctx* ctx, const uint8_t* in, size_t n, uint32_t flags, uint8_t** out, size_t* len);
+int dmx_inflate_gzip(dmx_ctx* ctx, const uint8_t* in, size_t n, uint32_t flags, uint8_t** out, size_t* len);
 
 /* ---- instrumentation -------------------------------------------------------------------- */
 typedef struct dmx_stats {

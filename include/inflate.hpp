@@ -11,8 +11,6 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
-#include <fstream>
-#include <iterator>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -40,15 +38,13 @@ class inflate {
     static std::vector<uint8_t> decompress(std::vector<uint8_t> in) { return run(in.data(), in.size()); }
 
     // inflate::decompress(std::string, std::string)  -- reference inflate.hpp:390-408.
-    // Whole-file decode; returns the decoded size (the reference's running total equals this
-    // for the single-Huffman-block files it handles, SURVEY A-8).
+    // Streaming file decode (dmx_inflate_file); returns the decoded size (the reference's
+    // running total equals this for the single-Huffman-block files it handles, SURVEY A-8).
     static size_t decompress(std::string file_path, std::string new_file) {
-        std::ifstream f(file_path, std::ios::binary);
-        std::vector<uint8_t> in((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-        std::vector<uint8_t> out = run(in.data(), in.size());
-        std::ofstream o(new_file, std::ios::binary);
-        o.write(reinterpret_cast<const char*>(out.data()), (std::streamsize)out.size());
-        return out.size();
+        size_t n = 0;
+        int rc = dmx_inflate_file(dmx_default_ctx(), file_path.c_str(), new_file.c_str(), &n);
+        if (rc != DMX_OK) throw std::runtime_error(dmx_strerror(rc));
+        return n;
     }
 
     // inflate::decompressZlib(void*, size_t, void*, size_t)  -- reference inflate.hpp:326-335.

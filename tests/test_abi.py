@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     hdr = open(os.path.join(ROOT, "include", "dmx.h")).read()
-    return sorted(set(re.findall(r"\b(dmx_[a-z_]+)\s*\(", hdr)))
+    return sorted(set(re.findall(r"\b(dmx_[a-z0-9_]+)\s*\(", hdr)))
 
 
 def test_every_declared_symbol_is_exported():

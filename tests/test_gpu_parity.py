@@ -239,3 +239,20 @@ def test_dropin_cpp_program():
         subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "cpp")], check=True)
     r = subprocess.run([exe, GOLD, "/tmp"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
+
+
+def test_segment_starts_device_index(ctx):
+    """dmx_segment_starts_device (multi-GPU inflate split points) lists the byte
+    after every 00 00 FF FF, as a plain byte search does, at any alignment."""
+    import torch
+    d = dmx.corpus("mixed", 3 << 20, offset=77)
+    s = ctx.compress(d, 2)
+    want, i = [], s.find(b"\x00\x00\xff\xff")
+    while i >= 0:
+        want.append(i + 4)
+        i = s.find(b"\x00\x00\xff\xff", i + 1)
+    assert len(want) >= 90
+    t = torch.frombuffer(bytearray(b"\x01\x02\x03" + s), dtype=torch.uint8).cuda()
+    for off in (0, 1, 3):
+        got = ctx.segment_starts_device(t.data_ptr() + 3 - off, len(s) + off)
+        assert got == [w + off for w in want], off
