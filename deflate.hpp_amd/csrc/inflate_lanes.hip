@@ -39,9 +39,18 @@
 
 namespace dmx {
 
-constexpr uint32_t LN_REGION = 1280;
+// LDS of one workgroup (one wavefront, LN_LANES segments): per segment a region of
+//     [   0, 1024)  lit/len lookup table, 512 x u16, indexed by the next 9 stream bits
+//                   (while the header is decoded: the code lengths, one byte per symbol, at
+//                   [LN_LENS, 1024): lit/len 0..287, distance 288..319)
+//     [1024, 1152)  distance lookup table, 64 x u16 (while the precode table of this segment
+//                   is built: its symbols in canonical order)
+// and a shared area of LN_LANES x 128 B: each segment's precode table (128 x u8) while the
+// headers are decoded, then the canonical symbol order of the table being built.
+constexpr uint32_t LN_REGION = 1152;
 constexpr uint32_t LN_DIST = 1024;
-constexpr uint32_t LN_PRE = 1152;
+constexpr uint32_t LN_LENS = 704;
+constexpr uint32_t LN_PRE_BYTES = 128;
 constexpr uint32_t LN_OUT_CAP = 32768;
 #ifndef DMX_LN_LANES
 #define DMX_LN_LANES 16
@@ -69,45 +78,119 @@ __device__ __forceinline__ uint32_t ln_lit_entry(uint32_t s, uint32_t l) {
     return (l << 11) | s;
 }
 
+// Canonical decode table of one code, built by the whole wavefront (RFC 1951 3.2.2; the
+// reference builds a bit-trie, FlatHuffmanTree::construct common.hpp:104-145).  lens(s) gives
+// the code length of symbol s < nsym (0 = unused); table[x] for every B-bit index x (the next B
+// stream bits, LSB first) decodes the code that is a prefix of x.  Steps: per-length counts by
+// ballots, canonical first codes, symbols in canonical order into `order`, then each lane fills
+// entries x = lane + 64 k: the code length is the first l with (rev(x) >> (B - l)) below that
+// length's limit (canonical codes are monotone, so the test is a count, no search), the symbol
+// order[base[l] + code].  Returns false unless the code is complete with all lengths <= B.
+template <int B, class Lens, class Order, class Put>
+__device__ __forceinline__ bool ln_coop_table(uint32_t nsym, Lens lens, Order order, Put put) {
+    const uint32_t lane = lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t cnt[B + 1];
+#pragma unroll
+    for (int l = 0; l <= B; l++) cnt[l] = 0;
+    bool bad = false;
+    for (uint32_t c = 0; c < nsym; c += 64) {
+        const uint32_t s = c + lane;
+        const uint32_t L = s < nsym ? lens(s) : 0u;
+        bad |= __ballot(L > (uint32_t)B) != 0;
+#pragma unroll
+        for (int l = 1; l <= B; l++) cnt[l] += (uint32_t)__popcll(__ballot(L == (uint32_t)l));
+    }
+    uint32_t kraft = 0;
+#pragma unroll
+    for (int l = 1; l <= B; l++) kraft += cnt[l] << (B - l);
+    if (bad || kraft != (1u << B)) return false;
+    uint32_t limit[B + 1], base[B + 1], run[B + 1];
+    uint32_t first = 0, off = 0;
+#pragma unroll
+    for (int l = 1; l <= B; l++) {
+        first = (first + cnt[l - 1]) << 1;  // cnt[0] = 0
+        limit[l] = first + cnt[l];
+        base[l] = off - first;  // order index = base + code (mod 2^32)
+        run[l] = off;
+        off += cnt[l];
+    }
+    for (uint32_t c = 0; c < nsym; c += 64) {
+        const uint32_t s = c + lane;
+        const uint32_t L = s < nsym ? lens(s) : 0u;
+#pragma unroll
+        for (int l = 1; l <= B; l++) {
+            const uint64_t b = __ballot(L == (uint32_t)l);
+            if (L == (uint32_t)l) order(run[l] + (uint32_t)__popcll(b & lt), s, 1);
+            run[l] += (uint32_t)__popcll(b);
+        }
+    }
+    wave_sync();
+    static_assert(B >= 6, "one table entry per lane at least");
+#pragma unroll
+    for (uint32_t k = 0; k < (1u << B) / 64; k++) {
+        const uint32_t x = lane + 64 * k;
+        const uint32_t v = bitrev(x, B);
+        uint32_t idx = 0, len = 0;
+#pragma unroll
+        for (int l = B; l >= 1; l--) {
+            const uint32_t p = v >> (B - l);
+            if (p < limit[l]) {
+                idx = base[l] + p;
+                len = (uint32_t)l;
+            }
+        }
+        put(x, order(idx, 0, 0), len);
+    }
+    wave_sync();
+    return true;
+}
+
 __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[LN_LANES * LN_REGION];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LN_LANES * (LN_REGION + LN_PRE_BYTES)];
     const uint32_t lane = threadIdx.x;
     const uint64_t j = (uint64_t)blockIdx.x * LN_LANES + lane;
-    // lanes are independent: no barrier anywhere in this kernel
-    if (lane >= LN_LANES || j >= A.ncand) return;
-    uint8_t* const R = lds + lane * LN_REGION;
-    const uint32_t rot = 4 * lane;  // rotate each lane's region by one bank per lane
-    auto at = [&](uint32_t b) -> uint32_t {
-        const uint32_t x = b + rot;
-        return x >= LN_REGION ? x - LN_REGION : x;
-    };
-    auto lut16 = [&](uint32_t b) -> uint32_t { return *reinterpret_cast<const uint16_t*>(R + at(b)); };
+    // lanes 0 .. LN_LANES-1 decode one segment each; the whole wave builds the tables
+    const bool seg_lane = lane < LN_LANES && j < A.ncand;
+    uint8_t* const R = lds + min(lane, LN_LANES - 1) * LN_REGION;
+    uint8_t* const SH = lds + LN_LANES * LN_REGION;  // shared area
+    uint8_t* const PRE = SH + min(lane, LN_LANES - 1) * LN_PRE_BYTES;
+    auto lut16 = [&](uint32_t b) -> uint32_t { return *reinterpret_cast<const uint16_t*>(R + b); };
+
+    // code-length bytes of every segment start at zero (zero runs are then just skipped)
+    for (uint32_t i = lane; i < LN_LANES * (1024 - LN_LENS) / 4; i += 64) {
+        const uint32_t sgm = i / ((1024 - LN_LENS) / 4), w = i % ((1024 - LN_LENS) / 4);
+        reinterpret_cast<uint32_t*>(lds + sgm * LN_REGION + LN_LENS)[w] = 0u;
+    }
+    wave_sync();
 
     const uintptr_t base4 = reinterpret_cast<uintptr_t>(A.in_words);
     const uintptr_t base16 = base4 & ~(uintptr_t)15;
     const uint64_t off0 = (uint64_t)(base4 - base16) + A.misalign;  // stream byte 0
     LaneIn br;
-    const uint64_t start = A.cands[j];
+    const uint64_t start = seg_lane ? A.cands[j] : 0;
     uint64_t cb = (off0 + start) & ~(uint64_t)15;  // stream byte of relative position 0
     if (cb >= 16 && cb >= off0 + A.n) cb -= 16;  // a candidate at the stream end: keep a quad in bounds
     br.blk = (GUint4*)(base16 + cb);
     br.E = (uint32_t)min(off0 + A.n - cb, (uint64_t)1 << 26);
     br.nblk = (br.E + 15) / 16;
-    uint64_t* const dbg = A.dbg ? A.dbg + j * kPhaseSlots : nullptr;  // DMX_PHASES developer aid
+    uint64_t* const dbg = (A.dbg && seg_lane) ? A.dbg + j * kPhaseSlots : nullptr;  // DMX_PHASES aid
     uint32_t n_iter = 0, n_top = 0;
     if (dbg) dbg[0] = __builtin_amdgcn_s_memtime();
-    br.seek((uint32_t)(off0 + start - cb));
-
-    uint32_t flags = 0, outpos = 0;
+    uint32_t flags = seg_lane ? 0u : SEGF_EXOTIC;
+    uint32_t outpos = 0;
     bool fin = false;
     uint64_t end_byte = 0;
+    uint32_t* const tk = seg_lane ? B.tok + B.tokoff[j] : B.tok;
+    const uint32_t tcap = seg_lane ? B.caps[j] : 0u;
+    if (seg_lane) {
+        br.seek((uint32_t)(off0 + start - cb));
+        // consume the loads above now: a later first use would wait with vmcnt(0), draining
+        // the stream prefetch in flight at that point
+        if (tcap == 0 || (reinterpret_cast<uintptr_t>(tk) & 15)) flags |= SEGF_EXOTIC;
+    }
 
     // token output: pending token (merges), 4-word queue, 16-byte stores
-    uint32_t* const tk = B.tok + B.tokoff[j];
-    const uint32_t tcap = B.caps[j];
-    // consume the loads above now: a later first use would wait with vmcnt(0), draining the
-    // stream prefetch in flight at that point
-    if (tcap == 0 || (reinterpret_cast<uintptr_t>(tk) & 15)) flags |= SEGF_EXOTIC;
     uint32_t ntok = 0, qn = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;
     uint32_t pk = 0, pa = 0, pd = 0;  // pending: kind (1 literal run, 2 match), bytes / L, count / d
     auto push = [&](uint32_t w) {
@@ -127,323 +210,273 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
         pk = 0;
     };
 
-    br.ensure(3);
-    const uint32_t bfinal = br.bits(1);
-    const uint32_t btype = br.bits(2);
-    if (btype == 0) {
-        // stored block (libdmx emits these for incompressible segments) or an empty segment
-        br.align();
-        br.ensure(32);
-        const uint32_t len = br.bits(16), nlen = br.bits(16);
-        const uint32_t b0 = br.bitpos() >> 3;  // byte of the data (relative)
-        if (!bfinal && len == 0 && nlen == 0xFFFF) {
-            end_byte = b0 + cb - off0;  // empty segment: the candidate is itself a marker
-        } else if (b0 + len > br.E || len > LN_OUT_CAP) {
-            flags |= SEGF_EXOTIC;
-        } else {
-            push(len);
-            push((uint32_t)(b0 + cb - off0 - start));
-            outpos = len;
-            br.seek(b0 + len);
-            if (bfinal) {
-                fin = true;
-                end_byte = b0 + len + cb - off0;
+    // ---- block header: BFINAL, BTYPE, stored segments, dynamic-header fields ---------------
+    uint32_t bfinal = 0, btype = 0, hlit = 288, hdist = 32;
+    uint64_t pl = 0;  // dynamic: 19 x 3-bit precode lengths, by symbol
+    if (seg_lane && !flags) {
+        br.ensure(3);
+        bfinal = br.bits(1);
+        btype = br.bits(2);
+        if (btype == 0) {
+            // stored block (libdmx emits these for incompressible segments) or an empty segment
+            br.align();
+            br.ensure(32);
+            const uint32_t len = br.bits(16), nlen = br.bits(16);
+            const uint32_t b0 = br.bitpos() >> 3;  // byte of the data (relative)
+            if (!bfinal && len == 0 && nlen == 0xFFFF) {
+                end_byte = b0 + cb - off0;  // empty segment: the candidate is itself a marker
+            } else if (b0 + len > br.E || len > LN_OUT_CAP) {
+                flags |= SEGF_EXOTIC;
             } else {
-                br.ensure(3);
-                const uint32_t f2 = br.bits(1), t2 = br.bits(2);
-                br.align();
-                br.ensure(32);
-                const uint32_t l2 = br.bits(16), n2 = br.bits(16);
-                if (f2 || t2 != 0 || l2 != 0 || n2 != 0xFFFF) flags |= SEGF_EXOTIC;
-                end_byte = (br.bitpos() >> 3) + cb - off0;
+                push(len);
+                push((uint32_t)(b0 + cb - off0 - start));
+                outpos = len;
+                br.seek(b0 + len);
+                if (bfinal) {
+                    fin = true;
+                    end_byte = b0 + len + cb - off0;
+                } else {
+                    br.ensure(3);
+                    const uint32_t f2 = br.bits(1), t2 = br.bits(2);
+                    br.align();
+                    br.ensure(32);
+                    const uint32_t l2 = br.bits(16), n2 = br.bits(16);
+                    if (f2 || t2 != 0 || l2 != 0 || n2 != 0xFFFF) flags |= SEGF_EXOTIC;
+                    end_byte = (br.bitpos() >> 3) + cb - off0;
+                }
             }
-        }
-    } else if (btype == 3) {
-        flags |= SEGF_EXOTIC;  // reference: empty block, then more blocks -- not this layout
-    } else {
-        // ---- code lengths: counts per length (pass 1) ---------------------------------------
-        uint32_t hlit = 288, hdist = 32, lmaxl = 9, lmaxd = 5;
-        uint64_t lc0 = 0, lc1 = 0, dcn = 0;  // lit counts: l 1..6 / 7..9 in 10-bit fields; dist 8-bit
-        LaneIn saved;
-        if (btype == 1) {  // fixed code (RFC 1951 3.2.6): 24 x 7, 152 x 8, 112 x 9; 32 x 5
-            lc1 = 24ull | (152ull << 10) | (112ull << 20);
-            dcn = 32ull << (8 * 4);
-        } else {
+        } else if (btype == 3) {
+            flags |= SEGF_EXOTIC;  // reference: empty block, then more blocks -- not this layout
+        } else if (btype == 2) {
             br.ensure(14);
             hlit = br.bits(5) + 257;
             hdist = br.bits(5) + 1;
             const uint32_t hclen = br.bits(4) + 4;
-            uint64_t pl = 0;  // 19 x 3-bit precode lengths, by symbol
             for (uint32_t i = 0; i < hclen; i++) {
                 br.ensure(3);
                 pl |= (uint64_t)br.bits(3) << (3 * kLnPerm[i]);
             }
             if (hlit > 286 || hdist > 30) flags |= SEGF_EXOTIC;
-            // precode: counts (5-bit fields), completeness, next codes (8-bit fields)
-            uint64_t pc = 0;
-            for (uint32_t s = 0; s < 19; s++) {
-                const uint32_t l = (uint32_t)(pl >> (3 * s)) & 7;
-                if (l) pc += 1ull << (5 * l);
-            }
-            uint32_t kr = 0, code = 0;
-            uint64_t pn = 0;
-            for (uint32_t l = 1; l <= 7; l++) {
-                const uint32_t c = (uint32_t)(pc >> (5 * l)) & 31;
-                kr += c << (7 - l);
-                code = (code + ((uint32_t)(pc >> (5 * (l - 1))) & 31) * (l > 1)) << 1;
-                pn |= (uint64_t)code << (8 * l);
-            }
-            if (kr != 128) flags |= SEGF_EXOTIC;
-            // precode table fill, one entry (or one symbol) per iteration
-            {
-                uint32_t s = 0, frem = 0, fp = 0, fst = 0, fe = 0;
-                while (!flags && (s < 19 || frem)) {
-                    if (frem) {
-                        R[at(LN_PRE + fp)] = (uint8_t)fe;
-                        fp += fst;
-                        frem--;
-                    } else {
-                        const uint32_t l = (uint32_t)(pl >> (3 * s)) & 7;
-                        if (l) {
-                            const uint32_t c = (uint32_t)(pn >> (8 * l)) & 255;
-                            pn += 1ull << (8 * l);
-                            fp = bitrev(c, l);
-                            fst = 1u << l;
-                            frem = 128u >> l;
-                            fe = s | (l << 5);
-                        }
-                        s++;
-                    }
-                }
-            }
-            saved = br;
-            // pass 1: decode the code-length sequence, count lengths, reject quirks
-            uint32_t i = 0, prev = 0, lm = 0, dm = 0;
-            bool prevok = false;
-            const uint32_t total = hlit + hdist;
-            while (!flags && i < total) {
-                if (__any(br.low())) br.topup();
-                br.ensure(14);
-                const uint32_t e = R[at(LN_PRE + (uint32_t)(br.bb & 127))];
-                br.consume(e >> 5);
-                const uint32_t sym = e & 31;
-                uint32_t val = 0, run = 1;
-                if (sym < 16) {
-                    val = sym;
-                    prev = sym;
-                    prevok = true;
-                } else if (sym == 16) {
-                    if (!prevok || i == hlit) flags |= SEGF_EXOTIC;  // A-12 / sequence-start repeat
-                    val = prev;
-                    run = 3 + br.bits(2);
-                } else if (sym == 17) {
-                    run = 3 + br.bits(3);
-                    prevok = false;
-                } else {
-                    run = 11 + br.bits(7);
-                    prevok = false;
-                }
-                if ((i < hlit && i + run > hlit) || i + run > total) flags |= SEGF_EXOTIC;  // A-11
-                if (val) {
-                    if (i < hlit) {
-                        if (val > 9) flags |= SEGF_EXOTIC;
-                        else if (val <= 6) lc0 += (uint64_t)run << (10 * (val - 1));
-                        else lc1 += (uint64_t)run << (10 * (val - 7));
-                        lm = max(lm, val);
-                    } else {
-                        if (val > 6) flags |= SEGF_EXOTIC;
-                        else dcn += (uint64_t)run << (8 * (val - 1));
-                        dm = max(dm, val);
-                    }
-                }
-                i += run;
-            }
-            lmaxl = lm;
-            lmaxd = dm;
         }
-        if (dbg) dbg[1] = __builtin_amdgcn_s_memtime();
-        // ---- completeness (both codes must fill their table exactly) and next codes --------
-        uint64_t nl0 = 0, nl1 = 0, nd = 0;  // next code per length (10-bit / 8-bit fields)
-        if (!flags) {
-            uint32_t kl = 0, kd = 0, code = 0, prevc = 0;
-            for (uint32_t l = 1; l <= 9; l++) {
-                const uint32_t c = (uint32_t)((l <= 6 ? lc0 >> (10 * (l - 1)) : lc1 >> (10 * (l - 7))) & 1023);
-                kl += c << (9 - l);
-                code = (code + prevc) << 1;
-                prevc = c;
-                if (l <= 6) nl0 |= (uint64_t)code << (10 * (l - 1));
-                else nl1 |= (uint64_t)code << (10 * (l - 7));
+    }
+    const bool huff = seg_lane && !flags && (btype == 1 || btype == 2);
+    const uint32_t dyn_mask = (uint32_t)__ballot(huff && btype == 2);
+    // ---- precode tables of the dynamic segments, built by the wave (7-bit, u8 entries) -------
+    uint32_t bad_mask = 0;
+    for (uint32_t m = dyn_mask; m; m &= m - 1) {
+        const uint32_t s = (uint32_t)__builtin_ctz(m);
+        const uint64_t pls = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(pl >> 32), s) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pl, s);
+        uint8_t* const ord = lds + s * LN_REGION + LN_DIST;  // canonical order scratch
+        uint8_t* const tab = SH + s * LN_PRE_BYTES;
+        const bool ok = ln_coop_table<7>(
+            19u, [&](uint32_t sym) { return (uint32_t)(pls >> (3 * sym)) & 7u; },
+            [&](uint32_t i, uint32_t sym, int wr) -> uint32_t {
+                if (wr) { ord[i] = (uint8_t)sym; return 0u; }
+                return ord[i];
+            },
+            [&](uint32_t x, uint32_t sym, uint32_t len) { tab[x] = (uint8_t)(sym | (len << 5)); });
+        if (!ok) bad_mask |= 1u << s;
+    }
+    if (seg_lane && ((bad_mask >> lane) & 1u)) flags |= SEGF_EXOTIC;
+    if (dbg) dbg[1] = __builtin_amdgcn_s_memtime();
+
+    // ---- code lengths of the dynamic segments, decoded once into bytes (lane-serial) ------------
+    if (seg_lane && !flags && btype == 2) {
+        uint8_t* const LL = R + LN_LENS;  // lit/len lengths [0, 288), distance [288, 320)
+        uint32_t i = 0, prev = 0;
+        bool prevok = false;
+        const uint32_t total = hlit + hdist;
+        while (!flags && i < total) {
+            if (__any(br.low())) br.topup();
+            br.ensure(14);
+            const uint32_t e = PRE[(uint32_t)(br.bb & 127)];
+            br.consume(e >> 5);
+            const uint32_t sym = e & 31;
+            uint32_t val = 0, run = 1;
+            if (sym < 16) {
+                val = sym;
+                prev = sym;
+                prevok = true;
+            } else if (sym == 16) {
+                if (!prevok || i == hlit) flags |= SEGF_EXOTIC;  // A-12 / sequence-start repeat
+                val = prev;
+                run = 3 + br.bits(2);
+            } else if (sym == 17) {
+                run = 3 + br.bits(3);
+                prevok = false;
+            } else {
+                run = 11 + br.bits(7);
+                prevok = false;
             }
-            code = 0;
-            prevc = 0;
-            for (uint32_t l = 1; l <= 6; l++) {
-                const uint32_t c = (uint32_t)(dcn >> (8 * (l - 1))) & 255;
-                kd += c << (6 - l);
-                code = (code + prevc) << 1;
-                prevc = c;
-                nd |= (uint64_t)code << (8 * (l - 1));
+            if ((i < hlit && i + run > hlit) || i + run > total) flags |= SEGF_EXOTIC;  // A-11
+            if (val && !flags) {
+                if (val > (i < hlit ? 9u : 6u)) flags |= SEGF_EXOTIC;  // beyond the lane tables
+                const uint32_t at = i < hlit ? i : 288 + (i - hlit);
+                for (uint32_t r = 0; r < run; r++) LL[at + r] = (uint8_t)val;
             }
-            if (kl != 512 || kd != 64 || lmaxl == 0 || lmaxd == 0) flags |= SEGF_EXOTIC;
+            i += run;
         }
-        // ---- pass 2: re-decode the lengths (or walk the fixed runs) and fill the tables ----
-        if (!flags) {
-            if (btype == 2) br = saved;
-            const uint32_t total = hlit + hdist;
-            uint32_t i = 0, runrem = 0, runval = 0, fk = 0, prev = 0;
-            uint32_t frem = 0, fp = 0, fst = 0, fe = 0, fb = 0;
-            while (i < total || frem) {
-                if (__any(br.low())) br.topup();
-                if (frem) {
-                    *reinterpret_cast<uint16_t*>(R + at(fb + 2 * fp)) = (uint16_t)fe;
-                    fp += fst;
-                    frem--;
-                } else if (runrem) {
-                    const uint32_t s = i++;
-                    runrem--;
-                    const uint32_t l = runval;
-                    if (l) {
-                        fst = 1u << l;
-                        if (s < hlit) {
-                            const bool lo = l <= 6;
-                            const uint32_t sh = 10 * (lo ? l - 1 : l - 7);
-                            const uint32_t c = (uint32_t)((lo ? nl0 : nl1) >> sh) & 1023;
-                            nl0 += lo ? 1ull << sh : 0ull;
-                            nl1 += lo ? 0ull : 1ull << sh;
-                            fp = bitrev(c, l);
-                            frem = (1u << lmaxl) >> l;
-                            fe = ln_lit_entry(s, l);
-                            fb = 0;
-                        } else {
-                            const uint32_t sh = 8 * (l - 1);
-                            const uint32_t c = (uint32_t)(nd >> sh) & 255;
-                            nd += 1ull << sh;
-                            fp = bitrev(c, l);
-                            frem = (1u << lmaxd) >> l;
-                            fe = 0x8000u | (l << 8) | (s - hlit);
-                            fb = LN_DIST;
-                        }
-                    }
-                } else if (btype == 1) {  // fixed: (8 x 144) (9 x 112) (7 x 24) (8 x 8) (5 x 32)
-                    runval = (0x58798u >> (4 * fk)) & 15;
-                    runrem = (uint32_t)(0x2008187090ull >> (8 * fk)) & 255;
-                    fk++;
-                } else {
-                    br.ensure(14);
-                    const uint32_t e = R[at(LN_PRE + (uint32_t)(br.bb & 127))];
-                    br.consume(e >> 5);
-                    const uint32_t sym = e & 31;
-                    if (sym < 16) {
-                        runval = sym;
-                        prev = sym;
-                        runrem = 1;
-                    } else if (sym == 16) {
-                        runval = prev;
-                        runrem = 3 + br.bits(2);
-                    } else if (sym == 17) {
-                        runval = 0;
-                        runrem = 3 + br.bits(3);
-                    } else {
-                        runval = 0;
-                        runrem = 11 + br.bits(7);
-                    }
-                }
-            }
-        }
-        if (dbg) dbg[2] = __builtin_amdgcn_s_memtime();
+    }
+    if (dbg) dbg[2] = __builtin_amdgcn_s_memtime();
+
+    // ---- lit/len (9-bit) and distance (6-bit) tables, built by the wave ---------------------------
+    const uint32_t huff_mask = (uint32_t)__ballot(huff && !flags);
+    uint16_t* const ORD = reinterpret_cast<uint16_t*>(SH);  // canonical order scratch (<= 288 x u16)
+    bad_mask = 0;
+    for (uint32_t m = huff_mask; m; m &= m - 1) {
+        const uint32_t s = (uint32_t)__builtin_ctz(m);
+        const bool fixed = (dyn_mask >> s & 1u) == 0;
+        const uint8_t* const LL = lds + s * LN_REGION + LN_LENS;
+        uint16_t* const lt = reinterpret_cast<uint16_t*>(lds + s * LN_REGION);
+        uint16_t* const dt = reinterpret_cast<uint16_t*>(lds + s * LN_REGION + LN_DIST);
+        // the lengths are read before the table writes (ln_coop_table: counts and order first)
+        auto ord16 = [&](uint32_t i, uint32_t sym, int wr) -> uint32_t {
+            if (wr) { ORD[i] = (uint16_t)sym; return 0u; }
+            return ORD[i];
+        };
+        bool ok = ln_coop_table<6>(
+            32u, [&](uint32_t sym) { return fixed ? 5u : (uint32_t)LL[288 + sym]; }, ord16,
+            [&](uint32_t x, uint32_t sym, uint32_t len) { dt[x] = (uint16_t)(0x8000u | (len << 8) | sym); });
+        ok = ok && ln_coop_table<9>(
+            288u,
+            [&](uint32_t sym) {
+                return fixed ? (sym < 144 ? 8u : sym < 256 ? 9u : sym < 280 ? 7u : 8u) : (uint32_t)LL[sym];
+            },
+            ord16, [&](uint32_t x, uint32_t sym, uint32_t len) { lt[x] = (uint16_t)ln_lit_entry(sym, len); });
+        if (!ok) bad_mask |= 1u << s;
+    }
+    if (seg_lane && ((bad_mask >> lane) & 1u)) flags |= SEGF_EXOTIC;
+    if (dbg) dbg[3] = __builtin_amdgcn_s_memtime();
+
+    uint32_t endbit = seg_lane ? br.bitpos() : 0u;
+    if (huff && !flags) {
         // ---- tokens until end-of-block -------------------------------------------------------
-        if (!flags) {
-            const uint32_t lmask = (1u << lmaxl) - 1u, dmask = (1u << lmaxd) - 1u;
-            bool going = true;
-            while (going) {
-                if (dbg) n_iter++;
-                if (__any(br.low())) {
-                    br.topup();
-                    if (dbg) n_top++;
-                }
-                if (br.nb < 32) br.refill();
-                const uint32_t e = lut16(2 * (uint32_t)(br.bb & lmask));
-                const uint32_t cl = (e >> 11) & 15;
-                if (e & 0x8000u) {
-                    const uint32_t ex = (e >> 8) & 7;
-                    const uint32_t L = (e & 255) + 3 + ((uint32_t)(br.bb >> cl) & ((1u << ex) - 1u));
-                    br.consume(cl + ex);
-                    if (br.nb < 19) br.refill();
-                    const uint32_t de = lut16(LN_DIST + 2 * (uint32_t)(br.bb & dmask));
-                    const uint32_t dcl = (de >> 8) & 7, ds = de & 31;
-                    const uint32_t dx = dist_extra(ds);
-                    const uint32_t d = dist_base(ds) + ((uint32_t)(br.bb >> dcl) & ((1u << dx) - 1u));
-                    br.consume(dcl + dx);
-                    if (ds >= 30) {
-                        flags |= SEGF_EXOTIC;  // reference: distance symbols 30/31 = distance 0
-                        going = false;
-                    } else if (d > outpos) {
-                        if (j != 0) {
-                            flags |= SEGF_XREF;
-                            going = false;
-                        } else if (br.bitpos() > 8 * br.E) {  // the one branch that does not
-                            flags |= SEGF_EXOTIC;             // advance outpos: bound it here
-                            going = false;
-                        }  // stream start: the reference copies nothing
-                    } else if (outpos + L > LN_OUT_CAP) {
-                        flags |= SEGF_EXOTIC;
-                        going = false;
-                    } else {
-                        if (pk == 2 && pd == d && pa + L <= 0xFFFFu) {
-                            pa += L;
-                        } else {
-                            flushp();
-                            pk = 2;
-                            pa = L;
-                            pd = d;
-                        }
-                        outpos += L;
-                    }
-                } else {
-                    const uint32_t sym = e & 511;
-                    br.consume(cl);
-                    if (sym < 256) {
-                        if (outpos >= LN_OUT_CAP) {
-                            flags |= SEGF_EXOTIC;
-                            going = false;
-                        } else {
-                            if (pk == 1 && pd < 3) {
-                                pa |= sym << (8 * pd);
-                                pd++;
-                            } else {
-                                flushp();
-                                pk = 1;
-                                pa = sym;
-                                pd = 1;
-                            }
-                            outpos++;
-                        }
-                    } else {
-                        if (sym != 256) flags |= SEGF_EXOTIC;  // 286/287: reference length 0
-                        going = false;
-                    }
-                }
-                // over-read is checked after the loop (and in the branch above): every other
-                // iteration advances outpos or ends the loop, so LN_OUT_CAP bounds it
-            }
+        // The stream comes through a ring of 8 quads (128 B) per lane in the shared LDS area:
+        // each step reads the 64 bits at the bit position (two ds_read_b64 + funnel shifts), so
+        // every symbol -- a literal, or a length and distance with their extra bits (<= 33
+        // bits) -- decodes from one window with no refill branch.  Every LN_PERIOD steps the
+        // lane loads the next quad of its stream into a staging register and writes the quad
+        // staged two periods earlier into the ring (loads complete off the critical path); a
+        // quad goes into the ring only once the one it replaces is consumed.  LN_PERIOD steps
+        // consume <= 99 bits < one quad, so the ring stays >= 5 quads ahead.  The token logic
+        // is written with selects so the 16 lanes of a wave, each on its own segment, execute
+        // one short path per step.
+        constexpr uint32_t LN_PERIOD = 3;
+        u32x4* const ring = reinterpret_cast<u32x4*>(SH + lane * LN_PRE_BYTES);
+        const uint64_t* const ring2 = reinterpret_cast<const uint64_t*>(ring);
+        uint32_t bp = br.bitpos();
+        {
+            const uint32_t q0 = bp >> 7;
+            u32x4 t[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; k++) t[k] = br.blk[min(q0 + k, br.nblk - 1)];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; k++) ring[(q0 + k) & 7] = t[k];
         }
-        if (dbg) dbg[3] = __builtin_amdgcn_s_memtime();
+        uint32_t nextq = (bp >> 7) + 8, tq0 = 0, tq1 = 0;
+        u32x4 S0 = {0, 0, 0, 0}, S1 = {0, 0, 0, 0};
+        bool v0 = false, v1 = false;
+        // one symbol; returns false once the lane's block has ended (EOB or a flag)
+        auto step = [&]() -> bool {
+            if (dbg) n_iter++;
+            // 64-bit window at bp: words wi .. wi + 2 from two aligned word pairs
+            const uint32_t wi = bp >> 5, pr = wi >> 1;
+            const uint64_t pa0 = ring2[pr & 15], pa1 = ring2[(pr + 1) & 15];
+            const bool odd = wi & 1;
+            const uint32_t w0 = odd ? (uint32_t)(pa0 >> 32) : (uint32_t)pa0;
+            const uint32_t w1 = odd ? (uint32_t)pa1 : (uint32_t)(pa0 >> 32);
+            const uint32_t w2 = odd ? (uint32_t)(pa1 >> 32) : (uint32_t)pa1;
+            const uint32_t sh = bp & 31;
+            const uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32) |
+                                 __builtin_amdgcn_alignbit(w1, w0, sh);
+            // lit/len symbol, then the distance decoded from the same window (used for lengths)
+            const uint32_t e = lut16(2 * ((uint32_t)win & 511u));
+            const uint32_t cl = (e >> 11) & 15;
+            const bool isl = (e & 0x8000u) != 0;
+            const uint32_t ex = isl ? (e >> 8) & 7 : 0u;
+            const uint32_t L = (e & 255) + 3 + ((uint32_t)(win >> cl) & ((1u << ex) - 1u));
+            const uint32_t n1 = cl + ex;
+            const uint64_t dwin = win >> n1;
+            const uint32_t de = lut16(LN_DIST + 2 * ((uint32_t)dwin & 63u));
+            const uint32_t dcl = (de >> 8) & 7, ds = de & 31;
+            const uint32_t dx = dist_extra(ds);
+            const uint32_t d = dist_base(ds) + ((uint32_t)(dwin >> dcl) & ((1u << dx) - 1u));
+            const uint32_t sym = e & 511;
+            bp += n1 + (isl ? dcl + dx : 0u);
+            // outcome: literal, match (or the stream-start copy of nothing), end, or a flag
+            const bool lit = !isl && sym < 256;
+            const bool far = isl && d > outpos;
+            uint32_t fl = 0;
+            if (isl) {
+                if (ds >= 30) fl = SEGF_EXOTIC;  // reference: distance symbols 30/31 = distance 0
+                else if (far) fl = j != 0 ? SEGF_XREF : (bp > 8 * br.E ? SEGF_EXOTIC : 0u);
+                else if (outpos + L > LN_OUT_CAP) fl = SEGF_EXOTIC;
+            } else if (lit) {
+                if (outpos >= LN_OUT_CAP) fl = SEGF_EXOTIC;
+            } else if (sym != 256) {
+                fl = SEGF_EXOTIC;  // 286/287: reference length 0
+            }
+            const bool mt = isl && !far && !fl;   // a copy that produces bytes
+            const bool lt = lit && !fl;
+            const bool lcont = lt && pk == 1 && pd < 3;
+            const bool mcont = mt && pk == 2 && pd == d && pa + L <= 0xFFFFu;
+            const bool emit = (lt || mt) && !(lcont || mcont) && pk != 0;
+            const uint32_t ew = pk == 1 ? (pd << 24) | pa : 0x80000000u | (pa << 15) | (pd - 1);
+            if (lt || mt) {
+                pa = lcont ? pa | (sym << (8 * pd)) : mcont ? pa + L : lt ? sym : L;
+                pd = lcont ? pd + 1 : mcont ? pd : lt ? 1u : d;
+                pk = lt ? 1u : 2u;
+                outpos += lt ? 1u : L;
+            }
+            if (emit) push(ew);
+            flags |= fl;
+            return !fl && (isl || lit);
+        };
+        // two periods per trip, each with its own staging register (a select between them
+        // would make every load's latency part of the step that follows it)
+        auto stage = [&](u32x4& S, bool& v, uint32_t& tq) {
+            if (v) ring[tq & 7] = S;  // staged two periods ago
+            const bool adv = nextq < (bp >> 7) + 8;  // its slot's quad is consumed
+            S = br.blk[min(nextq, br.nblk - 1)];
+            v = adv;
+            tq = nextq;
+            nextq += adv ? 1u : 0u;
+        };
+        static_assert(LN_PERIOD == 3, "steps per period below");
+        for (;;) {
+            stage(S0, v0, tq0);
+            if (!step() || !step() || !step()) break;
+            stage(S1, v1, tq1);
+            if (!step() || !step() || !step()) break;
+        }
+        endbit = bp;
+        if (dbg) dbg[4] = __builtin_amdgcn_s_memtime();
         // ---- what follows the block: BFINAL, or the empty stored block of a segment end ------
         if (!flags) {
             if (bfinal) {
                 fin = true;
-                end_byte = ((br.bitpos() + 7) >> 3) + cb - off0;
-            } else {
-                br.ensure(3);
-                const uint32_t f2 = br.bits(1), t2 = br.bits(2);
-                br.align();
-                br.ensure(32);
-                const uint32_t l2 = br.bits(16), n2 = br.bits(16);
-                if (f2 || t2 != 0 || l2 != 0 || n2 != 0xFFFF) flags |= SEGF_EXOTIC;
-                end_byte = (br.bitpos() >> 3) + cb - off0;
+                end_byte = ((bp + 7) >> 3) + cb - off0;
+            } else {  // 000, pad to the byte, LEN = 0000, NLEN = FFFF: from a window at bp
+                const uint32_t wi = bp >> 5, pr = wi >> 1;
+                const uint64_t pa0 = ring2[pr & 15], pa1 = ring2[(pr + 1) & 15];
+                const bool odd = wi & 1;
+                const uint32_t w0 = odd ? (uint32_t)(pa0 >> 32) : (uint32_t)pa0;
+                const uint32_t w1 = odd ? (uint32_t)pa1 : (uint32_t)(pa0 >> 32);
+                const uint32_t w2 = odd ? (uint32_t)(pa1 >> 32) : (uint32_t)pa1;
+                const uint32_t sh = bp & 31;
+                const uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32) |
+                                     __builtin_amdgcn_alignbit(w1, w0, sh);
+                const uint32_t pad = (8u - ((bp + 3) & 7u)) & 7u;
+                const uint32_t hdr = (uint32_t)win & 7u, ln = (uint32_t)(win >> (3 + pad));
+                if (hdr != 0 || ln != 0xFFFF0000u) flags |= SEGF_EXOTIC;
+                endbit = bp + 3 + pad + 32;
+                end_byte = (endbit >> 3) + cb - off0;
             }
         }
     }
-    if (br.bitpos() > 8 * br.E) flags |= SEGF_EXOTIC;
+    if (!seg_lane) return;
+    if (endbit > 8 * br.E) flags |= SEGF_EXOTIC;
     flushp();
     if (qn) {  // the queue's last partial group: the newest qn words, q[4 - qn .. 3]
         if (ntok + qn <= tcap) {
@@ -468,8 +501,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
     r.flags = flags | (fin ? SEGF_FINAL : 0u);
     A.recs[j] = r;
     B.ntok[j] = ntok;
-    if (dbg) {
-        dbg[4] = __builtin_amdgcn_s_memtime();
+    if (dbg) {  // (slots 5..7 belong to k_inflate_resolve)
         dbg[8] = n_iter;
         dbg[9] = n_top;
         dbg[10] = ntok;
