@@ -2,17 +2,18 @@
 //
 // Phase A, k_inflate_lanes: ONE LANE PER CANDIDATE SEGMENT.  Huffman decoding is serial within
 // a segment, but a 1 GiB stream holds ~32K independent segments (libdmx's deflate, or any
-// encoder's full-flush points), so 64 segments decode side by side in one wavefront and the
-// whole stream is in flight at once.  Each lane owns a 1280-byte LDS region:
-//     [   0, 1024)  lit/len lookup table, 512 x u16, indexed by the next <= 9 stream bits
-//     [1024, 1152)  distance lookup table, 64 x u16 (<= 6-bit codes)
-//     [1152, 1280)  code-length (precode) lookup table, 128 x u8 (<= 7-bit codes, RFC 1951)
-// 16 lanes x 1280 B = 20 KiB per workgroup (a quarter wave: the decode is issue-bound, so eight
-// one-wave workgroups per CU put two waves on every SIMD): 32768 lanes on 256 CUs.
-// The block header is read twice (pass 1 counts the code lengths, pass 2 re-decodes them and
-// fills the tables), so no per-symbol code-length array is stored; per-length counters and
-// next-code values live in packed registers (dynamic "indexing" by shifts).  The decoded
-// tokens go to HBM as 32-bit words:
+// encoder's full-flush points), so 32 segments decode side by side in one wavefront and the
+// whole stream is in flight at once.  LDS layout (per segment 1152 B of tables + 128 B shared
+// area; 32 segments per one-wave workgroup = 40 KiB, four workgroups per CU): see LN_REGION.
+// Phases of a workgroup:
+//   1. each lane reads its block header (BTYPE; stored segments are handled right there);
+//   2. the wave builds every dynamic segment's precode table in turn (ln_coop_table: ballot
+//      counts, canonical order, one table entry per lane);
+//   3. each lane decodes its code-length sequence once into bytes (branch-free steps);
+//   4. the wave builds every segment's 9-bit lit/len and 6-bit distance tables in turn;
+//   5. each lane decodes its tokens: a 64-bit window per symbol from a per-lane LDS ring of
+//      the stream (no refill branch), table lookups, select-based token logic.  The decoded
+//      tokens go to HBM as 32-bit words:
 //     match        1 | L(16) | d-1(15)          consecutive matches with the same distance are
 //                                               merged: one periodic copy of their summed length
 //     literal run  0 | count(7) = 1..3 | bytes(24)
@@ -53,12 +54,13 @@ constexpr uint32_t LN_LENS = 704;
 constexpr uint32_t LN_PRE_BYTES = 128;
 constexpr uint32_t LN_OUT_CAP = 32768;
 #ifndef DMX_LN_LANES
-#define DMX_LN_LANES 16
+#define DMX_LN_LANES 32
 #endif
-constexpr uint32_t LN_LANES = DMX_LN_LANES;  // segments per 64-thread workgroup: 16 x 1280 B = 20 KiB of LDS,
-                                   // eight workgroups per CU, two decoding waves on every SIMD
-                                   // (the decode is issue-bound: lanes per wave cost nothing,
-                                   // waves per SIMD double the issue rate)
+// segments per 64-thread workgroup: 32 x 1280 B = 40 KiB of LDS, four workgroups per CU, one
+// decoding wave per SIMD holding 32 segments.  The branch-free token step is VALU-issue-bound,
+// so one wave of 32 segments beats two of 16 (1 GiB text inflate 12.3 -> 10.9 ms); the
+// table builds take the other half of the wave's lanes.
+constexpr uint32_t LN_LANES = DMX_LN_LANES;
 
 __constant__ const uint8_t kLnPerm[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5,
                                           11, 4,  12, 3, 13, 2, 14, 1, 15};
@@ -287,35 +289,31 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
         uint32_t i = 0, prev = 0;
         bool prevok = false;
         const uint32_t total = hlit + hdist;
+        // one precode symbol per step, outcome by selects (short-circuit && would branch)
         while (!flags && i < total) {
             if (__any(br.low())) br.topup();
-            br.ensure(14);
+            br.ensure(14);  // a precode code (<= 7 bits) and its repeat bits (<= 7)
             const uint32_t e = PRE[(uint32_t)(br.bb & 127)];
-            br.consume(e >> 5);
-            const uint32_t sym = e & 31;
-            uint32_t val = 0, run = 1;
-            if (sym < 16) {
-                val = sym;
-                prev = sym;
-                prevok = true;
-            } else if (sym == 16) {
-                if (!prevok || i == hlit) flags |= SEGF_EXOTIC;  // A-12 / sequence-start repeat
-                val = prev;
-                run = 3 + br.bits(2);
-            } else if (sym == 17) {
-                run = 3 + br.bits(3);
-                prevok = false;
-            } else {
-                run = 11 + br.bits(7);
-                prevok = false;
-            }
-            if ((i < hlit && i + run > hlit) || i + run > total) flags |= SEGF_EXOTIC;  // A-11
-            if (val && !flags) {
-                if (val > (i < hlit ? 9u : 6u)) flags |= SEGF_EXOTIC;  // beyond the lane tables
-                const uint32_t at = i < hlit ? i : 288 + (i - hlit);
-                for (uint32_t r = 0; r < run; r++) LL[at + r] = (uint8_t)val;
-            }
+            const uint32_t len = e >> 5, sym = e & 31;
+            const uint32_t ex = sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u;
+            const uint32_t xv = (uint32_t)(br.bb >> len) & ((1u << ex) - 1u);
+            br.consume(len + ex);
+            const bool lit = sym < 16;
+            const uint32_t run = lit ? 1u : (sym == 18 ? 11u : 3u) + xv;
+            const uint32_t val = lit ? sym : (sym == 16 ? prev : 0u);
+            const bool inl = i < hlit;
+            const bool bad = ((sym == 16) & (!prevok | (i == hlit))) |  // A-12 / sequence-start repeat
+                             (inl & (i + run > hlit)) | (i + run > total) |  // A-11
+                             (val > (inl ? 9u : 6u));                      // beyond the lane tables
+            prevok = lit | ((sym == 16) & prevok);
+            prev = lit ? sym : prev;
+            const uint32_t at = inl ? i : 288 + (i - hlit);
+            const uint32_t nw = ((val != 0u) & !bad) ? run : 0u;  // <= 6 bytes (a 16 repeats <= 6)
+#pragma unroll
+            for (uint32_t r = 0; r < 6; r++)
+                if (r < nw) LL[at + r] = (uint8_t)val;
             i += run;
+            flags |= bad ? (uint32_t)SEGF_EXOTIC : 0u;
         }
     }
     if (dbg) dbg[2] = __builtin_amdgcn_s_memtime();
@@ -360,7 +358,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
         // staged two periods earlier into the ring (loads complete off the critical path); a
         // quad goes into the ring only once the one it replaces is consumed.  LN_PERIOD steps
         // consume <= 99 bits < one quad, so the ring stays >= 5 quads ahead.  The token logic
-        // is written with selects so the 16 lanes of a wave, each on its own segment, execute
+        // is written with selects so the lanes of a wave, each on its own segment, execute
         // one short path per step.
         constexpr uint32_t LN_PERIOD = 3;
         u32x4* const ring = reinterpret_cast<u32x4*>(SH + lane * LN_PRE_BYTES);
@@ -378,18 +376,27 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
         u32x4 S0 = {0, 0, 0, 0}, S1 = {0, 0, 0, 0};
         bool v0 = false, v1 = false;
         // one symbol; returns false once the lane's block has ended (EOB or a flag)
+        const uint32_t E8 = 8 * br.E;
+        const uint32_t xref_fl = j != 0 ? (uint32_t)SEGF_XREF : 0u;
+        // The 64-bit window at bp lives in registers; each step reads the next 64 bits (from
+        // two word pairs addressed by the old bp, so the LDS latency overlaps the table lookups)
+        // and funnels them in after consuming the symbol.
+        auto window_at = [&](uint32_t pos, uint64_t q0, uint64_t q1) -> uint64_t {  // q0, q1: pairs
+            const bool odd = (pos >> 5) & 1;                                       // holding pos
+            const uint32_t w0 = odd ? (uint32_t)(q0 >> 32) : (uint32_t)q0;
+            const uint32_t w1 = odd ? (uint32_t)q1 : (uint32_t)(q0 >> 32);
+            const uint32_t w2 = odd ? (uint32_t)(q1 >> 32) : (uint32_t)q1;
+            const uint32_t sh = pos & 31;
+            return ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32) | __builtin_amdgcn_alignbit(w1, w0, sh);
+        };
+        uint64_t win;
+        {
+            const uint32_t pr = bp >> 6;
+            win = window_at(bp, ring2[pr & 15], ring2[(pr + 1) & 15]);
+        }
         auto step = [&]() -> bool {
-            if (dbg) n_iter++;
-            // 64-bit window at bp: words wi .. wi + 2 from two aligned word pairs
-            const uint32_t wi = bp >> 5, pr = wi >> 1;
-            const uint64_t pa0 = ring2[pr & 15], pa1 = ring2[(pr + 1) & 15];
-            const bool odd = wi & 1;
-            const uint32_t w0 = odd ? (uint32_t)(pa0 >> 32) : (uint32_t)pa0;
-            const uint32_t w1 = odd ? (uint32_t)pa1 : (uint32_t)(pa0 >> 32);
-            const uint32_t w2 = odd ? (uint32_t)(pa1 >> 32) : (uint32_t)pa1;
-            const uint32_t sh = bp & 31;
-            const uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32) |
-                                 __builtin_amdgcn_alignbit(w1, w0, sh);
+            const uint32_t pr = bp >> 6;
+            const uint64_t nq0 = ring2[(pr + 1) & 15], nq1 = ring2[(pr + 2) & 15];
             // lit/len symbol, then the distance decoded from the same window (used for lengths)
             const uint32_t e = lut16(2 * ((uint32_t)win & 511u));
             const uint32_t cl = (e >> 11) & 15;
@@ -403,35 +410,55 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             const uint32_t dx = dist_extra(ds);
             const uint32_t d = dist_base(ds) + ((uint32_t)(dwin >> dcl) & ((1u << dx) - 1u));
             const uint32_t sym = e & 511;
-            bp += n1 + (isl ? dcl + dx : 0u);
-            // outcome: literal, match (or the stream-start copy of nothing), end, or a flag
-            const bool lit = !isl && sym < 256;
-            const bool far = isl && d > outpos;
-            uint32_t fl = 0;
-            if (isl) {
-                if (ds >= 30) fl = SEGF_EXOTIC;  // reference: distance symbols 30/31 = distance 0
-                else if (far) fl = j != 0 ? SEGF_XREF : (bp > 8 * br.E ? SEGF_EXOTIC : 0u);
-                else if (outpos + L > LN_OUT_CAP) fl = SEGF_EXOTIC;
-            } else if (lit) {
-                if (outpos >= LN_OUT_CAP) fl = SEGF_EXOTIC;
-            } else if (sym != 256) {
-                fl = SEGF_EXOTIC;  // 286/287: reference length 0
+            const uint32_t c = n1 + (isl ? dcl + dx : 0u);  // 1 .. 33 bits
+            const uint64_t ext = window_at(bp + 64, nq0, nq1);
+            win = (win >> c) | ((ext << 1) << (63 - c));
+            bp += c;
+            // outcome by selects: literal, match (or the stream-start copy of nothing), end of
+            // block, or a flag (distance symbol 30/31 = the reference's distance 0; length
+            // symbols 286/287 = its length 0; a segment past 32 KiB; a reference before the
+            // segment start, or at the stream start an over-read -- the one step that produces
+            // nothing, so the loop stays bounded)
+            // (bitwise & / | on the conditions: short-circuit && would become branches)
+            const bool lit = !isl & (sym < 256);
+            const bool far = d > outpos;
+            const uint32_t EXO = SEGF_EXOTIC;
+            const uint32_t f_far = xref_fl | (((xref_fl == 0u) & (bp > E8)) ? EXO : 0u);
+            const uint32_t f_m = (ds >= 30) ? EXO : (far ? f_far : ((outpos + L > LN_OUT_CAP) ? EXO : 0u));
+            const uint32_t f_o = lit ? ((outpos >= LN_OUT_CAP) ? EXO : 0u) : ((sym != 256) ? EXO : 0u);
+            const uint32_t fl = isl ? f_m : f_o;
+            const bool ok = fl == 0u;
+            const bool mt = isl & !far & ok;
+            const bool lt = lit & ok;
+            const bool prod = lt | mt;
+            const bool lcont = lt & (pk == 1u) & (pd < 3u);
+            const bool mcont = mt & (pk == 2u) & (pd == d) & (pa + L <= 0xFFFFu);
+            const bool cont = lcont | mcont;
+            const bool emit = prod & !cont & (pk != 0u);
+            const uint32_t ew = pk == 1u ? (pd << 24) | pa : 0x80000000u | (pa << 15) | (pd - 1u);
+            const uint32_t a_cont = lcont ? (pa | (sym << (8 * pd))) : (pa + L);
+            const uint32_t a_new = lt ? sym : L;
+            const uint32_t d_cont = lcont ? pd + 1u : pd;
+            const uint32_t d_new = lt ? 1u : d;
+            const uint32_t npa = cont ? a_cont : a_new;
+            const uint32_t npd = cont ? d_cont : d_new;
+            pa = prod ? npa : pa;
+            pd = prod ? npd : pd;
+            pk = prod ? (lt ? 1u : 2u) : pk;
+            outpos += prod ? (lt ? 1u : L) : 0u;
+            // queue of 4 token words (shift register), one 16-byte store per 4 words
+            q0 = emit ? q1 : q0;
+            q1 = emit ? q2 : q1;
+            q2 = emit ? q3 : q2;
+            q3 = emit ? ew : q3;
+            qn += emit ? 1u : 0u;
+            if (qn == 4) {
+                if (ntok + 4 <= tcap) *reinterpret_cast<uint4*>(tk + ntok) = make_uint4(q0, q1, q2, q3);
+                ntok += 4;
+                qn = 0;
             }
-            const bool mt = isl && !far && !fl;   // a copy that produces bytes
-            const bool lt = lit && !fl;
-            const bool lcont = lt && pk == 1 && pd < 3;
-            const bool mcont = mt && pk == 2 && pd == d && pa + L <= 0xFFFFu;
-            const bool emit = (lt || mt) && !(lcont || mcont) && pk != 0;
-            const uint32_t ew = pk == 1 ? (pd << 24) | pa : 0x80000000u | (pa << 15) | (pd - 1);
-            if (lt || mt) {
-                pa = lcont ? pa | (sym << (8 * pd)) : mcont ? pa + L : lt ? sym : L;
-                pd = lcont ? pd + 1 : mcont ? pd : lt ? 1u : d;
-                pk = lt ? 1u : 2u;
-                outpos += lt ? 1u : L;
-            }
-            if (emit) push(ew);
             flags |= fl;
-            return !fl && (isl || lit);
+            return ok & (isl | lit);
         };
         // two periods per trip, each with its own staging register (a select between them
         // would make every load's latency part of the step that follows it)
