@@ -45,8 +45,6 @@ constexpr int df_hash_bits(int seg) {  // hash bits of each of the two match tab
 // (inflate_lanes.hip: 512 + 64 entries per segment in LDS) at < 1% ratio cost.
 constexpr int DF_LIT_MAXBITS = 9;
 constexpr int DF_DIST_MAXBITS = 6;
-constexpr int DF_PPT = 2;      // positions per thread in one match round (4 halves the rounds
-                               // but loses recent candidates: -4% ratio on repeat, -1% on text)
 
 // ---------------------------------------------------------------------------------------
 // block primitives
@@ -409,7 +407,7 @@ struct DfSmem {
     static constexpr int UW1 = SEG / 4 + 64;
     static constexpr int UW = UW0 > UW1 ? UW0 : UW1;
     uint32_t data32[SEG / 4 + 32];  // + 128 B: matchlen4 reads up to 84 B past a match end
-    uint16_t cand[SEG + 8];
+    alignas(16) uint16_t cand[SEG + 8];
     // while matching: HT pairs {head, first} (one ds_read_b64 per lookup); the output bit image
     // afterwards
     alignas(16) uint32_t U[UW];
@@ -430,7 +428,7 @@ struct DfSmem {
     // block_build_codes: ranks (lit/len at [0, 286), distance at [320, 350)), per-alphabet
     // class sizes, class start ranks, next canonical code, per-wave length counts, F / used
     uint32_t hb_rank[352];
-    uint32_t hb_xbuf[2][512];
+    alignas(16) uint32_t hb_xbuf[2][512];
     uint32_t hb_cnt[2][16];
     uint32_t hb_start[2][16];
     uint32_t hb_next[2][16];
@@ -897,70 +895,79 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
             //   head  = p + 1 (16) | fp16                       (atomicMax: latest p, 0 = none)
             // stored as {head, first} pairs, one ds_read_b64 per lookup.  A fingerprint match
             // that is not a key match is rare; the parse walk then finds a match length < 3
-            // and emits a literal.
-            static_assert(SEG / (DF_PPT * DF_NT) <= 16, "round number is 4 bits");
+            // and emits a literal.  Thread t handles the consecutive positions p0 = r0 + 2t and
+            // p0 + 1 of each round: both keys come from one pair of words, both candidates go
+            // out as one 32-bit store, and the neighbour tests that skip redundant table updates
+            // are mostly in-thread.  A position's latest-occurrence update waits one round (a
+            // lookup must not see later positions of its own round); the first occurrence in a
+            // round is resolved by the round number in the entry.
+            static_assert(SEG / (2 * DF_NT) <= 16, "round number is 4 bits");
             constexpr uint32_t HB = DfSmem<SEG>::HB;
-            bool pok[DF_PPT] = {};
-            uint32_t ph[DF_PPT] = {}, pp[DF_PPT] = {}, pt[DF_PPT] = {};
-            const uint32_t wave = t >> 6, lane = t & 63;
             const uint2* const tab = reinterpret_cast<const uint2*>(S.U);
-            // Straight-line rounds: every LDS read is issued unconditionally (addresses stay in
-            // bounds: p < SEG), so both positions' reads share one wait per step.
-            for (uint32_t r0 = 0, rr = 0; r0 < nb; r0 += DF_PPT * DF_NT, rr++) {
-                uint32_t h[DF_PPT], p[DF_PPT], prod[DF_PPT];
-                bool ok[DF_PPT];
-#pragma unroll
-                for (int k = 0; k < DF_PPT; k++) {
-                    p[k] = r0 + k * DF_NT + t;
-                    prod[k] = ld32u(S.data32, p[k]) * 0x1E35A7BDu;
-                }
-#pragma unroll
-                for (int k = 0; k < DF_PPT; k++) {
-                    ok[k] = p[k] + 4 <= nb;
-                    h[k] = ok[k] ? prod[k] >> (32 - HB) : 0;
-                    // skip an update a neighbour position makes redundant (runs of equal keys
-                    // would otherwise serialize on one LDS address): the first occurrence needs
-                    // no write when position p - 1 has the same hash, the latest none when p + 1
-                    // has.  Neighbours come by DPP within rows of 16 lanes; row edges just write.
-                    const uint32_t hx = ok[k] ? h[k] : 0xFFFFFFFFu;
-                    const uint32_t hl = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)hx, 0x111, 0xF, 0xF, false);
-                    const uint32_t phx = pok[k] ? ph[k] : 0xFFFFFFFFu;
-                    const uint32_t phr = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)phx, 0x101, 0xF, 0xF, false);
-                    if (ok[k] && hl != hx)  // first in round
-                        atomicMax(&S.U[2 * h[k] + 1], (rr << 28) | ((0x7FFFu - p[k]) << 13) |
-                                                          ((prod[k] >> (32 - HB - 13)) & 0x1FFFu));
-                    if (pok[k] && phr != phx) atomicMax(&S.U[2 * ph[k]], ((pp[k] + 1) << 16) | pt[k]);  // previous round
-                }
+            uint32_t* const cand32 = reinterpret_cast<uint32_t*>(S.cand);
+            uint32_t ph0 = 0, ph1 = 0, pp0 = 0, pf0 = 0, pf1 = 0;  // previous round: hashes, p0, fp16s
+            bool pok0 = false, pok1 = false;
+            constexpr uint32_t NOH = 0xFFFFFFFFu;  // "no hash" for the neighbour compares
+            for (uint32_t r0 = 0, rr = 0; r0 < nb; r0 += 2 * DF_NT, rr++) {
+                const uint32_t p0 = r0 + 2 * t, p1 = p0 + 1;
+                const uint32_t i0 = p0 >> 2, sh = p0 & 3;  // sh = 0 or 2
+                const uint32_t wa = S.data32[i0], wb = S.data32[i0 + 1];
+                const uint32_t prod0 = __builtin_amdgcn_alignbyte(wb, wa, sh) * 0x1E35A7BDu;
+                const uint32_t prod1 = __builtin_amdgcn_alignbyte(wb, wa, sh + 1) * 0x1E35A7BDu;
+                const bool ok0 = p0 + 4 <= nb, ok1 = p1 + 4 <= nb;
+                const uint32_t h0 = ok0 ? prod0 >> (32 - HB) : NOH, h1 = ok1 ? prod1 >> (32 - HB) : NOH;
+                const uint32_t fa0 = (prod0 >> (32 - HB - 16)) & 0xFFFFu, fa1 = (prod1 >> (32 - HB - 16)) & 0xFFFFu;
+                // first occurrence in this round: p1 needs no update when p0 has its hash, p0 none
+                // when p0 - 1 (the previous lane's p1, by DPP within rows of 16) has it
+                const uint32_t hl = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)h1, 0x111, 0xF, 0xF, false);
+                const uint32_t rtag = rr << 28;
+                if (ok0 && h0 != hl)
+                    atomicMax(&S.U[2 * h0 + 1], rtag | ((0x7FFFu - p0) << 13) | (fa0 >> 3));
+                if (ok1 && h1 != h0)
+                    atomicMax(&S.U[2 * h1 + 1], rtag | ((0x7FFFu - p1) << 13) | (fa1 >> 3));
+                // latest occurrence, for the previous round's positions: pp0 needs no update when
+                // pp0 + 1 has its hash, pp0 + 1 none when pp0 + 2 (the next lane's) has it
+                const uint32_t hn = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)(pok0 ? ph0 : NOH), 0x101, 0xF, 0xF, false);
+                if (pok0 && ph0 != (pok1 ? ph1 : NOH)) atomicMax(&S.U[2 * ph0], ((pp0 + 1) << 16) | pf0);
+                if (pok1 && ph1 != hn) atomicMax(&S.U[2 * ph1], ((pp0 + 2) << 16) | pf1);
                 __syncthreads();
-                uint2 e[DF_PPT];
-#pragma unroll
-                for (int k = 0; k < DF_PPT; k++) e[k] = tab[h[k]];
-#pragma unroll
-                for (int k = 0; k < DF_PPT; k++) {
-                    const uint32_t f = e[k].y, hd = e[k].x;
-                    const uint32_t fp16 = (prod[k] >> (32 - HB - 16)) & 0xFFFFu;
+                const uint2 e0 = tab[ok0 ? h0 : 0u], e1 = tab[ok1 ? h1 : 0u];
+                auto pick = [&](uint2 e, uint32_t p, uint32_t fa, bool ok) -> uint32_t {
+                    const uint32_t f = e.y, hd = e.x;
                     const uint32_t q = 0x7FFFu - ((f >> 13) & 0x7FFFu);
-                    uint32_t c = ((f >> 28) == rr && q < p[k] && (f & 0x1FFFu) == (fp16 >> 3)) ? p[k] - q : 0u;
-                    if (!c && hd && (hd & 0xFFFFu) == fp16) c = p[k] - ((hd >> 16) - 1);
-                    // keep only matches that can reach 3 bytes inside this chunk (matches never
-                    // cross a chunk, so the parse lanes stay independent)
-                    const uint32_t cend = min(p[k] / DF_CHUNK * DF_CHUNK + DF_CHUNK, nb);
-                    if (!ok[k] || cend - p[k] < 3) c = 0;
-                    if (p[k] < nb) S.cand[p[k]] = (uint16_t)c;
-                    // bit p of mmap = "a candidate (4-byte fingerprint match) starts at p"
-                    const uint64_t m = __ballot(c != 0);
-                    const uint32_t w0 = (r0 + k * DF_NT + wave * 64) >> 5;
-                    if (lane == 0 && w0 < NMAP) {
-                        S.mmap[w0] = (uint32_t)m;
-                        if (w0 + 1 < NMAP) S.mmap[w0 + 1] = (uint32_t)(m >> 32);
-                    }
-                    pok[k] = ok[k];
-                    ph[k] = h[k];
-                    pp[k] = p[k];
-                    pt[k] = fp16;
-                }
+                    const bool fr = ((f >> 28) == rr) & (q < p) & ((f & 0x1FFFu) == (fa >> 3));
+                    const bool lt = (hd != 0u) & ((hd & 0xFFFFu) == fa);
+                    const uint32_t c = fr ? p - q : (lt ? p + 1u - (hd >> 16) : 0u);
+                    return ok ? c : 0u;
+                };
+                if (p0 < nb) cand32[p0 >> 1] = pick(e0, p0, fa0, ok0) | (pick(e1, p1, fa1, ok1) << 16);
+                ph0 = h0;
+                ph1 = h1;
+                pp0 = p0;
+                pf0 = fa0;
+                pf1 = fa1;
+                pok0 = ok0;
+                pok1 = ok1;
                 __syncthreads();
             }
+            // match bitmap from the candidates: bit p = "a candidate starts at p"
+            for (uint32_t w = t; w < NMAP; w += DF_NT) {
+                const uint4* c4 = reinterpret_cast<const uint4*>(S.cand + 32 * w);
+                uint32_t m = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint4 v = c4[k];
+                    const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        m |= ((x[j] & 0xFFFFu) ? 1u : 0u) << (8 * k + 2 * j);
+                        m |= ((x[j] >> 16) ? 1u : 0u) << (8 * k + 2 * j + 1);
+                    }
+                }
+                const uint32_t b0 = 32 * w;  // positions past the segment end hold stale entries
+                S.mmap[w] = b0 + 32 <= nb ? m : (nb > b0 ? m & ((1u << (nb - b0)) - 1u) : 0u);
+            }
+            __syncthreads();
             DMX_PHASE(A.dbg, seg, 14);
         }
         DMX_PHASE(A.dbg, seg, 2);
