@@ -34,7 +34,10 @@
 namespace dmx {
 
 constexpr int DF_NT = 1024;    // threads per workgroup (16 waves)
-constexpr int DF_CHUNK = 258;  // bytes per parse lane: one maximal match per chunk, and not a
+#ifndef DMX_DF_CHUNK
+#define DMX_DF_CHUNK 258
+#endif
+constexpr int DF_CHUNK = DMX_DF_CHUNK;  // bytes per parse lane: one maximal match per chunk, and not a
                                // multiple of 256, so the lanes' chunk starts spread over the LDS
                                // banks (at 256 every lane of a wave hit one bank per matchlen read)
 constexpr int df_hash_bits(int seg) {  // hash bits of each of the two match tables: 11 at 16 KiB
@@ -43,8 +46,20 @@ constexpr int df_hash_bits(int seg) {  // hash bits of each of the two match tab
 // Code-length limits of the emitted lit/len and distance codes.  RFC 1951 allows 15; 9 and 6
 // keep every code inside the one-level lookup tables of the lane decoder
 // (inflate_lanes.hip: 512 + 64 entries per segment in LDS) at < 1% ratio cost.
-constexpr int DF_LIT_MAXBITS = 9;
-constexpr int DF_DIST_MAXBITS = 6;
+#ifndef DMX_LIT_MAXBITS
+#define DMX_LIT_MAXBITS 9
+#define DMX_DIST_MAXBITS 6
+#endif
+constexpr int DF_LIT_MAXBITS = DMX_LIT_MAXBITS;
+constexpr int DF_DIST_MAXBITS = DMX_DIST_MAXBITS;
+#ifndef DMX_L3_DEPTH
+#define DMX_L3_DEPTH 16
+#endif
+constexpr int DF_L3_DEPTH = DMX_L3_DEPTH;  // level 3: candidate-chain links searched per position
+#ifndef DMX_L3_ROUND
+#define DMX_L3_ROUND 128
+#endif
+constexpr uint32_t DF_L3_ROUND = DMX_L3_ROUND;  // level 3: positions per link-building round
 
 // ---------------------------------------------------------------------------------------
 // block primitives
@@ -908,48 +923,141 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
             uint32_t ph0 = 0, ph1 = 0, pp0 = 0, pf0 = 0, pf1 = 0;  // previous round: hashes, p0, fp16s
             bool pok0 = false, pok1 = false;
             constexpr uint32_t NOH = 0xFFFFFFFFu;  // "no hash" for the neighbour compares
-            for (uint32_t r0 = 0, rr = 0; r0 < nb; r0 += 2 * DF_NT, rr++) {
-                const uint32_t p0 = r0 + 2 * t, p1 = p0 + 1;
-                const uint32_t i0 = p0 >> 2, sh = p0 & 3;  // sh = 0 or 2
-                const uint32_t wa = S.data32[i0], wb = S.data32[i0 + 1];
-                const uint32_t prod0 = __builtin_amdgcn_alignbyte(wb, wa, sh) * 0x1E35A7BDu;
-                const uint32_t prod1 = __builtin_amdgcn_alignbyte(wb, wa, sh + 1) * 0x1E35A7BDu;
-                const bool ok0 = p0 + 4 <= nb, ok1 = p1 + 4 <= nb;
-                const uint32_t h0 = ok0 ? prod0 >> (32 - HB) : NOH, h1 = ok1 ? prod1 >> (32 - HB) : NOH;
-                const uint32_t fa0 = (prod0 >> (32 - HB - 16)) & 0xFFFFu, fa1 = (prod1 >> (32 - HB - 16)) & 0xFFFFu;
-                // first occurrence in this round: p1 needs no update when p0 has its hash, p0 none
-                // when p0 - 1 (the previous lane's p1, by DPP within rows of 16) has it
-                const uint32_t hl = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)h1, 0x111, 0xF, 0xF, false);
-                const uint32_t rtag = rr << 28;
-                if (ok0 && h0 != hl)
-                    atomicMax(&S.U[2 * h0 + 1], rtag | ((0x7FFFu - p0) << 13) | (fa0 >> 3));
-                if (ok1 && h1 != h0)
-                    atomicMax(&S.U[2 * h1 + 1], rtag | ((0x7FFFu - p1) << 13) | (fa1 >> 3));
-                // latest occurrence, for the previous round's positions: pp0 needs no update when
-                // pp0 + 1 has its hash, pp0 + 1 none when pp0 + 2 (the next lane's) has it
-                const uint32_t hn = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)(pok0 ? ph0 : NOH), 0x101, 0xF, 0xF, false);
-                if (pok0 && ph0 != (pok1 ? ph1 : NOH)) atomicMax(&S.U[2 * ph0], ((pp0 + 1) << 16) | pf0);
-                if (pok1 && ph1 != hn) atomicMax(&S.U[2 * ph1], ((pp0 + 2) << 16) | pf1);
-                __syncthreads();
-                const uint2 e0 = tab[ok0 ? h0 : 0u], e1 = tab[ok1 ? h1 : 0u];
-                auto pick = [&](uint2 e, uint32_t p, uint32_t fa, bool ok) -> uint32_t {
-                    const uint32_t f = e.y, hd = e.x;
-                    const uint32_t q = 0x7FFFu - ((f >> 13) & 0x7FFFu);
-                    const bool fr = ((f >> 28) == rr) & (q < p) & ((f & 0x1FFFu) == (fa >> 3));
-                    const bool lt = (hd != 0u) & ((hd & 0xFFFFu) == fa);
-                    const uint32_t c = fr ? p - q : (lt ? p + 1u - (hd >> 16) : 0u);
-                    return ok ? c : 0u;
-                };
-                if (p0 < nb) cand32[p0 >> 1] = pick(e0, p0, fa0, ok0) | (pick(e1, p1, fa1, ok1) << 16);
-                ph0 = h0;
-                ph1 = h1;
-                pp0 = p0;
-                pf0 = fa0;
-                pf1 = fa1;
-                pok0 = ok0;
-                pok1 = ok1;
-                __syncthreads();
+            if (level == 3) {
+                // Level 3 builds links for the chain search below: rounds of DF_L3_ROUND
+                // positions, each position linked to the latest occurrence of its key before
+                // its round (or to its pair partner, in-thread), so consecutive links skip at
+                // most one round -- the hash chain of the reference's getMatchesSlow scan
+                // (deflate.hpp:268-304) in a form the parallel rounds can build.
+                const bool act = t < DF_L3_ROUND / 2;
+                for (uint32_t r0 = 0; r0 < nb; r0 += DF_L3_ROUND) {
+                    const uint32_t p0 = r0 + 2 * t, p1 = p0 + 1;
+                    uint32_t h0 = NOH, h1 = NOH, fa0 = 0, fa1 = 0, k0 = 0, k1 = 1;
+                    bool ok0 = false, ok1 = false;
+                    if (act) {
+                        const uint32_t wa = S.data32[p0 >> 2], wb = S.data32[(p0 >> 2) + 1];
+                        k0 = __builtin_amdgcn_alignbyte(wb, wa, p0 & 3);
+                        k1 = __builtin_amdgcn_alignbyte(wb, wa, (p0 & 3) + 1);
+                        const uint32_t prod0 = k0 * 0x1E35A7BDu, prod1 = k1 * 0x1E35A7BDu;
+                        ok0 = p0 + 4 <= nb;
+                        ok1 = p1 + 4 <= nb;
+                        h0 = ok0 ? prod0 >> (32 - HB) : NOH;
+                        h1 = ok1 ? prod1 >> (32 - HB) : NOH;
+                        fa0 = (prod0 >> (32 - HB - 16)) & 0xFFFFu;
+                        fa1 = (prod1 >> (32 - HB - 16)) & 0xFFFFu;
+                        const uint32_t hn = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)(pok0 ? ph0 : NOH), 0x101, 0xF, 0xF, false);
+                        if (pok0 && ph0 != (pok1 ? ph1 : NOH)) atomicMax(&S.U[2 * ph0], ((pp0 + 1) << 16) | pf0);
+                        if (pok1 && ph1 != hn) atomicMax(&S.U[2 * ph1], ((pp0 + 2) << 16) | pf1);
+                    }
+                    __syncthreads();
+                    if (act) {
+                        const uint32_t e0 = tab[ok0 ? h0 : 0u].x, e1 = tab[ok1 ? h1 : 0u].x;
+                        const uint32_t c0 = ok0 && e0 && (e0 & 0xFFFFu) == fa0 ? p0 + 1u - (e0 >> 16) : 0u;
+                        uint32_t c1 = ok1 && e1 && (e1 & 0xFFFFu) == fa1 ? p1 + 1u - (e1 >> 16) : 0u;
+                        if (ok1 && ok0 && k1 == k0) c1 = 1;
+                        cand32[p0 >> 1] = c0 | (c1 << 16);
+                    }
+                    ph0 = h0;
+                    ph1 = h1;
+                    pp0 = p0;
+                    pf0 = fa0;
+                    pf1 = fa1;
+                    pok0 = ok0;
+                    pok1 = ok1;
+                    __syncthreads();
+                }
+            } else {
+                for (uint32_t r0 = 0, rr = 0; r0 < nb; r0 += 2 * DF_NT, rr++) {
+                    const uint32_t p0 = r0 + 2 * t, p1 = p0 + 1;
+                    const uint32_t i0 = p0 >> 2, sh = p0 & 3;  // sh = 0 or 2
+                    const uint32_t wa = S.data32[i0], wb = S.data32[i0 + 1];
+                    const uint32_t prod0 = __builtin_amdgcn_alignbyte(wb, wa, sh) * 0x1E35A7BDu;
+                    const uint32_t prod1 = __builtin_amdgcn_alignbyte(wb, wa, sh + 1) * 0x1E35A7BDu;
+                    const bool ok0 = p0 + 4 <= nb, ok1 = p1 + 4 <= nb;
+                    const uint32_t h0 = ok0 ? prod0 >> (32 - HB) : NOH, h1 = ok1 ? prod1 >> (32 - HB) : NOH;
+                    const uint32_t fa0 = (prod0 >> (32 - HB - 16)) & 0xFFFFu, fa1 = (prod1 >> (32 - HB - 16)) & 0xFFFFu;
+                    // first occurrence in this round: p1 needs no update when p0 has its hash, p0 none
+                    // when p0 - 1 (the previous lane's p1, by DPP within rows of 16) has it
+                    const uint32_t hl = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)h1, 0x111, 0xF, 0xF, false);
+                    const uint32_t rtag = rr << 28;
+                    if (ok0 && h0 != hl)
+                        atomicMax(&S.U[2 * h0 + 1], rtag | ((0x7FFFu - p0) << 13) | (fa0 >> 3));
+                    if (ok1 && h1 != h0)
+                        atomicMax(&S.U[2 * h1 + 1], rtag | ((0x7FFFu - p1) << 13) | (fa1 >> 3));
+                    // latest occurrence, for the previous round's positions: pp0 needs no update when
+                    // pp0 + 1 has its hash, pp0 + 1 none when pp0 + 2 (the next lane's) has it
+                    const uint32_t hn = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)(pok0 ? ph0 : NOH), 0x101, 0xF, 0xF, false);
+                    if (pok0 && ph0 != (pok1 ? ph1 : NOH)) atomicMax(&S.U[2 * ph0], ((pp0 + 1) << 16) | pf0);
+                    if (pok1 && ph1 != hn) atomicMax(&S.U[2 * ph1], ((pp0 + 2) << 16) | pf1);
+                    __syncthreads();
+                    const uint2 e0 = tab[ok0 ? h0 : 0u], e1 = tab[ok1 ? h1 : 0u];
+                    auto pick = [&](uint2 e, uint32_t p, uint32_t fa, bool ok) -> uint32_t {
+                        const uint32_t f = e.y, hd = e.x;
+                        const uint32_t q = 0x7FFFu - ((f >> 13) & 0x7FFFu);
+                        const bool fr = ((f >> 28) == rr) & (q < p) & ((f & 0x1FFFu) == (fa >> 3));
+                        const bool lt = (hd != 0u) & ((hd & 0xFFFFu) == fa);
+                        const uint32_t c = fr ? p - q : (lt ? p + 1u - (hd >> 16) : 0u);
+                        return ok ? c : 0u;
+                    };
+                    if (p0 < nb) cand32[p0 >> 1] = pick(e0, p0, fa0, ok0) | (pick(e1, p1, fa1, ok1) << 16);
+                    ph0 = h0;
+                    ph1 = h1;
+                    pp0 = p0;
+                    pf0 = fa0;
+                    pf1 = fa1;
+                    pok0 = ok0;
+                    pok1 = ok1;
+                    __syncthreads();
+                }
             }
+            DMX_PHASE(A.dbg, seg, 14);
+        }
+        if (level == 3) {
+            // ---- level 3: deeper search along the candidate chains ----------------------------
+            // cand[q] links q to an earlier occurrence of its 4-byte key, so p -> p - cand[p] ->
+            // ... walks the occurrences of p's key from the most recent back (a hash chain whose
+            // links the match rounds already made).  Every position takes the longest match
+            // among the first DF_L3_DEPTH links (the nearest on ties; stop at the longest
+            // possible).  Thread t handles positions t + DF_NT k; the results stay in registers
+            // until every chain walk is done, so the links read are always the rounds' (the
+            // output does not depend on scheduling).  Replaces the reference's O(W^2) backward
+            // scan LZ77::getMatchesSlow (deflate.hpp:268-304), whose lengths above 258 turn into
+            // literal 0x00 bytes (SURVEY A-2); here matches stay within 258 and the parse chunk.
+            constexpr int KP = SEG / DF_NT;  // positions per thread
+            uint32_t best[KP / 2];
+#pragma unroll
+            for (int k = 0; k < KP; k++) {
+                const uint32_t p = t + DF_NT * k;
+                uint32_t bd = 0;
+                const uint32_t d0 = p < nb ? S.cand[p] : 0u;
+                if (d0) {
+                    const uint32_t hi = min(p / DF_CHUNK * DF_CHUNK + DF_CHUNK, nb);
+                    const uint32_t maxl = min(258u, hi - p);
+                    uint32_t bl = 2, q = p - d0;
+                    for (int hop = 0; hop < DF_L3_DEPTH; hop++) {
+                        const uint32_t L = matchlen(S.data32, p, q, maxl);
+                        if (L > bl) {
+                            bl = L;
+                            bd = p - q;
+                            if (L >= maxl) break;
+                        }
+                        const uint32_t dq = S.cand[q];
+                        if (!dq) break;
+                        q -= dq;
+                    }
+                }
+                if (k & 1) best[k / 2] |= bd << 16;
+                else best[k / 2] = bd;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < KP; k++) {
+                const uint32_t p = t + DF_NT * k;
+                if (p < nb) S.cand[p] = (uint16_t)(k & 1 ? best[k / 2] >> 16 : best[k / 2] & 0xFFFFu);
+            }
+            __syncthreads();
+        }
+        if (level >= 2) {
             // match bitmap from the candidates: bit p = "a candidate starts at p"
             for (uint32_t w = t; w < NMAP; w += DF_NT) {
                 const uint4* c4 = reinterpret_cast<const uint4*>(S.cand + 32 * w);
@@ -968,7 +1076,6 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
                 S.mmap[w] = b0 + 32 <= nb ? m : (nb > b0 ? m & ((1u << (nb - b0)) - 1u) : 0u);
             }
             __syncthreads();
-            DMX_PHASE(A.dbg, seg, 14);
         }
         DMX_PHASE(A.dbg, seg, 2);
 
