@@ -1214,22 +1214,40 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
     emit_stored<SEG>(S, nb, is_final, slot, &A.sizes[seg]);
 }
 
-// exclusive scan of segment sizes -> offsets (single workgroup of 1024 threads).  Each thread
-// owns a contiguous run of sizes; the loads of a run go out eight at a time (independent loads,
-// one memory latency per batch instead of one per size).
+// exclusive scan of segment sizes -> offsets (single workgroup of 1024 threads).  Thread t owns
+// the contiguous run [t per, (t + 1) per) and moves it in batches of 32 sizes: eight 16-byte
+// loads issued together (one memory latency per batch), registers summed, a block scan of the
+// run totals, then the offsets of each batch written back as 16-byte stores.  A 1 GiB shard
+// (32768 sizes) is one batch per thread.
 __global__ __launch_bounds__(1024) void k_scan_sizes(const uint32_t* sizes, uint64_t* offs,
                                                       uint64_t nseg, uint64_t* total) {
     __shared__ uint64_t part[1024];
     const int t = threadIdx.x;
-    const uint64_t per = (nseg + 1023) / 1024;
-    const uint64_t b = t * per, e = min(nseg, b + per);
+    const uint64_t per = ((nseg + 1023) / 1024 + 31) & ~31ull;  // multiple of 32
+    const uint64_t b = min(nseg, t * per), e = min(nseg, b + per);
+    const bool vec = ((reinterpret_cast<uintptr_t>(sizes) | reinterpret_cast<uintptr_t>(offs)) & 15) == 0;
+    auto load32 = [&](uint64_t i, uint32_t (&v)[32]) {
+        if (vec && i + 32 <= e) {
+            const uint4* s4 = reinterpret_cast<const uint4*>(sizes + i);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint4 q = s4[k];
+                v[4 * k] = q.x;
+                v[4 * k + 1] = q.y;
+                v[4 * k + 2] = q.z;
+                v[4 * k + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 32; k++) v[k] = i + k < e ? sizes[i + k] : 0u;
+        }
+    };
     uint64_t s = 0;
-    for (uint64_t i = b; i < e; i += 8) {
-        uint32_t v[8];
+    for (uint64_t i = b; i < e; i += 32) {
+        uint32_t v[32];
+        load32(i, v);
 #pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = i + k < e ? sizes[i + k] : 0u;
-#pragma unroll
-        for (int k = 0; k < 8; k++) s += v[k];
+        for (int k = 0; k < 32; k++) s += v[k];
     }
     part[t] = s;
     __syncthreads();
@@ -1240,14 +1258,23 @@ __global__ __launch_bounds__(1024) void k_scan_sizes(const uint32_t* sizes, uint
         __syncthreads();
     }
     uint64_t run = part[t] - s;
-    for (uint64_t i = b; i < e; i += 8) {
-        uint32_t v[8];
+    for (uint64_t i = b; i < e; i += 32) {
+        uint32_t v[32];
+        load32(i, v);  // L2-hot
+        uint64_t o[32];
 #pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = i + k < e ? sizes[i + k] : 0u;
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            if (i + k < e) offs[i + k] = run;
+        for (int k = 0; k < 32; k++) {
+            o[k] = run;
             run += v[k];
+        }
+        if (vec && i + 32 <= e) {
+            ulonglong2* d2 = reinterpret_cast<ulonglong2*>(offs + i);
+#pragma unroll
+            for (int k = 0; k < 16; k++) d2[k] = make_ulonglong2(o[2 * k], o[2 * k + 1]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 32; k++)
+                if (i + k < e) offs[i + k] = o[k];
         }
     }
     if (t == 1023) *total = part[1023];

@@ -84,6 +84,7 @@ struct Scal {  // small device-side scalars, one allocation
     uint32_t ticket;
     uint32_t fb_err;  // block-parallel path: a copy reached before the stream start
     InflateResult res;
+    ValidateWords vw;
 };
 
 // DMX_PHASES=<file>: kernels record s_memtime per phase and segment; the host appends one line
@@ -432,7 +433,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
             HIPCHK(hipMemsetAsync(&ds->ticket, 0, 4, st));
             HIPCHK(launch_inflate_segments(A, st, e0, e1));
         }
-        HIPCHK(launch_inflate_validate(A, &ds->res, st));
+        HIPCHK(launch_inflate_validate(A, &ds->vw, &ds->res, st));
         if (A.dbg) phase_dump(c, "inflate", ncand, st);
         HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));

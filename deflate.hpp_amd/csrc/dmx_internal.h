@@ -98,7 +98,12 @@ hipError_t launch_inflate_pj(const InflateArgs& A, uint32_t seg, hipStream_t st,
 hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* tokoff,
                                 uint32_t* ntok, uint32_t* caps, hipStream_t st, hipEvent_t ev0,
                                 hipEvent_t ev1);
-hipError_t launch_inflate_validate(const InflateArgs& A, InflateResult* res, hipStream_t st);
+// validation scratch: five device words, zeroed by the launch
+struct ValidateWords {
+    unsigned long long kmin, bmin, umin, xmin, xcnt;
+};
+hipError_t launch_inflate_validate(const InflateArgs& A, ValidateWords* W, InflateResult* res,
+                                   hipStream_t st);
 
 // block-parallel inflate of arbitrary streams (inflate_blocks.hip, path 5)
 struct FbUnit {         // per-unit record written by k_fb_decode

@@ -947,47 +947,63 @@ hipError_t launch_inflate_pj(const InflateArgs& A, uint32_t seg, hipStream_t st,
 // Candidate chain check.  Valid iff, up to the first BFINAL segment k, every segment decoded
 // without error and ended exactly at the next candidate.  Speculative mode additionally needs
 // every segment before k to have segment 0's size (else status 1: re-run with look-back).
-__global__ __launch_bounds__(1024) void k_inflate_validate(InflateArgs A, InflateResult* res) {
+// Validation in two launches: k_inflate_validate_scan spreads the candidate records over the
+// whole GPU and folds them into five global words (first BFINAL, first break of the chain,
+// first non-uniform size, first declined candidate, declined count); k_inflate_validate
+// turns them into the result.  (A single workgroup walking 32K records serially on dependent
+// loads took ~38 us per call.)  The minima are kept as maxima of ~j so that the five words start
+// from one zero memset (0 = none).
+__global__ __launch_bounds__(256) void k_inflate_validate_scan(InflateArgs A, ValidateWords* W) {
     __shared__ unsigned long long kmin, bmin, umin, xmin, xcnt;
     const int t = threadIdx.x;
     if (t == 0) { kmin = ~0ull; bmin = ~0ull; umin = ~0ull; xmin = ~0ull; xcnt = 0; }
     __syncthreads();
-    // mode 2 (k_inflate_lanes) placed segment j at j * 32768
+    // mode 2 / 4 placed segment j at j * slot
     const uint32_t size0 = A.mode >= 2 ? A.slot : A.recs[0].out_size;
-    for (uint64_t j = t; j < A.ncand; j += 1024) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + t;
+    if (j < A.ncand) {
         const SegRecord r = A.recs[j];
-        if (r.flags & SEGF_EXOTIC) {  // k_inflate_pj declined this candidate
+        if (r.flags & SEGF_EXOTIC) {  // the pass declined this candidate
             atomicMin(&xmin, (unsigned long long)j);
             atomicAdd(&xcnt, 1ull);
-            continue;
+        } else {
+            const bool fin = (r.flags & SEGF_FINAL) != 0;
+            const bool err = (r.flags & ~SEGF_FINAL) != 0;
+            const bool chain = (j + 1 < A.ncand) && r.end_byte == A.cands[j + 1];
+            if (fin) atomicMin(&kmin, (unsigned long long)j);
+            if (err || (!fin && !chain)) atomicMin(&bmin, (unsigned long long)j);
+            if (!fin && r.out_size != size0) atomicMin(&umin, (unsigned long long)j);
         }
-        const bool fin = (r.flags & SEGF_FINAL) != 0;
-        const bool err = (r.flags & ~SEGF_FINAL) != 0;
-        const bool chain = (j + 1 < A.ncand) && r.end_byte == A.cands[j + 1];
-        if (fin) atomicMin(&kmin, (unsigned long long)j);
-        if (err || (!fin && !chain)) atomicMin(&bmin, (unsigned long long)j);
-        if (!fin && r.out_size != size0) atomicMin(&umin, (unsigned long long)j);
     }
     __syncthreads();
     if (t == 0) {
-        const uint64_t k = kmin;
-        res->fin_index = (uint32_t)k;
-        res->exotic = xcnt;
-        if (xmin < A.ncand) {
+        if (kmin != ~0ull) atomicMax(&W->kmin, ~kmin);
+        if (bmin != ~0ull) atomicMax(&W->bmin, ~bmin);
+        if (umin != ~0ull) atomicMax(&W->umin, ~umin);
+        if (xmin != ~0ull) atomicMax(&W->xmin, ~xmin);
+        if (xcnt) atomicAdd(&W->xcnt, xcnt);
+    }
+}
+
+__global__ void k_inflate_validate(InflateArgs A, const ValidateWords* W, InflateResult* res) {
+    auto unmax = [](unsigned long long v) -> uint64_t { return v ? ~v : ~0ull; };
+    const uint64_t k = unmax(W->kmin), bmin = unmax(W->bmin), umin = unmax(W->umin), xmin = unmax(W->xmin);
+    res->fin_index = (uint32_t)k;
+    res->exotic = W->xcnt;
+    if (xmin < A.ncand) {
+        res->status = 1;
+        res->total = 0;
+    } else if (k < A.ncand && bmin > k) {
+        if (A.mode != 1 && umin < k) {
             res->status = 1;
             res->total = 0;
-        } else if (k < A.ncand && bmin > k) {
-            if (A.mode != 1 && umin < k) {
-                res->status = 1;
-                res->total = 0;
-            } else {
-                res->status = 0;
-                res->total = A.recs[k].offset + A.recs[k].out_size;
-            }
         } else {
-            res->total = 0;
-            res->status = 2;
+            res->status = 0;
+            res->total = A.recs[k].offset + A.recs[k].out_size;
         }
+    } else {
+        res->total = 0;
+        res->status = 2;
     }
 }
 
@@ -1023,8 +1039,12 @@ hipError_t launch_inflate_segments(const InflateArgs& A, hipStream_t st, hipEven
     return hipGetLastError();
 }
 
-hipError_t launch_inflate_validate(const InflateArgs& A, InflateResult* res, hipStream_t st) {
-    hipLaunchKernelGGL(k_inflate_validate, dim3(1), dim3(1024), 0, st, A, res);
+hipError_t launch_inflate_validate(const InflateArgs& A, ValidateWords* W, InflateResult* res,
+                                   hipStream_t st) {
+    hipError_t e = hipMemsetAsync(W, 0, sizeof(ValidateWords), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_inflate_validate_scan, dim3((uint32_t)((A.ncand + 255) / 256)), dim3(256), 0, st, A, W);
+    hipLaunchKernelGGL(k_inflate_validate, dim3(1), dim3(1), 0, st, A, (const ValidateWords*)W, res);
     return hipGetLastError();
 }
 
