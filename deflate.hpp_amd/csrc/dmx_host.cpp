@@ -391,7 +391,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     int np = 0;
     r.status = 2;
     if (path_env == -1 || path_env == 4) {
-        const uint64_t words = std::min<uint64_t>(ncand * 32788ull, 8ull * n + 20ull * ncand);
+        const uint64_t words = std::min<uint64_t>(ncand * 16404ull, 8ull * n + 20ull * ncand);  // k_lane_caps
         if (c->ltok.ensure(words * 4) && c->ltokoff.ensure((ncand + 1) * 8) &&
             c->lntok.ensure(ncand * 4) && c->lcaps.ensure(ncand * 4)) {
             plan[np][0] = 4, plan[np][1] = c->seg, np++;

@@ -94,7 +94,7 @@ hipError_t launch_inflate_pj(const InflateArgs& A, uint32_t seg, hipStream_t st,
                              hipEvent_t ev1);
 // lane-per-segment Huffman decode (k_inflate_lanes) + wave-per-segment LZ77 resolve
 // (k_inflate_resolve); segment j lands at j * A.slot (mode 4).  tok holds
-// min(ncand * 32788, 8 * n + 20 * ncand) words; tokoff ncand + 1, ntok / caps ncand entries.
+// min(ncand * 16404, 8 * n + 20 * ncand) words; tokoff ncand + 1, ntok / caps ncand entries.
 hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* tokoff,
                                 uint32_t* ntok, uint32_t* caps, hipStream_t st, hipEvent_t ev0,
                                 hipEvent_t ev1);

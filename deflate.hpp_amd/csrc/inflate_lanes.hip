@@ -536,14 +536,16 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
     }
 }
 
-// token-list capacity per candidate: min(32 KiB of tokens, one per compressed bit) + 16,
-// rounded to whole 16-byte groups
+// token-list capacity per candidate: min(one word per compressed bit, LN_OUT_CAP / 2 + 2) + 16,
+// rounded to whole 16-byte groups.  A segment of at most 32 KiB needs at most 16 Ki + 1 words:
+// a literal-run word holds up to 3 bytes and two consecutive ones hold >= 4 (a short run is
+// followed by a match), a match word >= 3 bytes, so words <= bytes / 2 + 1.
 __global__ void k_lane_caps(const uint64_t* cands, uint64_t ncand, uint64_t n, uint32_t* caps) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= ncand) return;
     const uint64_t nxt = j + 1 < ncand ? cands[j + 1] : n;
     const uint64_t bits = 8 * (nxt - cands[j]);
-    const uint64_t c = min(bits, (uint64_t)LN_OUT_CAP) + 16;
+    const uint64_t c = min(bits, (uint64_t)LN_OUT_CAP / 2 + 2) + 16;
     caps[j] = (uint32_t)((c + 3) & ~3ull);
 }
 

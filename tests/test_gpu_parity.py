@@ -256,3 +256,30 @@ def test_segment_starts_device_index(ctx):
     for off in (0, 1, 3):
         got = ctx.segment_starts_device(t.data_ptr() + 3 - off, len(s) + off)
         assert got == [w + off for w in want], off
+
+
+def test_c4_eight_shards_of_1GiB_mixed_on_one_gpu(ctx, oracle):
+    """Config C4 at per-GPU size: the 1 GiB mixed corpus cut into 8 shards (one
+    per GPU of an 8-GPU node), each deflated NOT_FINAL except the last, the shards concatenated
+    on the device as the RCCL gather would, the whole stream inflated and compared with the
+    input; the first shard's stream (closed with a final empty block) is checked by the oracle."""
+    import torch
+    import shard
+    n, world = 1 << 30, 8
+    host = torch.empty(n, dtype=torch.uint8).pin_memory()
+    dmx.corpus_into("mixed", n, host.data_ptr())
+    d_in = host.cuda()
+    parts = []
+    for r in range(world):
+        b, e = shard.shard_range(n, r, world, 32768)
+        buf = torch.empty(dmx.deflate_bound(e - b) + 64, dtype=torch.uint8, device="cuda")
+        L = ctx.deflate_device(d_in.data_ptr() + b, e - b, 2, buf.data_ptr(), buf.numel(), not_final=(r < world - 1))
+        parts.append(buf[:L])
+    first = parts[0].cpu().numpy().tobytes() + b"\x03\x00"
+    b0, e0 = shard.shard_range(n, 0, world, 32768)
+    assert oracle.inflate(first) == host[b0:e0].numpy().tobytes()
+    full = torch.cat(parts)
+    d_out = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    olen = ctx.inflate_device(full.data_ptr(), full.numel(), d_out.data_ptr(), n + 64)
+    assert olen == n and torch.equal(d_out[:n], d_in)
+    assert ctx.stats().path == 4
