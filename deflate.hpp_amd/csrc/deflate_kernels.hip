@@ -863,8 +863,7 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, const TokRange tr, uint32_t nb, boo
 }
 
 template <int SEG>
-__global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
-    __shared__ DfSmem<SEG> S;
+__device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG>& S) {
     constexpr int NWALK = DfSmem<SEG>::NWALK;
     constexpr int HT = DfSmem<SEG>::HT;
     constexpr int NMAP = SEG / 32;
@@ -1214,6 +1213,19 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
     emit_stored<SEG>(S, nb, is_final, slot, &A.sizes[seg]);
 }
 
+// The 32 KiB kernel is limited to one workgroup per CU by its LDS (~146 KiB), so the compiler may
+// use up to 128 registers; the 16 KiB one fits two workgroups per CU (80 KiB each) only at <= 64
+// registers per lane, which amdgpu_waves_per_eu(8) asks for.
+template <int SEG>
+__global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
+    __shared__ DfSmem<SEG> S;
+    deflate_segment<SEG>(A, S);
+}
+__global__ __launch_bounds__(DF_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_deflate_segments16(DeflateArgs A) {
+    __shared__ DfSmem<16384> S;
+    deflate_segment<16384>(A, S);
+}
+
 // exclusive scan of segment sizes -> offsets (single workgroup of 1024 threads).  Thread t owns
 // the contiguous run [t per, (t + 1) per) and moves it in batches of 32 sizes: eight 16-byte
 // loads issued together (one memory latency per batch), registers summed, a block scan of the
@@ -1312,7 +1324,7 @@ hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t 
     if (seg_bytes == 32768)
         hipLaunchKernelGGL(k_deflate_segments<32768>, dim3((uint32_t)A.nseg), dim3(DF_NT), 0, st, A);
     else
-        hipLaunchKernelGGL(k_deflate_segments<16384>, dim3((uint32_t)A.nseg), dim3(DF_NT), 0, st, A);
+        hipLaunchKernelGGL(k_deflate_segments16, dim3((uint32_t)A.nseg), dim3(DF_NT), 0, st, A);
     if (ev_main1) (void)hipEventRecord(ev_main1, st);
     hipLaunchKernelGGL(k_scan_sizes, dim3(1), dim3(1024), 0, st, A.sizes, A.offsets, A.nseg, A.total);
     hipLaunchKernelGGL(k_compact, dim3((uint32_t)A.nseg), dim3(256), 0, st, A.slots, A.slot_bytes,
