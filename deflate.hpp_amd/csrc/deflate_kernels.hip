@@ -1,33 +1,35 @@
 // deflate_kernels.hip -- MI355X (gfx950) DEFLATE encoder kernels.
 //
-// One 256-thread workgroup compresses one independent segment (16 or 32 KiB) entirely out of
-// LDS, the way the reference compresses one 32 KiB chunk with a fresh LZ77 state
+// One 1024-thread workgroup (16 waves) compresses one independent segment (32 KiB, or 16 KiB)
+// entirely out of LDS, the way the reference compresses one 32 KiB chunk with a fresh LZ77 state
 // (realCompress, /root/reference/include/deflate.hpp:680-752):
 //
 //   load (16 B/lane coalesced)  -> LDS byte image of the segment
-//   match candidates            -> two LDS hash tables, rounds of 1024 positions (one per
-//                                  thread): cand[p] = distance to the first occurrence of p's
-//                                  4-byte prefix earlier in the same round, else to the latest
-//                                  one in earlier rounds   (replaces LZ77::getMatches
-//                                  deflate.hpp:310-383 / getMatchesSlow :268-304)
-//   parse walk                  -> 256-byte chunk per lane, greedy (level 2) or one-step lazy
-//                                  (level 3); matches never cross a chunk edge, so chunks parse
-//                                  independently; token starts -> LDS bitmap
-//   histogram                   -> one bitmap word (32 positions) per thread, LDS atomics
+//   match rounds                -> a fingerprinted {latest, first-in-round} hash table in LDS,
+//                                  rounds of 2048 positions (a consecutive pair per thread):
+//                                  cand[p] = distance to the first occurrence of p's 4-byte key
+//                                  earlier in the same round, else to the latest one in earlier
+//                                  rounds   (replaces LZ77::getMatches deflate.hpp:310-383)
+//   level 3                     -> link rounds of 128 positions and a depth-16 search along the
+//                                  candidate chains   (replaces getMatchesSlow :268-304)
+//   parse walk                  -> 258-byte chunk per quad of lanes, greedy (level 2) or one-step
+//                                  lazy (level 3); matches never cross a chunk edge, so chunks
+//                                  parse independently; token starts -> LDS bitmap
+//   histogram                   -> token ranges balanced over the threads, LDS atomics
 //                                  (constructDynamicHuffmanTree :402-418)
 //   code lengths                -> block-parallel length-limited Huffman
 //                                  (FlatHuffmanTree::generateCodeLengths common.hpp:322-404)
 //   canonical codes             -> (FlatHuffmanTree::construct common.hpp:104-145)
 //   dynamic header              -> parallel RLE of the two code-length sequences, precode
 //                                  (writeDynamicHuffmanTree deflate.hpp:544-626)
-//   bit pack                    -> per-lane bit counts, block scan, per-lane 64-bit
-//                                  accumulators OR-ed into an LDS word image  (compressBuffer
-//                                  deflate.hpp:630-674, Bitstream :80-159)
+//   bit pack                    -> per-thread bit counts, block scan, owned-range word stores into
+//                                  an LDS bit image (compressBuffer deflate.hpp:630-674,
+//                                  Bitstream :80-159)
 //   store                       -> dynamic / fixed / stored, whichever is smallest
 //                                  (deflate.hpp:739-746), then an empty stored block so every
 //                                  segment ends byte-aligned (segments concatenate bytewise).
 //
-// A second kernel scans the per-segment sizes and a third compacts the segment slots.
+// k_scan_sizes scans the per-segment sizes and k_compact concatenates the segment slots.
 #include "dmx_device.h"
 #include "dmx_internal.h"
 
