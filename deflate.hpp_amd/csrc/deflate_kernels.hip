@@ -702,7 +702,6 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, const TokRange tr, uint32_t nb, boo
     block_build_codes<SEG>(S, dbg, seg);
     __syncthreads();
     DMX_PHASE(dbg, seg, 4);
-    DMX_PHASE(dbg, seg, 5);
     const uint32_t dyn_tok = S.sh[32], fix_tok = S.sh[33];
     const uint32_t nlit = max(257u, S.sh[34]), ndist = max(1u, S.sh[35]);
     const uint32_t nall = nlit + ndist;
@@ -748,9 +747,11 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, const TokRange tr, uint32_t nb, boo
     }
     __syncthreads();
     DMX_PHASE(dbg, seg, 6);
-    uint32_t hclen = 4;
-    for (int i = 18; i >= 4; i--)
-        if (S.prelen[kPerm[i]]) { hclen = i + 1; break; }
+    // HCLEN: one past the last nonzero precode length in RFC order, by one ballot per wave
+    const int ln = t & 63;
+    const uint32_t pv = ln < 19 ? S.prelen[kPerm[ln]] : 0u;
+    const uint64_t nzp = __ballot(pv != 0u);
+    const uint32_t hclen = max(4u, nzp ? 64u - (uint32_t)__clzll(nzp) : 0u);
     const uint32_t runbits = isrun ? plan.n18 * (S.prelen[18] + 7) + plan.n17 * (S.prelen[17] + 3) +
                                          plan.n16 * (S.prelen[16] + 2) + plan.nlit * S.prelen[runv]
                                    : 0;
@@ -794,8 +795,13 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, const TokRange tr, uint32_t nb, boo
             bw.put(nlit - 257, 5);
             bw.put(ndist - 1, 5);
             bw.put(hclen - 4, 4);
-            for (uint32_t i = 0; i < hclen; i++) bw.put(S.prelen[kPerm[i]], 3);
         }
+        bw.flush();
+    }
+    if (use_dyn && t < (int)hclen) {  // the precode lengths in RFC order, 3 bits each, in parallel
+        BitOr bw;
+        bw.init(S.U, 17 + 3 * t);
+        bw.put(pv, 3);
         bw.flush();
     }
     if (use_dyn && isrun) {
@@ -827,6 +833,7 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, const TokRange tr, uint32_t nb, boo
         }
         bw.flush();
     }
+    DMX_PHASE(dbg, seg, 5);
     if (tr.n) {
         BitSt bw;
         bw.init(S.U, hdr_end + myoff);
@@ -1189,6 +1196,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
             tr.m = S.tokmap[lo];
             for (uint32_t r = tr.n ? first - S.mmap[lo] : 0u; r; r--) tr.m &= tr.m - 1;
         }
+        DMX_PHASE(A.dbg, seg, 15);
         // ---- histogram over the thread's tokens; the output image is zeroed meanwhile ------
         {
             uint32_t w = tr.w, m = tr.m;
