@@ -67,9 +67,17 @@ constexpr uint32_t DF_L3_ROUND = DMX_L3_ROUND;  // level 3: positions per link-b
 // block primitives
 // ---------------------------------------------------------------------------------------
 
+// threadIdx.x behind an empty volatile asm: the persistent segment loop would otherwise hoist
+// every thread-dependent address of every phase out of the loop (all live at once: spills)
+__device__ __forceinline__ int df_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 // exclusive block scan of one value per thread; returns the prefix, *total gets the sum
 __device__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
-    const int t = threadIdx.x, w = t >> 6;
+    const int t = df_tid(), w = t >> 6;
     const uint32_t inc = wave_incl_scan(v);
     if ((t & 63) == 63) scratch[w] = inc;
     __syncthreads();
@@ -469,7 +477,7 @@ struct DfSmem {
 template <int SEG>
 __device__ void block_build_codes(DfSmem<SEG>& S, uint64_t* dbg, uint64_t seg) {
     static_assert(DF_NT == 1024, "thread layout of block_build_codes");
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int t = df_tid(), lane = t & 63, w = t >> 6;
     const int a = t >= 320 ? 1 : 0;  // alphabet of the symbol thread: 0 lit/len, 1 distance
     const uint32_t s = a ? t - 320 : t;
     const bool sym = a ? (s < 30) : (s < 286);
@@ -605,11 +613,34 @@ __device__ void block_build_codes(DfSmem<SEG>& S, uint64_t* dbg, uint64_t seg) {
     }
 }
 
+// Persistent workgroups: the next segment of this workgroup (seg + gridDim.x) is loaded straight
+// into the LDS byte image (global_load_lds, no registers) once the current segment's bytes are
+// dead -- after the token bits are counted, the emission reads only the candidate array -- so
+// its memory latency passes during the emission and the copy-out.  The loop's closing
+// __syncthreads waits for it (an LDS-DMA load counts on vmcnt).
+template <int SEG>
+__device__ __forceinline__ bool df_prefetch_next(const DeflateArgs& A, uint64_t seg, DfSmem<SEG>& S) {
+    const uint64_t nbase = (seg + gridDim.x) * (uint64_t)SEG;
+    const bool go = seg + gridDim.x < A.nseg && nbase + SEG <= A.n &&
+                    ((reinterpret_cast<uintptr_t>(A.in + nbase) & 15) == 0);
+    if (go) {
+        const int t = df_tid();
+        const uint4* src = reinterpret_cast<const uint4*>(A.in + nbase) + t;
+        // one wave-instruction writes 64 x 16 B contiguously from a wave-uniform LDS base
+        uint4* dst = reinterpret_cast<uint4*>(S.data32) + (t & ~63);
+#pragma unroll
+        for (int k = 0; k < SEG / (16 * DF_NT); k++)
+            __builtin_amdgcn_global_load_lds(src + k * DF_NT, (__attribute__((address_space(3))) void*)(dst + k * DF_NT),
+                                             16, 0, 0);
+    }
+    return go;
+}
+
 // stored block: [BFINAL|00][LEN][NLEN][data] (+ empty stored block unless final)
 template <int SEG>
 __device__ void emit_stored(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t* slot,
                             uint32_t* size_out) {
-    const int t = threadIdx.x;
+    const int t = df_tid();
     __syncthreads();
     const uint32_t total = 5 + nb + (is_final ? 0 : 5);
     const uint32_t nw = (total + 3) / 4;
@@ -694,9 +725,10 @@ __device__ __forceinline__ uint32_t encode_token(DfSmem<SEG>& S, uint32_t p) {
 // Huffman (dynamic or fixed) block for the tokenized segment; returns false when a stored
 // block would be smaller (the caller then emits it), true after writing the slot.
 template <int SEG>
-__device__ bool emit_huffman(DfSmem<SEG>& S, const TokRange tr, uint32_t nb, bool is_final,
-                             uint8_t* slot, uint32_t* size_out, uint64_t* dbg, uint64_t seg) {
-    const int t = threadIdx.x;
+__device__ bool emit_huffman(const DeflateArgs& A, bool& staged, DfSmem<SEG>& S, const TokRange tr,
+                             uint32_t nb, bool is_final, uint8_t* slot, uint32_t* size_out, uint64_t* dbg,
+                             uint64_t seg) {
+    const int t = df_tid();
 
     // ---- code lengths, canonical codes, token cost, HLIT / HDIST (whole block) -----------
     block_build_codes<SEG>(S, dbg, seg);
@@ -785,6 +817,7 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, const TokRange tr, uint32_t nb, boo
     const uint32_t myoff = block_excl_scan(mybits, S.scan, &tok_total);
     const uint32_t hdr_end = 3 + (use_dyn ? hdr_bits : 0);
     DMX_PHASE(dbg, seg, 8);
+    staged = df_prefetch_next<SEG>(A, seg, S);  // the segment's bytes are dead from here
 
     // ---- emission into the zeroed LDS image ---------------------------------------------
     if (t == 0) {
@@ -872,12 +905,12 @@ __device__ bool emit_huffman(DfSmem<SEG>& S, const TokRange tr, uint32_t nb, boo
 }
 
 template <int SEG>
-__device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG>& S) {
+__device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG>& S, uint64_t seg,
+                                                bool& staged) {
     constexpr int NWALK = DfSmem<SEG>::NWALK;
     constexpr int HT = DfSmem<SEG>::HT;
     constexpr int NMAP = SEG / 32;
-    const int t = threadIdx.x;
-    const uint64_t seg = blockIdx.x;
+    const int t = df_tid();
     const uint64_t base = seg * (uint64_t)SEG;
     const uint32_t nb = (uint32_t)min((uint64_t)SEG, A.n - base);
     const bool is_final = (seg + 1 == A.nseg) && A.final_last;
@@ -890,7 +923,8 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
     {
         const uint8_t* src = A.in + base;
         const uint32_t nvec = nb / 16;
-        if ((((uintptr_t)src) & 15) == 0) {
+        if (staged) {  // loaded during the previous segment (df_prefetch_next)
+        } else if ((((uintptr_t)src) & 15) == 0) {
             const uint4* s4 = reinterpret_cast<const uint4*>(src);
             uint4* d4 = reinterpret_cast<uint4*>(S.data32);
             for (uint32_t i = t; i < nvec; i += DF_NT) d4[i] = s4[i];
@@ -908,6 +942,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
     }
     __syncthreads();
     DMX_PHASE(A.dbg, seg, 1);
+    staged = false;
 
     if (level != 0) {
         // ---- match candidates: rounds of 2*DF_NT positions, two per thread ---------------
@@ -1215,7 +1250,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         if (t == 0) atomicAdd(&S.litfreq[256], 1u);  // end-of-block
         __syncthreads();
         DMX_PHASE(A.dbg, seg, 11);
-        if (emit_huffman<SEG>(S, tr, nb, is_final, slot, &A.sizes[seg], A.dbg, seg)) {
+        if (emit_huffman<SEG>(A, staged, S, tr, nb, is_final, slot, &A.sizes[seg], A.dbg, seg)) {
             DMX_PHASE(A.dbg, seg, 10);
             return;
         }
@@ -1226,14 +1261,24 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
 // The 32 KiB kernel is limited to one workgroup per CU by its LDS (~146 KiB), so the compiler may
 // use up to 128 registers; the 16 KiB one fits two workgroups per CU (80 KiB each) only at <= 64
 // registers per lane, which amdgpu_waves_per_eu(8) asks for.
+// Persistent workgroups (as many as fit the GPU at once): workgroup b compresses segments
+// b, b + G, b + 2G, ... and loads each next segment while it works on the current one.
+template <int SEG>
+__device__ __forceinline__ void deflate_segments(const DeflateArgs& A, DfSmem<SEG>& S) {
+    bool staged = false;  // S.data32 already holds the segment's bytes
+    for (uint64_t seg = blockIdx.x; seg < A.nseg; seg += gridDim.x) {
+        deflate_segment<SEG>(A, S, seg, staged);
+        __syncthreads();  // the next segment reuses the LDS (and its prefetch has landed)
+    }
+}
 template <int SEG>
 __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
     __shared__ DfSmem<SEG> S;
-    deflate_segment<SEG>(A, S);
+    deflate_segments<SEG>(A, S);
 }
 __global__ __launch_bounds__(DF_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_deflate_segments16(DeflateArgs A) {
     __shared__ DfSmem<16384> S;
-    deflate_segment<16384>(A, S);
+    deflate_segments<16384>(A, S);
 }
 
 // exclusive scan of segment sizes -> offsets (single workgroup of 1024 threads).  Thread t owns
@@ -1244,7 +1289,7 @@ __global__ __launch_bounds__(DF_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 __global__ __launch_bounds__(1024) void k_scan_sizes(const uint32_t* sizes, uint64_t* offs,
                                                       uint64_t nseg, uint64_t* total) {
     __shared__ uint64_t part[1024];
-    const int t = threadIdx.x;
+    const int t = df_tid();
     const uint64_t per = ((nseg + 1023) / 1024 + 31) & ~31ull;  // multiple of 32
     const uint64_t b = min(nseg, t * per), e = min(nseg, b + per);
     const bool vec = ((reinterpret_cast<uintptr_t>(sizes) | reinterpret_cast<uintptr_t>(offs)) & 15) == 0;
@@ -1330,11 +1375,23 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* slots, uint32_t 
 
 hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t st,
                           hipEvent_t ev_main0, hipEvent_t ev_main1) {
-    if (ev_main0) (void)hipEventRecord(ev_main0, st);
+    // persistent grid: the workgroups that fit at once (CUs x workgroups per CU)
+    int dev = 0, ncu = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (seg_bytes == 32768)
-        hipLaunchKernelGGL(k_deflate_segments<32768>, dim3((uint32_t)A.nseg), dim3(DF_NT), 0, st, A);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_deflate_segments<32768>, DF_NT, 0);
     else
-        hipLaunchKernelGGL(k_deflate_segments16, dim3((uint32_t)A.nseg), dim3(DF_NT), 0, st, A);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_deflate_segments16, DF_NT, 0);
+    const uint64_t fit = (uint64_t)max(ncu, 1) * (uint64_t)max(per, 1);
+    const uint32_t grid = (uint32_t)min(A.nseg, fit);
+    if (ev_main0) (void)hipEventRecord(ev_main0, st);
+    if (grid) {
+        if (seg_bytes == 32768)
+            hipLaunchKernelGGL(k_deflate_segments<32768>, dim3(grid), dim3(DF_NT), 0, st, A);
+        else
+            hipLaunchKernelGGL(k_deflate_segments16, dim3(grid), dim3(DF_NT), 0, st, A);
+    }
     if (ev_main1) (void)hipEventRecord(ev_main1, st);
     hipLaunchKernelGGL(k_scan_sizes, dim3(1), dim3(1024), 0, st, A.sizes, A.offsets, A.nseg, A.total);
     hipLaunchKernelGGL(k_compact, dim3((uint32_t)A.nseg), dim3(256), 0, st, A.slots, A.slot_bytes,

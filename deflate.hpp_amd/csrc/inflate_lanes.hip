@@ -53,6 +53,11 @@ constexpr uint32_t LN_DIST = 1024;
 constexpr uint32_t LN_LENS = 704;
 constexpr uint32_t LN_PRE_BYTES = 128;
 constexpr uint32_t LN_OUT_CAP = 32768;
+// stream quads staged in LDS for a segment's code-length sequence: >= 15 bytes of offset + 553
+// (316 symbols x 14 bits at most) + 8 bytes of read-ahead, below the code-length bytes
+constexpr uint32_t LN_HDR_QUADS = 40;
+typedef uint64_t u64_unaligned __attribute__((aligned(1)));  // gfx950 LDS takes unaligned b64
+static_assert(LN_HDR_QUADS * 16 <= LN_LENS, "header quads overlap the code lengths");
 #ifndef DMX_LN_LANES
 #define DMX_LN_LANES 32
 #endif
@@ -284,15 +289,51 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
     if (dbg) dbg[1] = __builtin_amdgcn_s_memtime();
 
     // ---- code lengths of the dynamic segments, decoded once into bytes (lane-serial) ------------
+    // The sequences come from LDS: the next LN_HDR_QUADS stream quads of every segment go into
+    // its lit/len table area (built only after this), loaded by the whole wave at once -- one
+    // memory latency for all 32 segments, where the register ring's top-ups stalled the wave
+    // once per lane running low (a 300-byte header of a high-ratio segment: 4x the decode time).
+    const uint32_t hq0 = br.wi >> 2;  // stream quad of the area's first byte
+    if (dyn_mask) {
+        const uint64_t b64 = reinterpret_cast<uint64_t>(br.blk);
+        const uint32_t blo = (uint32_t)b64, bhi = (uint32_t)(b64 >> 32);
+        const uint32_t k = min(lane, LN_HDR_QUADS - 1);  // lanes >= LN_HDR_QUADS: not stored
+        u32x4 t[LN_LANES];
+#pragma unroll
+        for (uint32_t s = 0; s < LN_LANES; s++) {  // unconditional: every lane's blk is valid
+            const uint64_t b = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)bhi, s) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)blo, s);
+            const uint32_t q = min((uint32_t)__builtin_amdgcn_readlane((int)hq0, s) + k,
+                                   (uint32_t)__builtin_amdgcn_readlane((int)br.nblk, s) - 1u);
+            t[s] = reinterpret_cast<GUint4*>(b)[q];
+        }
+        if (lane < LN_HDR_QUADS) {
+#pragma unroll
+            for (uint32_t s = 0; s < LN_LANES; s++)
+                *reinterpret_cast<u32x4*>(lds + s * LN_REGION + 16 * lane) = t[s];
+        }
+        wave_sync();
+    }
     if (seg_lane && !flags && btype == 2) {
         uint8_t* const LL = R + LN_LENS;  // lit/len lengths [0, 288), distance [288, 320)
+        const uint32_t* const H = reinterpret_cast<const uint32_t*>(R);  // stream words from 4 hq0
+        const uint32_t hw0 = 4 * hq0;
         uint32_t i = 0, prev = 0;
         bool prevok = false;
         const uint32_t total = hlit + hdist;
+        uint32_t nxt = H[br.wi - hw0];  // the word at br.wi, read one step ahead
         // one precode symbol per step, outcome by selects (short-circuit && would branch)
         while (!flags && i < total) {
-            if (__any(br.low())) br.topup();
-            br.ensure(14);  // a precode code (<= 7 bits) and its repeat bits (<= 7)
+            {   // >= 14 bits buffered: a precode code (<= 7 bits) and its repeat bits (<= 7)
+                const bool need = br.nb < 14;
+                const uint32_t wb = br.wi * 4;
+                const uint32_t rem = min(max(br.E, wb) - wb, 4u);  // stream bytes left in the word
+                const uint32_t w = nxt & (uint32_t)((1ull << (8 * rem)) - 1ull);
+                br.bb |= need ? (uint64_t)w << br.nb : 0ull;
+                br.nb += need ? 32u : 0u;
+                br.wi += need ? 1u : 0u;
+                nxt = H[min(br.wi - hw0, 4 * LN_HDR_QUADS - 1)];
+            }
             const uint32_t e = PRE[(uint32_t)(br.bb & 127)];
             const uint32_t len = e >> 5, sym = e & 31;
             const uint32_t ex = sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u;
@@ -309,9 +350,12 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             prev = lit ? sym : prev;
             const uint32_t at = inl ? i : 288 + (i - hlit);
             const uint32_t nw = ((val != 0u) & !bad) ? run : 0u;  // <= 6 bytes (a 16 repeats <= 6)
-#pragma unroll
-            for (uint32_t r = 0; r < 6; r++)
-                if (r < nw) LL[at + r] = (uint8_t)val;
+            if (nw) {  // one unaligned 8-byte store: val x nw, then zeros over positions not yet
+                       // decoded (zero runs are skipped, the lengths start zeroed); at + 7 stays
+                       // inside the region (distance lengths end at 320 + 7 < 1152 - LN_LENS)
+                const uint64_t rep = (uint64_t)val * 0x0101010101010101ull;
+                *reinterpret_cast<u64_unaligned*>(LL + at) = rep & ((1ull << (8 * nw)) - 1ull);
+            }
             i += run;
             flags |= bad ? (uint32_t)SEGF_EXOTIC : 0u;
         }
