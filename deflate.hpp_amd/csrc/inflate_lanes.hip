@@ -685,8 +685,13 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
     uint64_t* const dbg = (A.dbg && lane == 0) ? A.dbg + j * kPhaseSlots : nullptr;
     if (dbg) dbg[5] = __builtin_amdgcn_s_memtime();
     uint32_t pos = 0, n_cx = 0;
+    uint32_t wnext = tk[min(lane, n - 1)];
     for (uint32_t t0 = 0; t0 < n; t0 += 64) {
-        const uint32_t w = t0 + lane < n ? tk[t0 + lane] : 0u;
+        // this step's 64 token words were loaded one step ahead: the memory latency of the next
+        // step's load passes while this step's copies run (unconditional, index clamped, so the
+        // wait before the use is for the older load only)
+        const uint32_t w = t0 + lane < n ? wnext : 0u;
+        wnext = tk[min(t0 + 64 + lane, n - 1)];
         const bool ism = (w >> 31) != 0;
         const uint32_t L = ism ? (w >> 15) & 0xFFFFu : (w >> 24) & 0x7Fu;
         const uint32_t d = (w & 0x7FFFu) + 1;
