@@ -450,11 +450,11 @@ struct DfSmem {
     uint32_t scan[4 * DF_NT / 64];
     uint64_t runmask[6];
     uint32_t sh[48];
-    // block_build_codes: ranks (lit/len at [0, 286), distance at [320, 350)), per-alphabet
-    // class sizes, class start ranks, next canonical code, per-wave length counts, F / used
-    uint32_t hb_rank[352];
-    alignas(16) uint32_t hb_xbuf[2][512];
-    uint32_t hb_cnt[2][16];
+    // block_build_codes: per-wave and per-alphabet sizes of the initial half-classes, class
+    // start ranks, next canonical code, per-wave length counts, F / used
+    uint32_t hb_wcnt0[6][32];
+    uint32_t hb_kcnt[2][32];
+    uint32_t hb_kpre[2][32];
     uint32_t hb_start[2][16];
     uint32_t hb_next[2][16];
     uint32_t hb_wcnt[6][16];
@@ -463,17 +463,18 @@ struct DfSmem {
 };
 
 // Block-parallel code lengths and canonical codes of the lit/len code (286 symbols, threads
-// 0..285) and the distance code (30 symbols, threads 320..349), built side by side.  The
-// lengths are those of the one-wave builder wave_build_lengths64 (and of the 512-key one it
-// replaces): symbols ranked by the key (f << 9 | 511 - s) descending, initial lengths
-// round(log2(F/f)) clamped to [1, maxbits], fit_classes on the class sizes, then lengths by
-// rank (lengths are non-decreasing in rank, so each class is a rank range).  The ranks come
-// from a bitonic sort over 512 threads (one key each) instead of a one-wave sort of 8 keys per
-// lane.  Canonical codes (RFC 1951 3.2.2; reference
-// FlatHuffmanTree::construct common.hpp:104-145) from the final class sizes and per-wave
-// ballots.  Also sums the token cost under the dynamic and the fixed code (sh[32], sh[33]) and
-// finds HLIT / HDIST (sh[34], sh[35]).  Stands in for generateCodeLengths
-// (common.hpp:322-404) and the cost compare of deflate.hpp:739-746.
+// 0..285) and the distance code (30 symbols, threads 320..349), built side by side.  Initial
+// lengths round(log2(F/f)) clamped to [1, maxbits] (init_len), fit_classes on the class sizes,
+// then lengths by rank in the order (initial length, frequency half of the class, symbol): each
+// final class is a rank range, so a Kraft repair lengthens the last symbols of a class and a
+// slack fill shortens the first.  Inside a half-class the frequencies differ by less than
+// sqrt(2), so this order stays close to a frequency sort and needs none: ranks come from
+// per-wave ballots and counts (the 512-key bitonic sort it replaced was 7% of a high-ratio
+// segment's time).
+// Canonical codes (RFC 1951 3.2.2; reference FlatHuffmanTree::construct common.hpp:104-145)
+// from the final class sizes and per-wave ballots.  Also sums the token cost under the dynamic
+// and the fixed code (sh[32], sh[33]) and finds HLIT / HDIST (sh[34], sh[35]).  Stands in for
+// generateCodeLengths (common.hpp:322-404) and the cost compare of deflate.hpp:739-746.
 template <int SEG>
 __device__ void block_build_codes(DfSmem<SEG>& S, uint64_t* dbg, uint64_t seg) {
     static_assert(DF_NT == 1024, "thread layout of block_build_codes");
@@ -485,7 +486,7 @@ __device__ void block_build_codes(DfSmem<SEG>& S, uint64_t* dbg, uint64_t seg) {
     const uint32_t f = sym ? freq[s] : 0;
     const int maxbits = a ? DF_DIST_MAXBITS : DF_LIT_MAXBITS;
     const uint64_t ltmask = (1ull << lane) - 1ull;
-    if (t < 32) S.hb_cnt[t >> 4][t & 15] = 0;
+    if (t < 64) S.hb_kcnt[t >> 5][t & 31] = 0;
     if (t < 4) { S.hb_sum[t] = 0; S.sh[32 + t] = 0; }
     if (t < 2) S.hb_used[t] = 0;
     __syncthreads();
@@ -498,53 +499,27 @@ __device__ void block_build_codes(DfSmem<SEG>& S, uint64_t* dbg, uint64_t seg) {
             atomicMax(&S.hb_used[a], (uint32_t)((w - 5 * a) * 64 + 64 - __clzll(nzm)));
         }
     }
-    {   // ranks by a bitonic sort of the keys (f << 9 | 511 - s), descending: lit/len keys on
-        // threads 0..511 (exchanges at strides >= 64 through LDS, one barrier each), distance
-        // keys on wave 8 (strides < 64 only; later stages leave its sorted run as it is)
-        const bool lk = t < 512, dk = t >= 512 && t < 576;
-        const uint32_t i = lk ? (uint32_t)t : (uint32_t)lane;
-        const uint32_t ks = lk ? (uint32_t)t : (uint32_t)lane;
-        const uint32_t kf = lk ? (ks < 286 ? S.litfreq[ks] : 0u) : (dk && ks < 30 ? S.distfreq[ks] : 0u);
-        uint32_t key = kf ? (kf << 9) | (511 - ks) : 0u;
-        int par = 0;
-#pragma unroll
-        for (int size = 2; size <= 512; size <<= 1) {
-#pragma unroll
-            for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                uint32_t o;
-                switch (stride) {
-                    case 1: o = xor_lane<1>(key); break;
-                    case 2: o = xor_lane<2>(key); break;
-                    case 4: o = xor_lane<4>(key); break;
-                    case 8: o = xor_lane<8>(key); break;
-                    case 16: o = xor_lane<16>(key); break;
-                    case 32: o = xor_lane<32>(key); break;
-                    default: {
-                        uint32_t* xb = S.hb_xbuf[par];
-                        par ^= 1;
-                        if (lk) xb[t] = key;
-                        __syncthreads();
-                        o = lk ? xb[t ^ stride] : key;
-                    }
-                }
-                const bool lower = (i & (uint32_t)stride) == 0, desc = (i & (uint32_t)size) == 0;
-                key = (lower == desc) ? max(key, o) : min(key, o);
-            }
-        }
-        if (key && (lk || dk)) S.hb_rank[(lk ? 0u : 320u) + 511 - (key & 511)] = i;
-    }
     __syncthreads();
     DMX_PHASE(dbg, seg, 12);
     const uint32_t nz = S.hb_sum[2 * a + 1];
-    if (t < 384) {  // class sizes of the initial lengths: lane k adds the wave's count of class k
-        const uint32_t L0 = sym ? init_len(f, S.hb_sum[2 * a], maxbits) : 0;
+    // class sizes of the initial lengths (lane k adds the wave's count of class k), per-wave
+    // class counts, and each symbol's rank among the wave's symbols of its class
+    // Symbols are ordered by half-classes k = 2 L0 + (f <= F / 2^L0): inside a class of initial
+    // length L0 the more frequent half comes first, then symbol order.
+    const uint32_t Fa = S.hb_sum[2 * a];
+    const uint32_t L0 = (t < 384 && sym) ? init_len(f, Fa, maxbits) : 0u;
+    const uint32_t k0 = L0 ? 2 * L0 + (((uint64_t)f << L0) <= Fa ? 1u : 0u) : 0u;
+    uint32_t within0 = 0;
+    if (t < 384) {
         uint32_t mine = 0;
 #pragma unroll
-        for (int L = 1; L <= 15; L++) {
-            const uint32_t c = __popcll(__ballot(L0 == (uint32_t)L));
-            mine = lane == L ? c : mine;
+        for (int k = 2; k <= 2 * DF_LIT_MAXBITS + 1; k++) {
+            const uint64_t b = __ballot(k0 == (uint32_t)k);
+            mine = lane == k ? (uint32_t)__popcll(b) : mine;
+            within0 = k0 == (uint32_t)k ? (uint32_t)__popcll(b & ltmask) : within0;
         }
-        if (mine) atomicAdd(&S.hb_cnt[a][lane], mine);
+        if (mine) atomicAdd(&S.hb_kcnt[a][lane], mine);
+        if (lane < 32) S.hb_wcnt0[w][lane] = mine;
     }
     __syncthreads();
     if (t == 0 || t == 320) {  // Kraft repair / slack fill on the class sizes, class starts,
@@ -552,7 +527,8 @@ __device__ void block_build_codes(DfSmem<SEG>& S, uint64_t* dbg, uint64_t seg) {
         uint32_t cnt[17];
         cnt[0] = cnt[16] = 0;
 #pragma unroll
-        for (int L = 1; L <= 15; L++) cnt[L] = nz > 1 ? S.hb_cnt[a][L] : (L == 1 ? 2u : 0u);
+        for (int L = 1; L <= 15; L++)
+            cnt[L] = nz > 1 ? S.hb_kcnt[a][2 * L] + S.hb_kcnt[a][2 * L + 1] : (L == 1 ? 2u : 0u);
         if (nz > 1) fit_classes(cnt, maxbits);
         uint32_t st = 0, code = 0;
 #pragma unroll
@@ -563,13 +539,20 @@ __device__ void block_build_codes(DfSmem<SEG>& S, uint64_t* dbg, uint64_t seg) {
             S.hb_next[a][L] = code;
         }
     }
+    if (w == 2 || w == 3) {  // meanwhile: half-class start ranks (exclusive scans), one wave each
+        const uint32_t ka = w - 2, v = lane < 32 ? S.hb_kcnt[ka][lane] : 0u;
+        if (lane < 32) S.hb_kpre[ka][lane] = wave_incl_scan(v) - v;
+    }
     __syncthreads();
     DMX_PHASE(dbg, seg, 13);
     uint32_t L = 0;
     if (sym) {
         if (nz > 1) {
             if (f) {
-                const uint32_t q = S.hb_rank[t];
+                // rank in the order (initial length, symbol): symbols of shorter classes, the
+                // class members on earlier waves of the alphabet, then those below on this wave
+                uint32_t q = within0 + S.hb_kpre[a][k0];
+                for (int v = a ? 5 : 0; v < w; v++) q += S.hb_wcnt0[v][k0];
 #pragma unroll
                 for (int l = 1; l <= 15; l++) L += q >= S.hb_start[a][l] ? 1u : 0u;
             }
