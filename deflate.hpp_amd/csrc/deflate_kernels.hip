@@ -438,6 +438,7 @@ struct DfSmem {
     alignas(16) uint32_t U[UW];
     uint32_t mmap[SEG / 32];    // "a verified match of >= 3 starts here" (match rounds)
     uint32_t tokmap[SEG / 32];  // token-start bitmap (parse walk; chunks share boundary words)
+    uint16_t lasttok[NWALK + 1];  // last token start of each parse chunk
     alignas(16) uint32_t litfreq[288];  // 16-B aligned: the rank count reads 4 at a time
     alignas(16) uint32_t distfreq[32];
     uint32_t prefreq[32];
@@ -1120,7 +1121,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
             auto full_len = [&](uint32_t q) -> uint32_t {  // < 3 only on a fingerprint collision
                 return matchlen4(S.data32, q, q - S.cand[q], min(258u, hi - q), sub);
             };
-            uint32_t p = lo, w = lo >> 5, mw = S.mmap[w], tok = 0;
+            uint32_t p = lo, w = lo >> 5, mw = S.mmap[w], tok = 0, lastp = lo;  // lastp: last token
             auto mbit = [&](uint32_t q) -> bool {
                 return (S.mmap[q >> 5] >> (q & 31)) & 1u;
             };
@@ -1137,11 +1138,13 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                 if (q >= hi || !m) {  // literals to the end of the word (or chunk)
                     const uint32_t e = min((w + 1) * 32, hi);
                     tok |= bits_range(p, e, w);
+                    lastp = e - 1;
                     p = e;
                     continue;
                 }
                 tok |= bits_range(p, q, w);  // literals before the match
                 p = q;
+                lastp = p;
                 uint32_t L = full_len(p);
                 if (L < 3) {  // fingerprint collision, not a match: a literal
                     tok |= 1u << (p & 31);
@@ -1181,6 +1184,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                 p += L;
             }
             if (tok && lead) atomicOr(&S.tokmap[w], tok);
+            if (lead) S.lasttok[t >> 2] = (uint16_t)lastp;
         }
         if (level < 2) {  // Huffman only: every position is a literal token
             for (uint32_t i = t; i < nb; i += DF_NT) S.cand[i] = 0;
@@ -1191,6 +1195,72 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         }
         __syncthreads();
         DMX_PHASE(A.dbg, seg, 3);
+
+        // ---- chunk-edge fix-up: matches cross the parse-chunk edges --------------------------
+        // The walk clips every match at its chunk's end.  Per edge (one quad each): when the
+        // last token of the chunk before it is a match clipped at the edge, its full length at
+        // the same distance is measured; if it ends inside a match q of the next chunk's parse,
+        // q's remainder (a suffix of a verified match: no compare) or 1..2 literals follow, and
+        // the next parse resumes unchanged after q.  Committed when that takes fewer tokens.
+        // The extension ends before the next chunk's last token (so does q's match), so every
+        // edge's rewrite stays inside [last token of chunk c, last token of chunk c + 1) and the
+        // edges are independent.
+        if (level >= 2) {
+            const uint32_t sub = t & 3, c = t >> 2;
+            const uint32_t hb = (c + 1) * DF_CHUNK;  // the edge
+            if (t < 4 * (NWALK - 1) && hb < nb) {
+                const uint32_t s0 = S.lasttok[c], d0 = S.cand[s0], L0 = S.cand[s0 + 1];
+                const uint32_t sn = S.lasttok[c + 1];  // the extension ends before it
+                if (d0 != 0 && s0 + L0 == hb && L0 < 258 && sn >= hb + 2) {
+                    const uint32_t Lx = matchlen4(S.data32, s0, s0 - d0, min(258u, sn - 1 - s0), sub);
+                    const uint32_t e = s0 + Lx;  // < sn
+                    uint32_t q = 0;
+                    if (Lx > L0) {  // the next chunk's token at or before e (before sn)
+                        uint32_t w = e >> 5;
+                        uint32_t m = S.tokmap[w] & (0xFFFFFFFFu >> (31 - (e & 31)));
+                        while (!m) m = S.tokmap[--w];
+                        q = w * 32 + 31 - (uint32_t)__clz(m);
+                    }
+                    if (Lx > L0 && sub == 0) {
+                        const uint32_t dq = S.cand[q], Lq = q == e ? 0u : S.cand[q + 1];
+                        const uint32_t r = q == e ? 0u : q + Lq - e;  // q's bytes from e on
+                        const uint32_t sync = q == e ? e : q + Lq;
+                        uint32_t old = 0;  // tokens now in [s0, sync)
+                        for (uint32_t wi = s0 >> 5; wi <= (sync - 1) >> 5; wi++) {
+                            const uint32_t a = max(s0, wi * 32) - wi * 32, z = min(sync, wi * 32 + 32) - wi * 32;
+                            const uint32_t rm = (z >= 32 ? 0xFFFFFFFFu : ((1u << z) - 1u)) & (0xFFFFFFFFu << a);
+                            old += (uint32_t)__popc(S.tokmap[wi] & rm);
+                        }
+                        const uint32_t nt = 1 + (r >= 3 ? 1u : r);
+                        if (nt < old) {
+                            // new token starts: s0 (kept), e (and e + 1 for two literals)
+                            uint32_t nb0 = 0, nb1 = 0;  // bits of e, e + 1
+                            if (r) {
+                                atomicOr(&S.tokmap[e >> 5], 1u << (e & 31));
+                                if (r == 2) atomicOr(&S.tokmap[(e + 1) >> 5], 1u << ((e + 1) & 31));
+                            }
+                            S.cand[s0 + 1] = (uint16_t)Lx;
+                            if (r >= 3) {
+                                S.cand[e] = (uint16_t)dq;
+                                S.cand[e + 1] = (uint16_t)r;
+                            } else if (r) {
+                                S.cand[e] = 0;
+                                if (r == 2) S.cand[e + 1] = 0;
+                            }
+                            for (uint32_t wi = s0 >> 5; wi <= (sync - 1) >> 5; wi++) {
+                                const uint32_t a = max(s0, wi * 32) - wi * 32, z = min(sync, wi * 32 + 32) - wi * 32;
+                                const uint32_t rm = (z >= 32 ? 0xFFFFFFFFu : ((1u << z) - 1u)) & (0xFFFFFFFFu << a);
+                                nb0 = (s0 >> 5) == wi ? 1u << (s0 & 31) : 0u;
+                                nb1 = (r && (e >> 5) == wi ? 1u << (e & 31) : 0u) |
+                                      (r == 2 && ((e + 1) >> 5) == wi ? 1u << ((e + 1) & 31) : 0u);
+                                atomicAnd(&S.tokmap[wi], ~rm | nb0 | nb1);
+                            }
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
 
         // ---- token ranges (TokRange): per-word token counts, block scan into the match
         //      bitmap (dead after the parse), binary search for the thread's first token ------
@@ -1211,8 +1281,17 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                 else hi = mid;
             }
             tr.w = lo;
-            tr.m = S.tokmap[lo];
-            for (uint32_t r = tr.n ? first - S.mmap[lo] : 0u; r; r--) tr.m &= tr.m - 1;
+            // drop the word's first r tokens: the r-th set bit by a 5-step popcount search
+            const uint32_t m = S.tokmap[lo];
+            uint32_t b = 0, k = tr.n ? first - S.mmap[lo] : 0u;
+#pragma unroll
+            for (uint32_t sh = 16; sh >= 1; sh >>= 1) {
+                const uint32_t c = (uint32_t)__popc((m >> b) & ((1u << sh) - 1u));
+                const bool up = k >= c;
+                b += up ? sh : 0u;
+                k -= up ? c : 0u;
+            }
+            tr.m = m & (0xFFFFFFFFu << b);
         }
         DMX_PHASE(A.dbg, seg, 15);
         // ---- histogram over the thread's tokens; the output image is zeroed meanwhile ------

@@ -56,7 +56,10 @@ constexpr uint32_t LN_OUT_CAP = 32768;
 // stream quads staged in LDS for a segment's code-length sequence: >= 15 bytes of offset + 553
 // (316 symbols x 14 bits at most) + 8 bytes of read-ahead, below the code-length bytes
 constexpr uint32_t LN_HDR_QUADS = 40;
-typedef uint64_t u64_unaligned __attribute__((aligned(1)));  // gfx950 LDS takes unaligned b64
+// gfx950 LDS takes unaligned 2-, 4- and 8-byte accesses
+typedef uint64_t u64_unaligned __attribute__((aligned(1)));
+typedef uint32_t u32_unaligned __attribute__((aligned(1)));
+typedef uint16_t u16_unaligned __attribute__((aligned(1)));
 static_assert(LN_HDR_QUADS * 16 <= LN_LENS, "header quads overlap the code lengths");
 #ifndef DMX_LN_LANES
 #define DMX_LN_LANES 32
@@ -620,6 +623,27 @@ __device__ __forceinline__ void ln_copy_plain(uint8_t* win, uint32_t o, uint32_t
     }
 }
 
+// 8 bytes of the window at byte a (a < LN_OUT_CAP); near the window's end the read is moved
+// back inside it and shifted (only bytes below the end are used)
+__device__ __forceinline__ uint64_t ln_rd8(const uint8_t* win, uint32_t a) {
+    const uint32_t c = min(a, LN_OUT_CAP - 8);
+    return *reinterpret_cast<const u64_unaligned*>(win + c) >> (8 * (a - c));
+}
+// the low r (1..7) bytes of x at q
+__device__ __forceinline__ void ln_store_tail(uint8_t* q, uint64_t x, uint32_t r) {
+    if (r & 4) {
+        *reinterpret_cast<u32_unaligned*>(q) = (uint32_t)x;
+        q += 4;
+        x >>= 32;
+    }
+    if (r & 2) {
+        *reinterpret_cast<u16_unaligned*>(q) = (uint16_t)x;
+        q += 2;
+        x >>= 16;
+    }
+    if (r & 1) *q = (uint8_t)x;
+}
+
 // periodic copy out[o + i] = out[o - d + (i mod d)], i < L (the reference's byte-serial
 // overlapping copy, inflate.hpp:268-270): the first period (or, for d < 64, the largest
 // multiple of d that fits one byte per lane) is built directly; after that the P bytes already
@@ -685,6 +709,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
     uint64_t* const dbg = (A.dbg && lane == 0) ? A.dbg + j * kPhaseSlots : nullptr;
     if (dbg) dbg[5] = __builtin_amdgcn_s_memtime();
     uint32_t pos = 0, n_cx = 0;
+    uint64_t c_simple = 0, c_cx = 0, tstep0 = dbg ? __builtin_amdgcn_s_memtime() : 0;  // DMX_PHASES
     uint32_t wnext = tk[min(lane, n - 1)];
     for (uint32_t t0 = 0; t0 < n; t0 += 64) {
         // this step's 64 token words were loaded one step ahead: the memory latency of the next
@@ -698,15 +723,29 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
         const uint32_t inc = wave_incl_scan(L);
         const uint32_t off = pos + inc - L;
         const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        if (!ism) {
-            if (L > 0) win[off] = (uint8_t)w;
-            if (L > 1) win[off + 1] = (uint8_t)(w >> 8);
-            if (L > 2) win[off + 2] = (uint8_t)(w >> 16);
+        if (!ism) {  // literal run of 1..3 bytes: exact-size stores
+            if (L & 2) {
+                *reinterpret_cast<u16_unaligned*>(win + off) = (uint16_t)w;
+                if (L & 1) win[off + 2] = (uint8_t)(w >> 16);
+            } else if (L) {
+                win[off] = (uint8_t)w;
+            }
         }
         // short matches whose source lies before this step: each lane copies its own
         const bool simple = ism && L <= 32 && off + min(L, d) <= pos + d;
         if (simple) {
-            if (d >= 4) {
+            if (d >= L) {  // the whole source is final: read it at once (one LDS latency, not one
+                           // per word), store exactly L bytes (neighbouring tokens store beside it)
+                uint64_t v[4];
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++) v[k] = 8 * k < L ? ln_rd8(win, off - d + 8 * k) : 0ull;
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++) {
+                    const uint32_t b = 8 * k;
+                    if (b + 8 <= L) *reinterpret_cast<u64_unaligned*>(win + off + b) = v[k];
+                    else if (b < L) ln_store_tail(win + off + b, v[k], L - b);
+                }
+            } else if (d >= 4) {
                 for (uint32_t i = 0; i < L; i += 4) {
                     const uint32_t v = ld32u(reinterpret_cast<const uint32_t*>(win), off + i - d);
                     win[off + i] = (uint8_t)v;
@@ -720,6 +759,11 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
         }
         wave_sync();
         uint64_t m = __ballot(ism && !simple);
+        uint64_t tcx0 = 0;
+        if (dbg) {
+            tcx0 = __builtin_amdgcn_s_memtime();
+            c_simple += tcx0 - tstep0;
+        }
         while (m) {
             const int k = __builtin_ctzll(m);
             m &= m - 1;
@@ -730,11 +774,17 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
             wave_sync();
             n_cx++;
         }
+        if (dbg) {
+            tstep0 = __builtin_amdgcn_s_memtime();
+            c_cx += tstep0 - tcx0;
+        }
         pos += tot;
     }
     if (dbg) {
         dbg[6] = __builtin_amdgcn_s_memtime();
         dbg[12] = n_cx;
+        dbg[13] = c_simple;
+        dbg[14] = c_cx;
     }
     if ((((uintptr_t)dst) & 15) == 0) {
         const uint32_t nv = nb / 16;
