@@ -1168,8 +1168,30 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                     const uint32_t c = S.cand[p];
                     const uint32_t ml = min(258u, hi - p);
                     uint32_t best = c;
-                    for (uint32_t dd = 1; dd <= 4 && dd < best; dd++)
-                        if (dd <= p && matchlen4(S.data32, p, p - dd, ml, sub) >= L) best = dd;
+                    {   // periods 1..4: one 16-byte compare round (lane sub tests 1 + sub), then
+                        // full lengths only for the periods that passed, shortest first
+                        const uint32_t dd = 1 + sub;
+                        bool pass = false;
+                        if (dd < c && dd <= p) {
+                            const uint32_t ip = p >> 2, sp = p & 3, iq = (p - dd) >> 2, sq = (p - dd) & 3;
+                            uint32_t x = 0;
+#pragma unroll
+                            for (int k = 0; k < 4; k++)
+                                x |= __builtin_amdgcn_alignbyte(S.data32[ip + k + 1], S.data32[ip + k], sp) ^
+                                     __builtin_amdgcn_alignbyte(S.data32[iq + k + 1], S.data32[iq + k], sq);
+                            pass = x == 0;
+                        }
+                        const int qb = lane_id() & ~3;
+                        uint32_t pm = (uint32_t)(__ballot(pass) >> qb) & 0xFu;
+                        while (pm) {
+                            const uint32_t d1 = 1 + (uint32_t)__builtin_ctz(pm);
+                            pm &= pm - 1;
+                            if (matchlen4(S.data32, p, p - d1, ml, sub) >= L) {
+                                best = d1;
+                                break;
+                            }
+                        }
+                    }
                     if (best == c) {  // one probe at c / k, k the largest divisor <= 8 (a probe
                                       // per k would serialize across lanes that differ in k)
                         uint32_t k = 1;
