@@ -1017,7 +1017,10 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                     if (pok0 && ph0 != (pok1 ? ph1 : NOH)) atomicMax(&S.U[2 * ph0], ((pp0 + 1) << 16) | pf0);
                     if (pok1 && ph1 != hn) atomicMax(&S.U[2 * ph1], ((pp0 + 2) << 16) | pf1);
                     __syncthreads();
-                    const uint2 e0 = tab[ok0 ? h0 : 0u], e1 = tab[ok1 ? h1 : 0u];
+                    uint2 e0 = tab[ok0 ? h0 : 0u], e1 = tab[ok1 ? h1 : 0u];
+                    // both halves now: otherwise the compiler sinks the head half of e0 into the
+                    // not-first-in-round branch, a second LDS round trip after the first
+                    asm volatile("" : "+v"(e0.x), "+v"(e0.y), "+v"(e1.x), "+v"(e1.y));
                     auto pick = [&](uint2 e, uint32_t p, uint32_t fa, bool ok) -> uint32_t {
                         const uint32_t f = e.y, hd = e.x;
                         const uint32_t q = 0x7FFFu - ((f >> 13) & 0x7FFFu);
