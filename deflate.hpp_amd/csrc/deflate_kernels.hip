@@ -994,28 +994,38 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                     __syncthreads();
                 }
             } else {
-                for (uint32_t r0 = 0, rr = 0; r0 < nb; r0 += 2 * DF_NT, rr++) {
+                // One round; cur receives this round's hashes for the next round's latest-occurrence
+                // updates, prev holds the previous round's.  Rounds go in pairs with the two states
+                // swapping roles (no register copies), and rounds that lie wholly inside the
+                // segment skip the bounds tests (`full`, a constant in each call).
+                struct RoundState {
+                    uint32_t h0, h1, p0, f0, f1;
+                    bool ok0, ok1;
+                };
+                auto round = [&](uint32_t r0, uint32_t rr, RoundState& cur, const RoundState& prev, auto full) {
+                    constexpr bool FULL = decltype(full)::value;
                     const uint32_t p0 = r0 + 2 * t, p1 = p0 + 1;
                     const uint32_t i0 = p0 >> 2, sh = p0 & 3;  // sh = 0 or 2
                     const uint32_t wa = S.data32[i0], wb = S.data32[i0 + 1];
                     const uint32_t prod0 = __builtin_amdgcn_alignbyte(wb, wa, sh) * 0x1E35A7BDu;
                     const uint32_t prod1 = __builtin_amdgcn_alignbyte(wb, wa, sh + 1) * 0x1E35A7BDu;
-                    const bool ok0 = p0 + 4 <= nb, ok1 = p1 + 4 <= nb;
+                    const bool ok0 = FULL || p0 + 4 <= nb, ok1 = FULL || p1 + 4 <= nb;
                     const uint32_t h0 = ok0 ? prod0 >> (32 - HB) : NOH, h1 = ok1 ? prod1 >> (32 - HB) : NOH;
                     const uint32_t fa0 = (prod0 >> (32 - HB - 16)) & 0xFFFFu, fa1 = (prod1 >> (32 - HB - 16)) & 0xFFFFu;
-                    // first occurrence in this round: p1 needs no update when p0 has its hash, p0 none
-                    // when p0 - 1 (the previous lane's p1, by DPP within rows of 16) has it
+                    // first occurrence in this round: p1 needs no update when p0 has its hash, p0
+                    // none when p0 - 1 (the previous lane's p1, by DPP within rows of 16) has it
                     const uint32_t hl = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)h1, 0x111, 0xF, 0xF, false);
                     const uint32_t rtag = rr << 28;
                     if (ok0 && h0 != hl)
                         atomicMax(&S.U[2 * h0 + 1], rtag | ((0x7FFFu - p0) << 13) | (fa0 >> 3));
                     if (ok1 && h1 != h0)
                         atomicMax(&S.U[2 * h1 + 1], rtag | ((0x7FFFu - p1) << 13) | (fa1 >> 3));
-                    // latest occurrence, for the previous round's positions: pp0 needs no update when
-                    // pp0 + 1 has its hash, pp0 + 1 none when pp0 + 2 (the next lane's) has it
-                    const uint32_t hn = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)(pok0 ? ph0 : NOH), 0x101, 0xF, 0xF, false);
-                    if (pok0 && ph0 != (pok1 ? ph1 : NOH)) atomicMax(&S.U[2 * ph0], ((pp0 + 1) << 16) | pf0);
-                    if (pok1 && ph1 != hn) atomicMax(&S.U[2 * ph1], ((pp0 + 2) << 16) | pf1);
+                    // latest occurrence, for the previous round's positions: its p0 needs no update
+                    // when its p0 + 1 has the hash, p0 + 1 none when p0 + 2 (the next lane's) has it
+                    const uint32_t hn = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)(prev.ok0 ? prev.h0 : NOH), 0x101, 0xF, 0xF, false);
+                    if (prev.ok0 && prev.h0 != (prev.ok1 ? prev.h1 : NOH))
+                        atomicMax(&S.U[2 * prev.h0], ((prev.p0 + 1) << 16) | prev.f0);
+                    if (prev.ok1 && prev.h1 != hn) atomicMax(&S.U[2 * prev.h1], ((prev.p0 + 2) << 16) | prev.f1);
                     __syncthreads();
                     uint2 e0 = tab[ok0 ? h0 : 0u], e1 = tab[ok1 ? h1 : 0u];
                     // both halves now: otherwise the compiler sinks the head half of e0 into the
@@ -1029,15 +1039,23 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                         const uint32_t c = fr ? p - q : (lt ? p + 1u - (hd >> 16) : 0u);
                         return ok ? c : 0u;
                     };
-                    if (p0 < nb) cand32[p0 >> 1] = pick(e0, p0, fa0, ok0) | (pick(e1, p1, fa1, ok1) << 16);
-                    ph0 = h0;
-                    ph1 = h1;
-                    pp0 = p0;
-                    pf0 = fa0;
-                    pf1 = fa1;
-                    pok0 = ok0;
-                    pok1 = ok1;
+                    if (FULL || p0 < nb) cand32[p0 >> 1] = pick(e0, p0, fa0, ok0) | (pick(e1, p1, fa1, ok1) << 16);
+                    cur = RoundState{h0, h1, p0, fa0, fa1, ok0, ok1};
                     __syncthreads();
+                };
+                using Full = std::integral_constant<bool, true>;
+                using Part = std::integral_constant<bool, false>;
+                RoundState A = {0, 0, 0, 0, 0, false, false}, B = A;
+                uint32_t r0 = 0, rr = 0;
+                for (; r0 + 4 * DF_NT + 3 <= nb; r0 += 4 * DF_NT, rr += 2) {  // two full rounds
+                    round(r0, rr, A, B, Full{});
+                    round(r0 + 2 * DF_NT, rr + 1, B, A, Full{});
+                }
+                for (; r0 < nb; r0 += 2 * DF_NT, rr++) {  // the rest (the last may be partial)
+                    round(r0, rr, A, B, Part{});
+                    const RoundState x = A;
+                    A = B;
+                    B = x;
                 }
             }
             DMX_PHASE(A.dbg, seg, 14);
