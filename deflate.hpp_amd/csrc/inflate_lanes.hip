@@ -790,7 +790,15 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
         const uint32_t nv = nb / 16;
         const uint4* s4 = reinterpret_cast<const uint4*>(win);
         uint4* d4 = reinterpret_cast<uint4*>(dst);
-        for (uint32_t i = lane; i < nv; i += 64) d4[i] = s4[i];
+        uint32_t i = lane;
+        for (; i + 192 < nv; i += 256) {  // four 16-byte LDS reads in flight per lane
+            const uint4 v0 = s4[i], v1 = s4[i + 64], v2 = s4[i + 128], v3 = s4[i + 192];
+            d4[i] = v0;
+            d4[i + 64] = v1;
+            d4[i + 128] = v2;
+            d4[i + 192] = v3;
+        }
+        for (; i < nv; i += 64) d4[i] = s4[i];
         for (uint32_t i = nv * 16 + lane; i < nb; i += 64) dst[i] = win[i];
     } else {
         for (uint32_t i = lane; i < nb; i += 64) dst[i] = win[i];
