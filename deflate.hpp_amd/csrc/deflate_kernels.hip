@@ -1489,7 +1489,7 @@ hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t 
     else
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_deflate_segments16, DF_NT, 0);
     const uint64_t fit = (uint64_t)max(ncu, 1) * (uint64_t)max(per, 1);
-    const uint32_t grid = (uint32_t)min(A.nseg, fit);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(A.nseg, fit);  // host min(int, int) would truncate
     if (ev_main0) (void)hipEventRecord(ev_main0, st);
     if (grid) {
         if (seg_bytes == 32768)

@@ -64,7 +64,7 @@ struct dmx_ctx {
     DevBuf ltok, ltokoff, lntok, lcaps;  // lane decoder token lists (mode 4)
     // block-parallel path (path 5): scan counts / hits / offsets, hit list, unit starts, token
     // offsets and words, unit records, chain (unit index, offset, size), 16-bit image
-    DevBuf fbc, fbh, fbo, fbl, fbs, fbt, fbk, fbu, fbch, fbco, fbcs, fbimg;
+    DevBuf fbc, fbh, fbo, fbl, fbs, fbt, fbk, fbu, fbch, fbco, fbcs, fbimg, fbstop;
     DevBuf ck;  // checksum scratch (checksum.hip) + the 4-byte result at its start
     bool timing = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -73,9 +73,18 @@ struct dmx_ctx {
 
 namespace {
 
+// DMX_DEBUG=1 names the failing HIP call on stderr (developer aid)
+static void hipchk_report(const char* what, hipError_t e, int line) {
+    if (std::getenv("DMX_DEBUG"))
+        std::fprintf(stderr, "dmx: %s failed (dmx_host.cpp:%d): %s\n", what, line, hipGetErrorString(e));
+}
 #define HIPCHK(x)                                   \
     do {                                            \
-        if ((x) != hipSuccess) return DMX_ERR_DEVICE; \
+        const hipError_t e_ = (x);                  \
+        if (e_ != hipSuccess) {                     \
+            hipchk_report(#x, e_, __LINE__);        \
+            return DMX_ERR_DEVICE;                  \
+        }                                           \
     } while (0)
 
 struct Scal {  // small device-side scalars, one allocation
@@ -156,6 +165,7 @@ void end_timing(dmx_ctx* c, hipStream_t st) {
     float a = 0, b = 0;
     (void)hipEventElapsedTime(&a, c->ev[0], c->ev[3]);
     (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
+    (void)hipGetLastError();  // a failed query must not surface in the caller's next HIP call
     c->stats.ms_device_total = a;
     c->stats.ms_main_kernel = b;
 }
@@ -242,27 +252,45 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         HIPCHK(hipMemcpyAsync(hits.data(), c->fbl.p, nhits * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
     }
-    // units: bit 0, then every hit (sorted: chunks in order, lanes in order within a chunk)
+    // units: bit 0, then every hit (sorted: chunks in order, lanes in order within a chunk);
+    // dynamic-header hits are "strong" (practically never false), stored-header hits "weak"
+    constexpr uint64_t kStored = 1ull << 62;
     std::vector<uint64_t> starts{0};
-    for (uint64_t h : hits)
-        if (h > starts.back()) starts.push_back(h);
+    std::vector<uint8_t> strong{1};
+    for (uint64_t h : hits) {
+        const uint64_t b = h & ~kStored;
+        if (b > starts.back()) {
+            starts.push_back(b);
+            strong.push_back((h & kStored) ? 0 : 1);
+        }
+    }
     const uint64_t K = starts.size();
-    // token words per unit: at most one per bit of its span (every token costs >= 1 bit), plus
-    // room for the block that crosses the next start when that start is false; 16-B groups
-    std::vector<uint64_t> tokoff(K + 1);
     const uint64_t nbits = 8ull * n;
+    // a unit stops after passing the next strong start (or on landing on any start): stops[k];
+    // token words: at most one per bit up to where it can stop, plus room for the block that
+    // crosses that start; a weak unit (a stored block, usually) gets its span to the next start
+    // and slack for a short block behind it.  16-B groups.
+    std::vector<uint64_t> stops(K), tokoff(K + 1);
+    uint64_t next_strong = ~0ull >> 1;  // no strong start after: never stop on passing one
+    for (uint64_t k = K; k-- > 0;) {
+        stops[k] = next_strong | (strong[k] ? 0ull : 1ull << 63);  // bit 63: stored-header unit
+        if (strong[k]) next_strong = starts[k];
+    }
     tokoff[0] = 0;
     for (uint64_t k = 0; k < K; k++) {
-        const uint64_t span = (k + 1 < K ? starts[k + 1] : nbits) - starts[k];
-        tokoff[k + 1] = tokoff[k] + ((span + 4096 + 63) & ~63ull);
+        const uint64_t reach = strong[k] ? std::min<uint64_t>(stops[k], nbits) : (k + 1 < K ? starts[k + 1] : nbits);
+        // (a strong unit's stop has bit 63 clear: std::min, not the host min(int, int))
+        const uint64_t words = (reach - starts[k]) + 4096 + (strong[k] ? 0u : 16384u);
+        tokoff[k + 1] = tokoff[k] + ((words + 63) & ~63ull);
     }
     if (!c->fbs.ensure(K * 8) || !c->fbt.ensure((K + 1) * 8) || !c->fbk.ensure(tokoff[K] * 4) ||
-        !c->fbu.ensure(K * sizeof(FbUnit)))
+        !c->fbu.ensure(K * sizeof(FbUnit)) || !c->fbstop.ensure(K * 8))
         return DMX_OK;
     HIPCHK(hipMemcpyAsync(c->fbs.p, starts.data(), K * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->fbstop.p, stops.data(), K * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(c->fbt.p, tokoff.data(), (K + 1) * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(launch_fb_decode(words, misalign, n, c->fbs.as<uint64_t>(), K, c->fbt.as<uint64_t>(),
-                            c->fbk.as<uint32_t>(), c->fbu.as<FbUnit>(), c->flags, st));
+    HIPCHK(launch_fb_decode(words, misalign, n, c->fbs.as<uint64_t>(), c->fbstop.as<uint64_t>(), K,
+                            c->fbt.as<uint64_t>(), c->fbk.as<uint32_t>(), c->fbu.as<FbUnit>(), c->flags, st));
     std::vector<FbUnit> units(K);
     HIPCHK(hipMemcpyAsync(units.data(), c->fbu.p, K * sizeof(FbUnit), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -479,6 +507,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     }
     // serial path: size pass, then write pass
     c->stats.path = 2;
+    if (c->timing) (void)hipEventRecord(c->ev[1], st);
     HIPCHK(launch_inflate_serial(A, 1, &ds->res, st));
     HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -492,6 +521,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
         return DMX_ERR_CAPACITY;
     }
     HIPCHK(launch_inflate_serial(A, 0, &ds->res, st));
+    if (c->timing) (void)hipEventRecord(c->ev[2], st);
     HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     end_timing(c, st);
@@ -624,7 +654,7 @@ void dmx_destroy(dmx_ctx* c) {
     for (DevBuf* b : {&c->in, &c->out, &c->slots, &c->sizes, &c->offs, &c->scal, &c->cands,
                       &c->tiles, &c->tileoffs, &c->recs, &c->status, &c->dbg, &c->ltok,
                       &c->ltokoff, &c->lntok, &c->lcaps, &c->fbc, &c->fbh, &c->fbo, &c->fbl,
-                      &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg,
+                      &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg, &c->fbstop,
                       &c->ck})
         b->release();
     for (auto& e : c->ev)

@@ -122,9 +122,11 @@ hipError_t launch_fb_scan(const uint32_t* in_words, uint64_t misalign, uint64_t 
                           hipStream_t st);
 hipError_t launch_fb_compact(const uint32_t* counts, const uint64_t* offs, const uint64_t* hits,
                              uint64_t nchunks, uint64_t* list, hipStream_t st);
+// hits carry bit 62 for a stored-block header; stops[u] = the next dynamic-header start after u
 hipError_t launch_fb_decode(const uint32_t* in_words, uint64_t misalign, uint64_t n,
-                            const uint64_t* starts, uint64_t nunits, const uint64_t* tokoff,
-                            uint32_t* tok, FbUnit* units, uint32_t flags, hipStream_t st);
+                            const uint64_t* starts, const uint64_t* stops, uint64_t nunits,
+                            const uint64_t* tokoff, uint32_t* tok, FbUnit* units, uint32_t flags,
+                            hipStream_t st);
 // replay + serial window hand-off + final resolve; *err (zeroed by the caller) becomes nonzero
 // when a copy reaches before the stream start
 hipError_t launch_fb_resolve(const uint8_t* stream, const uint64_t* starts, const uint32_t* chain,

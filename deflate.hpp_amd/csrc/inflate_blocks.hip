@@ -7,8 +7,9 @@
 // block loop (realDecompress, /root/reference/include/inflate.hpp:277-322); this path splits it
 // into units that decode side by side and stitches the windows together afterwards:
 //
-//   k_fb_scan    every bit offset of the stream is tested for a dynamic-block header that a
-//                real encoder could have written: BTYPE 2, HLIT <= 29, HDIST <= 29, a complete
+//   k_fb_scan    every bit offset of the stream is tested for a stored-block header (LEN, NLEN =
+//                ~LEN at the next byte boundary, data inside the stream) and for a dynamic-block
+//                header that a real encoder could have written: BTYPE 2, HLIT <= 29, HDIST <= 29, a complete
 //                code-length code whose last sent length is nonzero, a code-length sequence
 //                that decodes without overrun to a complete lit/len code with a nonzero
 //                end-of-block length and a complete (or at most one-symbol) distance code.
@@ -40,8 +41,10 @@ namespace dmx {
 
 constexpr uint32_t FB_SCAN_BITS = 32768;  // bit offsets tested per wavefront (4 KiB of stream)
 constexpr uint32_t FB_STAGE_WORDS = FB_SCAN_BITS / 32 + 128;  // + 4096 bits of header lookahead
-constexpr uint32_t FB_HITS = 4;           // hits kept per scan chunk (more only cost parallelism)
+constexpr uint32_t FB_HITS = 12;          // hits kept per scan chunk (stored headers in zero
+                                          // padding are found at several offsets)
 constexpr uint32_t FB_RING = 32768;       // replay window (entries of 16 bits)
+constexpr uint64_t FB_HIT_STORED = 1ull << 62;  // hit flag: a stored-block header
 constexpr uint32_t FB_GROUP_MAX = 8192;   // output entries per replay group (see k_fb_replay)
 
 // ---------------------------------------------------------------------------------------
@@ -156,10 +159,22 @@ __global__ __launch_bounds__(64) void k_fb_scan(const uint32_t* in_words, uint64
     for (uint32_t it = 0; it < FB_SCAN_BITS / 64 && found < FB_HITS; it++) {
         const uint32_t r = it * 64 + lane;  // offset tested by this lane, relative to b0
         const uint64_t sb = b0 + r;         // stream bit
-        bool hit = false;
+        bool hit = false, stored = false;
         if (sb + 17 + 12 < nbits) {
             const uint32_t q = sh + r;      // staged-image bit
             const uint32_t h = fb_bits(stg, q);
+            if (((h >> 1) & 3) == 0) {
+                // stored block: LEN and NLEN = ~LEN at the next byte boundary, data inside the
+                // stream (zlib writes these for incompressible runs; without them a unit ending
+                // before a stored block had no unit to continue the chain).  A header in zero
+                // padding is found at several offsets; the chain takes the one the unit before
+                // ends at, the others only cost parallelism.
+                const uint64_t bb = (sb + 3 + 7) & ~7ull;  // stream bit of LEN
+                if (bb + 32 <= nbits) {
+                    const uint32_t ln = fb_bits(stg, q + (uint32_t)(bb - sb));
+                    hit = stored = ((ln ^ (ln >> 16)) & 0xFFFFu) == 0xFFFFu && bb / 8 + 4 + (ln & 0xFFFFu) <= n;
+                }
+            }
             const uint32_t hlit = (h >> 3) & 31, hdist = (h >> 8) & 31, hclen = ((h >> 13) & 15) + 4;
             if (((h >> 1) & 3) == 2 && hlit <= 29 && hdist <= 29) {
                 const uint32_t x0 = fb_bits(stg, q + 17), x1 = fb_bits(stg, q + 49);
@@ -183,7 +198,8 @@ __global__ __launch_bounds__(64) void k_fb_scan(const uint32_t* in_words, uint64
         const uint64_t m = __ballot(hit);
         if (m) {
             const uint32_t before = __popcll(m & ((1ull << lane) - 1ull));
-            if (hit && found + before < FB_HITS) hits[c * FB_HITS + found + before] = sb;
+            if (hit && found + before < FB_HITS)
+                hits[c * FB_HITS + found + before] = sb | (stored ? FB_HIT_STORED : 0ull);
             found += __popcll(m);
         }
     }
@@ -282,15 +298,25 @@ struct TokSink {
 
 __global__ __launch_bounds__(64) void k_fb_decode(const uint32_t* in_words, uint64_t misalign,
                                                    uint64_t n, const uint64_t* starts,
-                                                   uint64_t nunits, const uint64_t* tokoff,
-                                                   uint32_t* tok, FbUnit* units, uint32_t flags) {
+                                                   const uint64_t* stops, uint64_t nunits,
+                                                   const uint64_t* tokoff, uint32_t* tok,
+                                                   FbUnit* units, uint32_t flags) {
     __shared__ Tables T;
     const uint64_t u = blockIdx.x;
     if (u >= nunits) return;
     if (lane_id() == 0) T.fixed_loaded = 0;
     wave_sync();
     const uint64_t start = starts[u];
-    const uint64_t stop = u + 1 < nunits ? starts[u + 1] : ~0ull;
+    // A unit ends after the first block that lands exactly on another unit's start, or that
+    // passes the next dynamic-header start (stored-header starts can be false: passing one
+    // inside a block is no reason to stop, landing on one is a chain link).
+    // A unit at a stored-header start (bit 63 of its stop) decodes stored blocks only and ends
+    // before the first other block: such a start can be false, and a false one then costs one
+    // bounded copy instead of a run of Huffman decoding over arbitrary bits.
+    const bool weak = (stops[u] >> 63) != 0;
+    const uint64_t stop = stops[u] & ~(1ull << 63);
+    uint64_t jn = u + 1;  // first unit start not below the current position
+    uint64_t end_at = 0;  // (weak units) stream bit of the first block they leave undecoded
     const uint64_t base = misalign * 8;  // stream bit 0 in the aligned image
     BitIn br;
     br.init(in_words, misalign, n);
@@ -308,11 +334,21 @@ __global__ __launch_bounds__(64) void k_fb_decode(const uint32_t* in_words, uint
     bool fin = false;
     // realDecompress (inflate.hpp:277-322) until the next unit's start or BFINAL
     for (bool first = true;; first = false) {
-        if (!first && br.abspos() - base >= stop) break;
+        if (!first) {
+            const uint64_t pos = br.abspos() - base;
+            if (pos >= stop) break;
+            while (jn < nunits && starts[jn] < pos) jn++;
+            if (jn < nunits && starts[jn] == pos) break;
+        }
+        const uint64_t hpos = br.abspos();
         br.ensure(3);
         const uint32_t bfinal = br.bits(1);
         const uint32_t btype = br.bits(2);
         if (br.over()) { err = SEGF_OVERREAD; break; }
+        if (weak && btype != 0) {
+            end_at = hpos;
+            break;
+        }
         if (btype == 0) {
             br.align();
             br.ensure(32);
@@ -348,7 +384,7 @@ __global__ __launch_bounds__(64) void k_fb_decode(const uint32_t* in_words, uint
     if (lane_id() == 0) {
         FbUnit r;
         r.start = start;
-        r.end = br.abspos() - base;
+        r.end = (end_at ? end_at : br.abspos()) - base;
         r.size = sk.pos;
         r.ntok = sk.n;
         r.flags = err | (fin ? SEGF_FINAL : 0u);
@@ -620,10 +656,11 @@ hipError_t launch_fb_compact(const uint32_t* counts, const uint64_t* offs, const
 }
 
 hipError_t launch_fb_decode(const uint32_t* in_words, uint64_t misalign, uint64_t n,
-                            const uint64_t* starts, uint64_t nunits, const uint64_t* tokoff,
-                            uint32_t* tok, FbUnit* units, uint32_t flags, hipStream_t st) {
+                            const uint64_t* starts, const uint64_t* stops, uint64_t nunits,
+                            const uint64_t* tokoff, uint32_t* tok, FbUnit* units, uint32_t flags,
+                            hipStream_t st) {
     hipLaunchKernelGGL(k_fb_decode, dim3((uint32_t)nunits), dim3(64), 0, st, in_words, misalign, n,
-                       starts, nunits, tokoff, tok, units, flags);
+                       starts, stops, nunits, tokoff, tok, units, flags);
     return hipGetLastError();
 }
 

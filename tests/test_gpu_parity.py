@@ -74,6 +74,19 @@ def test_inflate_foreign_stream_serial_path(ctx, oracle, kind):
         assert oracle.inflate(s) == out, (lvl, st)
 
 
+@pytest.mark.parametrize("kind,lvl", [("text", 1), ("mixed", 6), ("mixed", 1), ("random", 6), ("zeros", 6)])
+def test_inflate_foreign_stream_block_parallel_path(ctx, oracle, kind, lvl):
+    """Marker-less third-party streams take the block-parallel path 5,
+    including zlib's stored blocks for incompressible runs (mixed, random), bit-exact."""
+    d = dmx.corpus(kind, 4 << 20, offset=99)
+    s = zraw(d, lvl, 0)
+    out = ctx.decompress(s)
+    assert out == d
+    assert ctx.stats().path == 5
+    small = zraw(d[: 1 << 19], lvl, 0)
+    assert ctx.decompress(small) == oracle.inflate(small) == d[: 1 << 19]
+
+
 def test_inflate_c3_large_bmp_zlib1(ctx):
     """Config C3: the zlib level-1 raw stream of the full 25,165,962-B large.bmp
     stand-in (6.2 MB, hundreds of dynamic blocks with cross-block references), bit-exact with
