@@ -223,6 +223,7 @@ def corpus_record(run, kind, level, steps):
             "ratio": round(n / s["clen"], 4),
             "ref_ratio_L2": REF_RATIO_L2.get(kind), "ref_note": REF_NOTES.get(kind, "reference L2 round-trips"),
             "zlib1_ratio_16MiB": zlib_ratio(kind, 1),
+            "zlib1_ratio_32KiB_chunks_16MiB": zlib_ratio(kind, 1, chunk=32768),
             "kernel_ms": {"k_deflate_segments": round(s["k_def"], 4),
                           INF_KERNEL.get(s["path"], "k_inflate_segments"): round(s["k_inf"], 4)},
             "inflate_path": s["path"],
@@ -380,7 +381,7 @@ def main():
     if world == 1 and not a.no_extras:
         # sub-records (outside the timed region): the other corpora, C3 and C5
         extras = {}
-        for kind in ("text", "mixed", "random", "zeros"):
+        for kind in ("text", "mixed", "random", "zeros", "bmp"):
             if kind != a.corpus:
                 extras[kind] = corpus_record(run, kind, a.level, 3)
         res["corpora"] = extras

@@ -10,8 +10,8 @@
 //                                  cand[p] = distance to the first occurrence of p's 4-byte key
 //                                  earlier in the same round, else to the latest one in earlier
 //                                  rounds   (replaces LZ77::getMatches deflate.hpp:310-383)
-//   level 3                     -> link rounds of 128 positions and a depth-16 search along the
-//                                  candidate chains   (replaces getMatchesSlow :268-304)
+//   level 3                     -> a depth-16 search along the chains of those candidates
+//                                  (replaces getMatchesSlow :268-304)
 //   parse walk                  -> 258-byte chunk per quad of lanes, greedy (level 2) or one-step
 //                                  lazy (level 3); matches never cross a chunk edge, so chunks
 //                                  parse independently; token starts -> LDS bitmap
@@ -62,6 +62,13 @@ constexpr int DF_L3_DEPTH = DMX_L3_DEPTH;  // level 3: candidate-chain links sea
 #define DMX_L3_ROUND 128
 #endif
 constexpr uint32_t DF_L3_ROUND = DMX_L3_ROUND;  // level 3: positions per link-building round
+// Level 3 links: the level-2 candidates (first occurrence in the round, else the latest before
+// it) by default; 1 = the single-wave link rounds of DF_L3_ROUND positions (latest occurrence
+// before the position's round), which cannot see an occurrence inside the same round.
+#ifndef DMX_L3_LINK_ROUNDS
+#define DMX_L3_LINK_ROUNDS 0
+#endif
+constexpr bool DF_L3_LINK_ROUNDS = DMX_L3_LINK_ROUNDS != 0;
 
 // ---------------------------------------------------------------------------------------
 // block primitives
@@ -950,7 +957,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
             uint32_t ph0 = 0, ph1 = 0, pp0 = 0, pf0 = 0, pf1 = 0;  // previous round: hashes, p0, fp16s
             bool pok0 = false, pok1 = false;
             constexpr uint32_t NOH = 0xFFFFFFFFu;  // "no hash" for the neighbour compares
-            if (level == 3) {
+            if (level == 3 && DF_L3_LINK_ROUNDS) {
                 // Level 3 builds links for the chain search below: rounds of DF_L3_ROUND
                 // positions, each position linked to the latest occurrence of its key before
                 // its round (or to its pair partner, in-thread), so consecutive links skip at
