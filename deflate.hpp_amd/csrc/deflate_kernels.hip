@@ -69,6 +69,11 @@ constexpr uint32_t DF_L3_ROUND = DMX_L3_ROUND;  // level 3: positions per link-b
 #define DMX_L3_LINK_ROUNDS 0
 #endif
 constexpr bool DF_L3_LINK_ROUNDS = DMX_L3_LINK_ROUNDS != 0;
+// Level 3: positions per match round (the level-2 rounds take 2 * DF_NT = 2048)
+#ifndef DMX_L3_RP
+#define DMX_L3_RP 512
+#endif
+constexpr uint32_t DF_L3_RP = DMX_L3_RP;
 
 // ---------------------------------------------------------------------------------------
 // block primitives
@@ -940,7 +945,8 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         if (level >= 2) {
             // Table entries carry a fingerprint of the 4-byte key (product bits below the hash
             // bits), so a lookup verifies its candidate without reading the candidate's bytes:
-            //   first = round(4) | 0x7FFF - p (15) | fp13      (atomicMax: earliest p in round)
+            //   first = round(4) | 0x7FFF - p (15) | fp13      (atomicMax: earliest p in round;
+            //           shorter level-3 rounds: round(4 + e) and fp(13 - e))
             //   head  = p + 1 (16) | fp16                       (atomicMax: latest p, 0 = none)
             // stored as {head, first} pairs, one ds_read_b64 per lookup.  A fingerprint match
             // that is not a key match is rare; the parse walk then finds a match length < 3
@@ -950,7 +956,6 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
             // are mostly in-thread.  A position's latest-occurrence update waits one round (a
             // lookup must not see later positions of its own round); the first occurrence in a
             // round is resolved by the round number in the entry.
-            static_assert(SEG / (2 * DF_NT) <= 16, "round number is 4 bits");
             constexpr uint32_t HB = DfSmem<SEG>::HB;
             const uint2* const tab = reinterpret_cast<const uint2*>(S.U);
             uint32_t* const cand32 = reinterpret_cast<uint32_t*>(S.cand);
@@ -1004,66 +1009,83 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                 // One round; cur receives this round's hashes for the next round's latest-occurrence
                 // updates, prev holds the previous round's.  Rounds go in pairs with the two states
                 // swapping roles (no register copies), and rounds that lie wholly inside the
-                // segment skip the bounds tests (`full`, a constant in each call).
+                // segment skip the bounds tests (`full`, a constant in each call).  Rounds of RP
+                // positions: 2 * DF_NT at level 2; level 3 may use shorter rounds (DF_L3_RP, the
+                // first RP / 2 threads active) so the first-in-round links skip fewer occurrences
+                // for its chain search, with a wider round number and a narrower fingerprint.
                 struct RoundState {
                     uint32_t h0, h1, p0, f0, f1;
                     bool ok0, ok1;
                 };
-                auto round = [&](uint32_t r0, uint32_t rr, RoundState& cur, const RoundState& prev, auto full) {
-                    constexpr bool FULL = decltype(full)::value;
-                    const uint32_t p0 = r0 + 2 * t, p1 = p0 + 1;
-                    const uint32_t i0 = p0 >> 2, sh = p0 & 3;  // sh = 0 or 2
-                    const uint32_t wa = S.data32[i0], wb = S.data32[i0 + 1];
-                    const uint32_t prod0 = __builtin_amdgcn_alignbyte(wb, wa, sh) * 0x1E35A7BDu;
-                    const uint32_t prod1 = __builtin_amdgcn_alignbyte(wb, wa, sh + 1) * 0x1E35A7BDu;
-                    const bool ok0 = FULL || p0 + 4 <= nb, ok1 = FULL || p1 + 4 <= nb;
-                    const uint32_t h0 = ok0 ? prod0 >> (32 - HB) : NOH, h1 = ok1 ? prod1 >> (32 - HB) : NOH;
-                    const uint32_t fa0 = (prod0 >> (32 - HB - 16)) & 0xFFFFu, fa1 = (prod1 >> (32 - HB - 16)) & 0xFFFFu;
-                    // first occurrence in this round: p1 needs no update when p0 has its hash, p0
-                    // none when p0 - 1 (the previous lane's p1, by DPP within rows of 16) has it
-                    const uint32_t hl = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)h1, 0x111, 0xF, 0xF, false);
-                    const uint32_t rtag = rr << 28;
-                    if (ok0 && h0 != hl)
-                        atomicMax(&S.U[2 * h0 + 1], rtag | ((0x7FFFu - p0) << 13) | (fa0 >> 3));
-                    if (ok1 && h1 != h0)
-                        atomicMax(&S.U[2 * h1 + 1], rtag | ((0x7FFFu - p1) << 13) | (fa1 >> 3));
-                    // latest occurrence, for the previous round's positions: its p0 needs no update
-                    // when its p0 + 1 has the hash, p0 + 1 none when p0 + 2 (the next lane's) has it
-                    const uint32_t hn = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)(prev.ok0 ? prev.h0 : NOH), 0x101, 0xF, 0xF, false);
-                    if (prev.ok0 && prev.h0 != (prev.ok1 ? prev.h1 : NOH))
-                        atomicMax(&S.U[2 * prev.h0], ((prev.p0 + 1) << 16) | prev.f0);
-                    if (prev.ok1 && prev.h1 != hn) atomicMax(&S.U[2 * prev.h1], ((prev.p0 + 2) << 16) | prev.f1);
-                    __syncthreads();
-                    uint2 e0 = tab[ok0 ? h0 : 0u], e1 = tab[ok1 ? h1 : 0u];
-                    // both halves now: otherwise the compiler sinks the head half of e0 into the
-                    // not-first-in-round branch, a second LDS round trip after the first
-                    asm volatile("" : "+v"(e0.x), "+v"(e0.y), "+v"(e1.x), "+v"(e1.y));
-                    auto pick = [&](uint2 e, uint32_t p, uint32_t fa, bool ok) -> uint32_t {
-                        const uint32_t f = e.y, hd = e.x;
-                        const uint32_t q = 0x7FFFu - ((f >> 13) & 0x7FFFu);
-                        const bool fr = ((f >> 28) == rr) & (q < p) & ((f & 0x1FFFu) == (fa >> 3));
-                        const bool lt = (hd != 0u) & ((hd & 0xFFFFu) == fa);
-                        const uint32_t c = fr ? p - q : (lt ? p + 1u - (hd >> 16) : 0u);
-                        return ok ? c : 0u;
+                auto run_rounds = [&](auto rpc) {
+                    constexpr uint32_t RP = decltype(rpc)::value;
+                    constexpr uint32_t NR = SEG / RP;
+                    constexpr uint32_t TAGB = NR <= 16 ? 4 : NR <= 32 ? 5 : NR <= 64 ? 6 : 7;
+                    static_assert(NR <= 128, "round number is at most 7 bits");
+                    constexpr uint32_t FPB = 17 - TAGB;  // fingerprint bits in the first entry
+                    const bool act = RP >= 2 * DF_NT || t < (int)(RP / 2);
+                    const uint32_t tt = RP >= 2 * DF_NT ? (uint32_t)t : (uint32_t)t & (RP / 2 - 1);
+                    auto round = [&](uint32_t r0, uint32_t rr, RoundState& cur, const RoundState& prev, auto full) {
+                        constexpr bool FULL = decltype(full)::value;
+                        const uint32_t p0 = r0 + 2 * tt, p1 = p0 + 1;
+                        const uint32_t i0 = p0 >> 2, sh = p0 & 3;  // sh = 0 or 2
+                        const uint32_t wa = S.data32[i0], wb = S.data32[i0 + 1];
+                        const uint32_t prod0 = __builtin_amdgcn_alignbyte(wb, wa, sh) * 0x1E35A7BDu;
+                        const uint32_t prod1 = __builtin_amdgcn_alignbyte(wb, wa, sh + 1) * 0x1E35A7BDu;
+                        const bool ok0 = act && (FULL || p0 + 4 <= nb), ok1 = act && (FULL || p1 + 4 <= nb);
+                        const uint32_t h0 = ok0 ? prod0 >> (32 - HB) : NOH, h1 = ok1 ? prod1 >> (32 - HB) : NOH;
+                        const uint32_t fa0 = (prod0 >> (32 - HB - 16)) & 0xFFFFu, fa1 = (prod1 >> (32 - HB - 16)) & 0xFFFFu;
+                        // first occurrence in this round: p1 needs no update when p0 has its hash, p0
+                        // none when p0 - 1 (the previous lane's p1, by DPP within rows of 16) has it
+                        const uint32_t hl = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)h1, 0x111, 0xF, 0xF, false);
+                        const uint32_t rtag = rr << (32 - TAGB);
+                        if (ok0 && h0 != hl)
+                            atomicMax(&S.U[2 * h0 + 1], rtag | ((0x7FFFu - p0) << FPB) | (fa0 >> (16 - FPB)));
+                        if (ok1 && h1 != h0)
+                            atomicMax(&S.U[2 * h1 + 1], rtag | ((0x7FFFu - p1) << FPB) | (fa1 >> (16 - FPB)));
+                        // latest occurrence, for the previous round's positions: its p0 needs no update
+                        // when its p0 + 1 has the hash, p0 + 1 none when p0 + 2 (the next lane's) has it
+                        const uint32_t hn = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)(prev.ok0 ? prev.h0 : NOH), 0x101, 0xF, 0xF, false);
+                        if (prev.ok0 && prev.h0 != (prev.ok1 ? prev.h1 : NOH))
+                            atomicMax(&S.U[2 * prev.h0], ((prev.p0 + 1) << 16) | prev.f0);
+                        if (prev.ok1 && prev.h1 != hn) atomicMax(&S.U[2 * prev.h1], ((prev.p0 + 2) << 16) | prev.f1);
+                        __syncthreads();
+                        uint2 e0 = tab[ok0 ? h0 : 0u], e1 = tab[ok1 ? h1 : 0u];
+                        // both halves now: otherwise the compiler sinks the head half of e0 into the
+                        // not-first-in-round branch, a second LDS round trip after the first
+                        asm volatile("" : "+v"(e0.x), "+v"(e0.y), "+v"(e1.x), "+v"(e1.y));
+                        auto pick = [&](uint2 e, uint32_t p, uint32_t fa, bool ok) -> uint32_t {
+                            const uint32_t f = e.y, hd = e.x;
+                            const uint32_t q = 0x7FFFu - ((f >> FPB) & 0x7FFFu);
+                            const bool fr = ((f >> (32 - TAGB)) == rr) & (q < p) &
+                                            ((f & ((1u << FPB) - 1)) == (fa >> (16 - FPB)));
+                            const bool lt = (hd != 0u) & ((hd & 0xFFFFu) == fa);
+                            const uint32_t c = fr ? p - q : (lt ? p + 1u - (hd >> 16) : 0u);
+                            return ok ? c : 0u;
+                        };
+                        if (act && (FULL || p0 < nb)) cand32[p0 >> 1] = pick(e0, p0, fa0, ok0) | (pick(e1, p1, fa1, ok1) << 16);
+                        cur = RoundState{h0, h1, p0, fa0, fa1, ok0, ok1};
+                        __syncthreads();
                     };
-                    if (FULL || p0 < nb) cand32[p0 >> 1] = pick(e0, p0, fa0, ok0) | (pick(e1, p1, fa1, ok1) << 16);
-                    cur = RoundState{h0, h1, p0, fa0, fa1, ok0, ok1};
-                    __syncthreads();
+                    using Full = std::integral_constant<bool, true>;
+                    using Part = std::integral_constant<bool, false>;
+                    RoundState A = {0, 0, 0, 0, 0, false, false}, B = A;
+                    uint32_t r0 = 0, rr = 0;
+                    for (; r0 + 2 * RP + 3 <= nb; r0 += 2 * RP, rr += 2) {  // two full rounds
+                        round(r0, rr, A, B, Full{});
+                        round(r0 + RP, rr + 1, B, A, Full{});
+                    }
+                    for (; r0 < nb; r0 += RP, rr++) {  // the rest (the last may be partial)
+                        round(r0, rr, A, B, Part{});
+                        const RoundState x = A;
+                        A = B;
+                        B = x;
+                    }
                 };
-                using Full = std::integral_constant<bool, true>;
-                using Part = std::integral_constant<bool, false>;
-                RoundState A = {0, 0, 0, 0, 0, false, false}, B = A;
-                uint32_t r0 = 0, rr = 0;
-                for (; r0 + 4 * DF_NT + 3 <= nb; r0 += 4 * DF_NT, rr += 2) {  // two full rounds
-                    round(r0, rr, A, B, Full{});
-                    round(r0 + 2 * DF_NT, rr + 1, B, A, Full{});
-                }
-                for (; r0 < nb; r0 += 2 * DF_NT, rr++) {  // the rest (the last may be partial)
-                    round(r0, rr, A, B, Part{});
-                    const RoundState x = A;
-                    A = B;
-                    B = x;
-                }
+                if (level == 3 && DF_L3_RP != 2 * DF_NT)
+                    run_rounds(std::integral_constant<uint32_t, DF_L3_RP>{});
+                else
+                    run_rounds(std::integral_constant<uint32_t, 2 * DF_NT>{});
             }
             DMX_PHASE(A.dbg, seg, 14);
         }

@@ -572,32 +572,77 @@ __global__ __launch_bounds__(64) void k_fb_replay(FbReplayArgs A) {
 // k_fb_tails: the serial window hand-off.  One workgroup; for every unit on the chain, in
 // order, the markers of its last min(size, 32 KiB) entries are resolved against the last
 // 32 KiB of output before it (kept in LDS), the bytes go to the output, and the window moves.
+// The image entries of unit k + 1's tail are loaded into registers (32 per thread) while unit
+// k is resolved, so the chain of units pays the HBM latency once, not once per unit.
 // ---------------------------------------------------------------------------------------
 constexpr int FB_TNT = 1024;
-__global__ __launch_bounds__(FB_TNT) void k_fb_tails(const uint16_t* img, const uint64_t* offs,
-                                                     const uint64_t* sizes, uint64_t nchain,
-                                                     uint8_t* out) {
+constexpr int FB_TPT = FB_RING / FB_TNT;  // tail entries per thread
+__global__ __launch_bounds__(FB_TNT) void k_fb_tails(const uint16_t* __restrict__ img,
+                                                     const uint64_t* __restrict__ offs,
+                                                     const uint64_t* __restrict__ sizes,
+                                                     uint64_t nchain, uint8_t* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint8_t win[2][FB_RING];
     const uint32_t t = threadIdx.x;
     uint32_t cur = 0;
     for (uint32_t i = t; i < FB_RING; i += FB_TNT) win[0][i] = 0;
+    // entry i of a tail is held by thread i % FB_TNT, slot i / FB_TNT
+    struct Tail {
+        uint64_t off, s;
+        uint32_t v[FB_TPT];
+    };
+    auto load_tail = [&](uint64_t k, Tail& T) {
+        if (k >= nchain) return;
+        T.off = offs[k];
+        T.s = sizes[k];
+        const uint32_t tl = (uint32_t)min(T.s, (uint64_t)FB_RING);
+        const uint16_t* src = img + T.off + (T.s - tl);
+        uint32_t tq = t;  // opaque copy: the 32 indices are not hoisted out of the loop (spills)
+        asm volatile("" : "+v"(tq));
+#pragma unroll
+        for (int j = 0; j < FB_TPT; j++) {
+            const uint32_t i = tq + FB_TNT * j;
+            T.v[j] = src[i < tl ? i : 0u];  // unconditional (the image has 8 spare entries)
+        }
+    };
+    Tail ta, tb;
+    load_tail(0, ta);
     __syncthreads();
-    for (uint64_t k = 0; k < nchain; k++) {
-        const uint64_t off = offs[k], s = sizes[k];
+    auto resolve = [&](const Tail& T) {
+        const uint64_t off = T.off, s = T.s;
         const uint32_t tl = (uint32_t)min(s, (uint64_t)FB_RING);
         const uint64_t x0 = s - tl;  // first tail entry (unit-relative)
         const uint8_t* W = win[cur];
         uint8_t* N = win[cur ^ 1];
         // carry the part of the old window that stays (units shorter than the window)
         for (uint32_t i = t; i < FB_RING - tl; i += FB_TNT) N[i] = W[i + tl];
-        for (uint32_t i = t; i < tl; i += FB_TNT) {
-            const uint32_t v = img[off + x0 + i];
-            const uint8_t b = v < 0x8000u ? (uint8_t)v : W[FB_RING - 1 - (v & 0x7FFFu)];
-            out[off + x0 + i] = b;
-            N[FB_RING - tl + i] = b;
+        uint32_t tq = t;
+        asm volatile("" : "+v"(tq));
+        // all window reads first (unconditional, so they pipeline), then the stores
+        uint32_t bv[FB_TPT];
+#pragma unroll
+        for (int j = 0; j < FB_TPT; j++) {
+            const uint32_t e = T.v[j];
+            const uint32_t w = W[FB_RING - 1 - (e & 0x7FFFu)];
+            bv[j] = e < 0x8000u ? e : w;
+        }
+#pragma unroll
+        for (int j = 0; j < FB_TPT; j++) {
+            const uint32_t i = tq + FB_TNT * j;
+            if (i < tl) {
+                out[off + x0 + i] = (uint8_t)bv[j];
+                N[FB_RING - tl + i] = (uint8_t)bv[j];
+            }
         }
         __syncthreads();
         cur ^= 1;
+    };
+    // two units per iteration, the register sets swapping roles
+    for (uint64_t k = 0; k < nchain; k += 2) {
+        load_tail(k + 1, tb);
+        resolve(ta);
+        if (k + 1 >= nchain) break;
+        load_tail(k + 2, ta);
+        resolve(tb);
     }
 }
 
