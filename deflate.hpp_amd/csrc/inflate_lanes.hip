@@ -156,6 +156,72 @@ __device__ __forceinline__ bool ln_coop_table(uint32_t nsym, Lens lens, Order or
     return true;
 }
 
+// Per-lane canonical tables (one lane per segment, all segments of the wave at once).  Nine 9-bit
+// counters or next codes per lane in two registers: code lengths 1..6 in lo, 7..9 in hi.
+struct Pk9 {
+    uint64_t lo;
+    uint32_t hi;
+};
+__device__ __forceinline__ uint32_t pk_get(const Pk9& p, uint32_t L) {  // L in 1..9
+    return L <= 6 ? (uint32_t)(p.lo >> (9 * (L - 1))) & 511u : (p.hi >> (9 * (L - 7))) & 511u;
+}
+__device__ __forceinline__ void pk_add(Pk9& p, uint32_t L) {  // L in 0..9 (0: nothing)
+    p.lo += (L - 1u) < 6u ? 1ull << (9 * (L - 1)) : 0ull;
+    p.hi += L >= 7 ? 1u << (9 * (L - 7)) : 0u;
+}
+// The table T[0, 2^B) of a code with per-length counts `cnt` (lengths <= B), symbols s < nsym of
+// lengths nib(s) (4-bit nibbles, packed 8 per word: word(k) holds symbols 8k .. 8k + 7); entries
+// ent(s, L) whose length field is (e >> lsh) & lmask.  RFC 1951 3.2.2 canonical codes: the next
+// code of each length, symbols in order.  Each symbol's entry goes to its bit-reversed code
+// (a "seed", below 2^L); the table is then completed level by level: for b = 1 .. B-1 every entry
+// in [0, 2^b) of length <= b is copied to + 2^b (a longer code's seed stays, and its own positions
+// come from its seed).  Entries not yet written hold `mark` (a length above B).  Index rotation
+// by lane keeps the lanes' accesses (regions 1152 B apart) off a common bank.  Returns false
+// unless the code is complete.
+template <int B, class Word, class Ent>
+__device__ __forceinline__ bool ln_lane_table(uint16_t* T, const Pk9& cnt, uint32_t nsym, Word word, Ent ent,
+                                              uint32_t lsh, uint32_t lmask, uint32_t mark) {
+    const uint32_t lane = lane_id();
+    uint32_t kraft = 0, code = 0;
+    Pk9 nc = {0ull, 0u};
+#pragma unroll
+    for (uint32_t l = 1; l <= (uint32_t)B; l++) {
+        const uint32_t c = pk_get(cnt, l);
+        kraft += c << (B - l);
+        code = (code + (l > 1 ? pk_get(cnt, l - 1) : 0u)) << 1;  // first code of length l
+        if (l <= 6) nc.lo |= (uint64_t)code << (9 * (l - 1));
+        else nc.hi |= code << (9 * (l - 7));
+    }
+    if (kraft != (1u << B)) return false;
+    uint32_t* const T32 = reinterpret_cast<uint32_t*>(T);
+    constexpr uint32_t NW = (1u << B) / 2;  // table words
+#pragma unroll 4
+    for (uint32_t w = 0; w < NW; w++) T32[(w + lane) & (NW - 1)] = mark | (mark << 16);
+    for (uint32_t k = 0; 8 * k < nsym; k++) {
+        const uint32_t x = word(k);
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++) {
+            const uint32_t sym = 8 * k + i, L = (x >> (4 * i)) & 15u;
+            if (L != 0u && sym < nsym) {
+                const uint32_t c = pk_get(nc, L);
+                T[__builtin_bitreverse32(c) >> (32 - L)] = (uint16_t)ent(sym, L);
+            }
+            pk_add(nc, L);
+        }
+    }
+#pragma unroll
+    for (uint32_t b = 1; b < (uint32_t)B; b++) {
+        const uint32_t n = 1u << b;
+#pragma unroll 8
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t q = (i + 2 * lane) & (n - 1);
+            const uint32_t e = T[q];
+            if (((e >> lsh) & lmask) <= b) T[q + n] = (uint16_t)e;
+        }
+    }
+    return true;
+}
+
 __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[LN_LANES * (LN_REGION + LN_PRE_BYTES)];
     const uint32_t lane = threadIdx.x;
@@ -365,33 +431,45 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
     }
     if (dbg) dbg[2] = __builtin_amdgcn_s_memtime();
 
-    // ---- lit/len (9-bit) and distance (6-bit) tables, built by the wave ---------------------------
-    const uint32_t huff_mask = (uint32_t)__ballot(huff && !flags);
-    uint16_t* const ORD = reinterpret_cast<uint16_t*>(SH);  // canonical order scratch (<= 288 x u16)
-    bad_mask = 0;
-    for (uint32_t m = huff_mask; m; m &= m - 1) {
-        const uint32_t s = (uint32_t)__builtin_ctz(m);
-        const bool fixed = (dyn_mask >> s & 1u) == 0;
-        const uint8_t* const LL = lds + s * LN_REGION + LN_LENS;
-        uint16_t* const lt = reinterpret_cast<uint16_t*>(lds + s * LN_REGION);
-        uint16_t* const dt = reinterpret_cast<uint16_t*>(lds + s * LN_REGION + LN_DIST);
-        // the lengths are read before the table writes (ln_coop_table: counts and order first)
-        auto ord16 = [&](uint32_t i, uint32_t sym, int wr) -> uint32_t {
-            if (wr) { ORD[i] = (uint16_t)sym; return 0u; }
-            return ORD[i];
-        };
-        bool ok = ln_coop_table<6>(
-            32u, [&](uint32_t sym) { return fixed ? 5u : (uint32_t)LL[288 + sym]; }, ord16,
-            [&](uint32_t x, uint32_t sym, uint32_t len) { dt[x] = (uint16_t)(0x8000u | (len << 8) | sym); });
-        ok = ok && ln_coop_table<9>(
-            288u,
-            [&](uint32_t sym) {
-                return fixed ? (sym < 144 ? 8u : sym < 256 ? 9u : sym < 280 ? 7u : 8u) : (uint32_t)LL[sym];
-            },
-            ord16, [&](uint32_t x, uint32_t sym, uint32_t len) { lt[x] = (uint16_t)ln_lit_entry(sym, len); });
-        if (!ok) bad_mask |= 1u << s;
+    // ---- lit/len (9-bit) and distance (6-bit) tables, one lane per segment (ln_lane_table) -----
+    // The code lengths are first packed to nibbles (symbols 0..255 into the lane's 128 B of the
+    // shared area, 256..287 and the distance lengths into its distance-table area), because the
+    // lit/len table overwrites their bytes [LN_LENS, 1024); the distance table is built last.
+    if (huff && !flags) {
+        const bool fixed = btype == 1;
+        uint32_t* const PK = reinterpret_cast<uint32_t*>(SH + lane * LN_PRE_BYTES);  // words 0..31
+        uint32_t* const PD = reinterpret_cast<uint32_t*>(R + LN_DIST);             // words 32..39
+        const uint32_t* const LW = reinterpret_cast<const uint32_t*>(R + LN_LENS);
+        Pk9 cl = {0ull, 0u}, cd = {0ull, 0u};
+        for (uint32_t k = 0; k < 40; k++) {
+            // fixed code (RFC 1951 3.2.6): 8 (0..143), 9 (144..255), 7 (256..279), 8 (280..287), 5
+            const uint32_t fw = k < 18 ? 0x88888888u : k < 32 ? 0x99999999u : k < 35 ? 0x77777777u
+                              : k < 36 ? 0x88888888u : 0x55555555u;
+            const uint32_t lo = LW[2 * k], hi = LW[2 * k + 1];  // 8 length bytes (each <= 9)
+            auto nib4 = [](uint32_t x) {
+                return (x & 0xFu) | ((x >> 4) & 0xF0u) | ((x >> 8) & 0xF00u) | ((x >> 12) & 0xF000u);
+            };
+            const uint32_t x = fixed ? fw : nib4(lo) | (nib4(hi) << 16);
+            if (k < 32) PK[(k + lane) & 31] = x;  // rotated by lane (bank spread), read back alike
+            else PD[k - 32] = x;
+#pragma unroll
+            for (uint32_t i = 0; i < 8; i++) {
+                if (k < 36) pk_add(cl, (x >> (4 * i)) & 15u);
+                else pk_add(cd, (x >> (4 * i)) & 15u);
+            }
+        }
+        const uint32_t dw0 = PD[4], dw1 = PD[5], dw2 = PD[6], dw3 = PD[7];
+        uint16_t* const lt = reinterpret_cast<uint16_t*>(R);
+        uint16_t* const dt = reinterpret_cast<uint16_t*>(R + LN_DIST);
+        bool ok = ln_lane_table<9>(
+            lt, cl, 288u, [&](uint32_t k) { return k < 32 ? PK[(k + lane) & 31] : PD[k - 32]; },
+            [](uint32_t sym, uint32_t len) { return ln_lit_entry(sym, len); }, 11, 15, 0x7800u);
+        ok = ok && ln_lane_table<6>(
+            dt, cd, 32u, [&](uint32_t k) { return k == 0 ? dw0 : k == 1 ? dw1 : k == 2 ? dw2 : dw3; },
+            [](uint32_t sym, uint32_t len) { return 0x8000u | (len << 8) | sym; }, 8, 7, 0x8700u);
+        if (!ok) flags |= SEGF_EXOTIC;
     }
-    if (seg_lane && ((bad_mask >> lane) & 1u)) flags |= SEGF_EXOTIC;
+    wave_sync();
     if (dbg) dbg[3] = __builtin_amdgcn_s_memtime();
 
     uint32_t endbit = seg_lane ? br.bitpos() : 0u;
@@ -596,30 +674,78 @@ __global__ void k_lane_caps(const uint64_t* cands, uint64_t ncand, uint64_t n, u
     caps[j] = (uint32_t)((c + 3) & ~3ull);
 }
 
-// Wave-cooperative copies inside the 32 KiB window.  ln_copy_plain moves n bytes from s to o
-// with s + n <= o (source wholly before the destination, so every lane copies independently):
-// unaligned head and tail bytes one per lane, the body as 16-byte aligned stores, each lane
-// building its quad from five source words with alignbyte (1 KiB per wave-step).
+// Wave-cooperative copies inside the 32 KiB window.  The body of a copy goes as 16-byte aligned
+// stores, each lane building its quad from five source words with alignbyte; a lane issues the
+// loads of four quads (4 KiB per wave) before their stores, so one LDS latency covers them.
 constexpr uint32_t LN_WIN_WORDS = LN_OUT_CAP / 4;
+// the 16 bytes at window byte s (the fifth word is needed only when s is not word-aligned, and
+// is clamped into the window for the aligned case)
+__device__ __forceinline__ uint4 ln_quad_at(const uint8_t* win, uint32_t s) {
+    const uint32_t* const W = reinterpret_cast<const uint32_t*>(win);
+    const uint32_t i = s >> 2, sh = s & 3;
+    const uint32_t w0 = W[i], w1 = W[i + 1], w2 = W[i + 2], w3 = W[i + 3];
+    const uint32_t w4 = W[min(i + 4, LN_WIN_WORDS - 1)];
+    return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                      __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+}
+
+// ln_copy_plain moves n bytes from s to o with s + n <= o (source wholly before the destination,
+// so every lane copies independently): unaligned head and tail bytes one per lane, the body as
+// aligned quads.
 __device__ __forceinline__ void ln_copy_plain(uint8_t* win, uint32_t o, uint32_t s, uint32_t n) {
     const uint32_t lane = lane_id();
-    const uint32_t* const W = reinterpret_cast<const uint32_t*>(win);
     const uint32_t end = o + n;
     const uint32_t a0 = min((o + 15) & ~15u, end);  // first 16-byte aligned body byte
     const uint32_t a1 = max(a0, end & ~15u);        // first tail byte
     if (lane < a0 - o) win[o + lane] = win[s + lane];
     else if (lane >= 16 && lane - 16 < end - a1) win[a1 + lane - 16] = win[s + (a1 - o) + lane - 16];
     const uint32_t nq = (a1 - a0) >> 4;
-    const uint32_t sb = s + (a0 - o), sh = sb & 3;
-    for (uint32_t k = lane; k < nq; k += 64) {
-        const uint32_t i = (sb >> 2) + 4 * k;
-        // the fifth word is needed only when sh != 0, and then i + 4 < LN_WIN_WORDS (the source
-        // ends before the destination): the clamp only keeps the sh == 0 read in the window
-        const uint32_t w0 = W[i], w1 = W[i + 1], w2 = W[i + 2], w3 = W[i + 3];
-        const uint32_t w4 = W[min(i + 4, LN_WIN_WORDS - 1)];
-        *reinterpret_cast<uint4*>(win + a0 + 16 * k) =
-            make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                       __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+    const uint32_t sb = s + (a0 - o);
+    uint4* const D = reinterpret_cast<uint4*>(win + a0);
+    uint32_t k = lane;
+    for (; k + 192 < nq; k += 256) {
+        const uint4 v0 = ln_quad_at(win, sb + 16 * k), v1 = ln_quad_at(win, sb + 16 * (k + 64));
+        const uint4 v2 = ln_quad_at(win, sb + 16 * (k + 128)), v3 = ln_quad_at(win, sb + 16 * (k + 192));
+        D[k] = v0;
+        D[k + 64] = v1;
+        D[k + 128] = v2;
+        D[k + 192] = v3;
+    }
+    for (; k < nq; k += 64) D[k] = ln_quad_at(win, sb + 16 * k);
+}
+
+// ln_fill_mod: out[o + i] = out[o + (i mod Q)] for i in [P, L), where Q is a multiple of the match
+// distance (so this continues the periodic copy) and the prefix [o, o + Q + 16) is final
+// (P >= Q + 16): every source quad lies in that prefix, so the rest of the match is one pass of
+// independent quad copies.  Lane phases advance by 1024 mod Q per wave-step (one division per
+// lane, at the start).
+__device__ __forceinline__ void ln_fill_mod(uint8_t* win, uint32_t o, uint32_t P, uint32_t L, uint32_t Q) {
+    const uint32_t lane = lane_id();
+    const uint32_t beg = o + P, end = o + L;
+    const uint32_t a0 = min((beg + 15) & ~15u, end);
+    const uint32_t a1 = max(a0, end & ~15u);
+    if (lane < a0 - beg) win[beg + lane] = win[o + (P + lane) % Q];
+    else if (lane >= 16 && lane - 16 < end - a1) win[a1 + lane - 16] = win[o + (a1 - o + lane - 16) % Q];
+    const uint32_t nq = (a1 - a0) >> 4;
+    if (nq <= lane) return;
+    const uint32_t R = 1024u % Q;
+    auto adv = [&](uint32_t r) { r += R; return r >= Q ? r - Q : r; };
+    uint32_t r = (a0 - o + 16 * lane) % Q;  // phase of quad k = lane
+    uint4* const D = reinterpret_cast<uint4*>(win + a0);
+    uint32_t k = lane;
+    for (; k + 192 < nq; k += 256) {
+        const uint32_t r1 = adv(r), r2 = adv(r1), r3 = adv(r2);
+        const uint4 v0 = ln_quad_at(win, o + r), v1 = ln_quad_at(win, o + r1);
+        const uint4 v2 = ln_quad_at(win, o + r2), v3 = ln_quad_at(win, o + r3);
+        D[k] = v0;
+        D[k + 64] = v1;
+        D[k + 128] = v2;
+        D[k + 192] = v3;
+        r = adv(r3);
+    }
+    for (; k < nq; k += 64) {
+        D[k] = ln_quad_at(win, o + r);
+        r = adv(r);
     }
 }
 
@@ -646,9 +772,9 @@ __device__ __forceinline__ void ln_store_tail(uint8_t* q, uint64_t x, uint32_t r
 
 // periodic copy out[o + i] = out[o - d + (i mod d)], i < L (the reference's byte-serial
 // overlapping copy, inflate.hpp:268-270): the first period (or, for d < 64, the largest
-// multiple of d that fits one byte per lane) is built directly; after that the P bytes already
-// at o are the pattern for the next P (P stays a multiple of d), so each further round is a
-// plain copy of the doubled prefix -- log2(L / d) rounds, no division, no wrapping reads.
+// multiple of d that fits one byte per lane) is built directly; the prefix is doubled (a plain
+// copy of itself, P stays a multiple of d) until it holds a multiple Q >= 16 of d plus 16 bytes
+// (at most one doubling), then ln_fill_mod writes the rest in one pass.
 __device__ __forceinline__ void ln_copy_wave(uint8_t* win, uint32_t o, uint32_t L, uint32_t d) {
     if (d >= L) {
         ln_copy_plain(win, o, o - d, L);
@@ -663,27 +789,29 @@ __device__ __forceinline__ void ln_copy_wave(uint8_t* win, uint32_t o, uint32_t 
         P = d * (64 / d);  // 33..64 bytes, a multiple of d
         if (lane < min(P, L)) win[o + lane] = win[o - d + lane % d];
     }
-    while (P < L) {
+    const uint32_t c16 = d >= 16 ? d : d * ((15 + d) / d);  // smallest multiple of d >= 16
+    while (P < L && P < c16 + 16) {
         wave_sync();
         const uint32_t n = min(P, L - P);
         ln_copy_plain(win, o + P, o, n);
         P += n;
     }
+    if (P < L) {
+        wave_sync();
+        ln_fill_mod(win, o, P, L, P - c16);
+    }
 }
 
-__global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs B) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[LN_OUT_CAP];  // exactly 32 KiB: five per CU
+// One segment of k_inflate_resolve: `sf` = its record's {out_size, flags}, n token words at tk.
+__device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j, uint2 sf, uint32_t n,
+                                               const uint32_t* tk, uint8_t* win) {
     const uint32_t lane = threadIdx.x;
-    const uint64_t j = blockIdx.x;
-    const SegRecord rec = A.recs[j];
-    if (rec.flags & ~SEGF_FINAL) return;
+    if (sf.y & ~SEGF_FINAL) return;
     const uint64_t dst0 = j * (uint64_t)A.slot;
     if (dst0 >= A.cap) return;
-    const uint32_t size = rec.out_size;
+    const uint32_t size = sf.x;
     const uint32_t nb = (uint32_t)min((uint64_t)size, A.cap - dst0);
     uint8_t* const dst = A.out + dst0;
-    const uint32_t n = B.ntok[j];
-    const uint32_t* const tk = B.tok + B.tokoff[j];
     if (n == 0) return;
     const uint32_t w0 = tk[0];
     if ((w0 >> 24) == 0) {  // stored segment: straight from the stream, 16-byte stores
@@ -710,13 +838,11 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
     if (dbg) dbg[5] = __builtin_amdgcn_s_memtime();
     uint32_t pos = 0, n_cx = 0;
     uint64_t c_simple = 0, c_cx = 0, tstep0 = dbg ? __builtin_amdgcn_s_memtime() : 0;  // DMX_PHASES
-    uint32_t wnext = tk[min(lane, n - 1)];
-    for (uint32_t t0 = 0; t0 < n; t0 += 64) {
-        // this step's 64 token words were loaded one step ahead: the memory latency of the next
-        // step's load passes while this step's copies run (unconditional, index clamped, so the
-        // wait before the use is for the older load only)
-        const uint32_t w = t0 + lane < n ? wnext : 0u;
-        wnext = tk[min(t0 + 64 + lane, n - 1)];
+    // One step = 64 token words, loaded one step ahead: the memory latency of the next step's
+    // load passes while this step's copies run (unconditional, index clamped, so the wait before
+    // the use is for the older load only; four steps ahead measured the same on text).
+    auto tstep = [&](uint32_t t0, uint32_t wraw) {
+        const uint32_t w = t0 + lane < n ? wraw : 0u;
         const bool ism = (w >> 31) != 0;
         const uint32_t L = ism ? (w >> 15) & 0xFFFFu : (w >> 24) & 0x7Fu;
         const uint32_t d = (w & 0x7FFFu) + 1;
@@ -779,6 +905,13 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
             c_cx += tstep0 - tcx0;
         }
         pos += tot;
+    };
+    auto ldw = [&](uint32_t t) { return tk[min(t + lane, n - 1)]; };
+    uint32_t wa = ldw(0);
+    for (uint32_t t0 = 0; t0 < n; t0 += 64) {
+        const uint32_t w = wa;
+        wa = ldw(t0 + 64);
+        tstep(t0, w);
     }
     if (dbg) {
         dbg[6] = __builtin_amdgcn_s_memtime();
@@ -804,6 +937,15 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
         for (uint32_t i = lane; i < nb; i += 64) dst[i] = win[i];
     }
     if (dbg) dbg[7] = __builtin_amdgcn_s_memtime();
+}
+
+// one workgroup per segment (a persistent grid with ticket-drawn segments and the next record
+// prefetched measured 5-20% slower on repeat and zeros, equal on text)
+__global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs B) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[LN_OUT_CAP];  // exactly 32 KiB: five per CU
+    const uint64_t j = blockIdx.x;
+    const SegRecord* const rp = &A.recs[j];
+    ln_resolve_one(A, j, make_uint2(rp->out_size, rp->flags), B.ntok[j], B.tok + B.tokoff[j], win);
 }
 
 hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* tokoff,
