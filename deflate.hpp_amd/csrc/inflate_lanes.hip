@@ -176,7 +176,7 @@ __device__ __forceinline__ void pk_add(Pk9& p, uint32_t L) {  // L in 0..9 (0: n
 // (a "seed", below 2^L); the table is then completed level by level: for b = 1 .. B-1 every entry
 // in [0, 2^b) of length <= b is copied to + 2^b (a longer code's seed stays, and its own positions
 // come from its seed).  Entries not yet written hold `mark` (a length above B).  Index rotation
-// by lane keeps the lanes' accesses (regions 1152 B apart) off a common bank.  Returns false
+// by lane keeps the lanes' accesses (regions 1152 B apart) off a common bank.  B >= 6.  Returns false
 // unless the code is complete.
 template <int B, class Word, class Ent>
 __device__ __forceinline__ bool ln_lane_table(uint16_t* T, const Pk9& cnt, uint32_t nsym, Word word, Ent ent,
@@ -193,10 +193,11 @@ __device__ __forceinline__ bool ln_lane_table(uint16_t* T, const Pk9& cnt, uint3
         else nc.hi |= code << (9 * (l - 7));
     }
     if (kraft != (1u << B)) return false;
-    uint32_t* const T32 = reinterpret_cast<uint32_t*>(T);
     constexpr uint32_t NW = (1u << B) / 2;  // table words
+    uint64_t* const T64w = reinterpret_cast<uint64_t*>(T);
+    const uint64_t m4 = (uint64_t)(mark | (mark << 16)) * 0x0000000100000001ull;
 #pragma unroll 4
-    for (uint32_t w = 0; w < NW; w++) T32[(w + lane) & (NW - 1)] = mark | (mark << 16);
+    for (uint32_t w = 0; w < NW / 2; w++) T64w[(w + lane) & (NW / 2 - 1)] = m4;
     for (uint32_t k = 0; 8 * k < nsym; k++) {
         const uint32_t x = word(k);
 #pragma unroll
@@ -209,14 +210,28 @@ __device__ __forceinline__ bool ln_lane_table(uint16_t* T, const Pk9& cnt, uint3
             pk_add(nc, L);
         }
     }
+    auto put = [&](uint32_t q, uint32_t e, uint32_t b) {
+        if (((e >> lsh) & lmask) <= b) T[q] = (uint16_t)e;
+    };
+    // levels 1 and 2 entry by entry; from level 3 on (n >= 8) the reads of a batch go first (8
+    // entries as two 8-byte reads, 4-entry aligned, rotated by 4 * lane), then the writes
+    // (reads in [0, n), writes in [n, 2n): no overlap)
+    put(2, T[0], 1);
+    put(3, T[1], 1);
 #pragma unroll
-    for (uint32_t b = 1; b < (uint32_t)B; b++) {
+    for (uint32_t i = 0; i < 4; i++) put(4 + i, T[i], 2);
+    const uint64_t* const T64 = reinterpret_cast<const uint64_t*>(T);
+#pragma unroll
+    for (uint32_t b = 3; b < (uint32_t)B; b++) {
         const uint32_t n = 1u << b;
-#pragma unroll 8
-        for (uint32_t i = 0; i < n; i++) {
-            const uint32_t q = (i + 2 * lane) & (n - 1);
-            const uint32_t e = T[q];
-            if (((e >> lsh) & lmask) <= b) T[q + n] = (uint16_t)e;
+        for (uint32_t i = 0; i < n; i += 8) {
+            const uint32_t q0 = (i + 4 * lane) & (n - 1), q1 = (q0 + 4) & (n - 1);
+            const uint64_t v0 = T64[q0 >> 2], v1 = T64[q1 >> 2];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                put(q0 + n + k, (uint32_t)(v0 >> (16 * k)) & 0xFFFFu, b);
+                put(q1 + n + k, (uint32_t)(v1 >> (16 * k)) & 0xFFFFu, b);
+            }
         }
     }
     return true;
@@ -774,7 +789,7 @@ __device__ __forceinline__ void ln_store_tail(uint8_t* q, uint64_t x, uint32_t r
 // overlapping copy, inflate.hpp:268-270): the first period (or, for d < 64, the largest
 // multiple of d that fits one byte per lane) is built directly; the prefix is doubled (a plain
 // copy of itself, P stays a multiple of d) until it holds a multiple Q >= 16 of d plus 16 bytes
-// (at most one doubling), then ln_fill_mod writes the rest in one pass.
+// and the rest is more than 3 prefixes long, then ln_fill_mod writes the rest in one pass.
 __device__ __forceinline__ void ln_copy_wave(uint8_t* win, uint32_t o, uint32_t L, uint32_t d) {
     if (d >= L) {
         ln_copy_plain(win, o, o - d, L);
@@ -789,8 +804,11 @@ __device__ __forceinline__ void ln_copy_wave(uint8_t* win, uint32_t o, uint32_t 
         P = d * (64 / d);  // 33..64 bytes, a multiple of d
         if (lane < min(P, L)) win[o + lane] = win[o - d + lane % d];
     }
-    const uint32_t c16 = d >= 16 ? d : d * ((15 + d) / d);  // smallest multiple of d >= 16
-    while (P < L && P < c16 + 16) {
+    // smallest multiple of d >= 16 (d < 16: d * ceil(16 / d), no division)
+    const uint32_t c16 = d >= 16 ? d : d * (d == 1 ? 16u : d == 2 ? 8u : d == 3 ? 6u : d <= 5 ? 4u : d <= 7 ? 3u : 2u);
+    // doubling while the rest is short (at most two more rounds: no divisions), or until the
+    // prefix holds c16 + 16 bytes
+    while (P < L && (P < c16 + 16 || L <= 4 * P)) {
         wave_sync();
         const uint32_t n = min(P, L - P);
         ln_copy_plain(win, o + P, o, n);
