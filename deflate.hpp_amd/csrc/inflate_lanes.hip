@@ -831,9 +831,12 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
     const uint32_t nb = (uint32_t)min((uint64_t)size, A.cap - dst0);
     uint8_t* const dst = A.out + dst0;
     if (n == 0) return;
-    const uint32_t w0 = tk[0];
+    // the first step's token words are loaded together with word 0 (one memory latency)
+    uint32_t wa = tk[min(lane, n - 1)];
+    const uint32_t w0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)wa);  // lane 0 holds word 0
     if ((w0 >> 24) == 0) {  // stored segment: straight from the stream, 16-byte stores
-        const uint8_t* src = reinterpret_cast<const uint8_t*>(A.in_words) + A.misalign + A.cands[j] + tk[1];
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(A.in_words) + A.misalign + A.cands[j] +
+                           (uint32_t)__builtin_amdgcn_readlane((int)wa, 1);  // word 1 (n = 2)
         if ((((uintptr_t)dst) & 15) == 0) {
             // word-aligned source base; the words read stay inside the stream (its last word
             // holds the last data byte) except the fifth at sh == 0, which is not used then
@@ -925,7 +928,6 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
         pos += tot;
     };
     auto ldw = [&](uint32_t t) { return tk[min(t + lane, n - 1)]; };
-    uint32_t wa = ldw(0);
     for (uint32_t t0 = 0; t0 < n; t0 += 64) {
         const uint32_t w = wa;
         wa = ldw(t0 + 64);
