@@ -690,8 +690,7 @@ __global__ void k_lane_caps(const uint64_t* cands, uint64_t ncand, uint64_t n, u
 }
 
 // Wave-cooperative copies inside the 32 KiB window.  The body of a copy goes as 16-byte aligned
-// stores, each lane building its quad from five source words with alignbyte; a lane issues the
-// loads of four quads (4 KiB per wave) before their stores, so one LDS latency covers them.
+// stores, each lane building its quad from five source words with alignbyte.
 constexpr uint32_t LN_WIN_WORDS = LN_OUT_CAP / 4;
 // the 16 bytes at window byte s (the fifth word is needed only when s is not word-aligned, and
 // is clamped into the window for the aligned case)
@@ -706,27 +705,27 @@ __device__ __forceinline__ uint4 ln_quad_at(const uint8_t* win, uint32_t s) {
 
 // ln_copy_plain moves n bytes from s to o with s + n <= o (source wholly before the destination,
 // so every lane copies independently): unaligned head and tail bytes one per lane, the body as
-// aligned quads.
+// aligned quads (one quad per lane and wave-step: these copies are mostly short).
 __device__ __forceinline__ void ln_copy_plain(uint8_t* win, uint32_t o, uint32_t s, uint32_t n) {
     const uint32_t lane = lane_id();
+    const uint32_t* const W = reinterpret_cast<const uint32_t*>(win);
     const uint32_t end = o + n;
     const uint32_t a0 = min((o + 15) & ~15u, end);  // first 16-byte aligned body byte
     const uint32_t a1 = max(a0, end & ~15u);        // first tail byte
     if (lane < a0 - o) win[o + lane] = win[s + lane];
     else if (lane >= 16 && lane - 16 < end - a1) win[a1 + lane - 16] = win[s + (a1 - o) + lane - 16];
     const uint32_t nq = (a1 - a0) >> 4;
-    const uint32_t sb = s + (a0 - o);
-    uint4* const D = reinterpret_cast<uint4*>(win + a0);
-    uint32_t k = lane;
-    for (; k + 192 < nq; k += 256) {
-        const uint4 v0 = ln_quad_at(win, sb + 16 * k), v1 = ln_quad_at(win, sb + 16 * (k + 64));
-        const uint4 v2 = ln_quad_at(win, sb + 16 * (k + 128)), v3 = ln_quad_at(win, sb + 16 * (k + 192));
-        D[k] = v0;
-        D[k + 64] = v1;
-        D[k + 128] = v2;
-        D[k + 192] = v3;
+    const uint32_t sb = s + (a0 - o), sh = sb & 3;
+    for (uint32_t k = lane; k < nq; k += 64) {
+        const uint32_t i = (sb >> 2) + 4 * k;
+        // the fifth word is needed only when sh != 0, and then i + 4 < LN_WIN_WORDS (the source
+        // ends before the destination): the clamp only keeps the sh == 0 read in the window
+        const uint32_t w0 = W[i], w1 = W[i + 1], w2 = W[i + 2], w3 = W[i + 3];
+        const uint32_t w4 = W[min(i + 4, LN_WIN_WORDS - 1)];
+        *reinterpret_cast<uint4*>(win + a0 + 16 * k) =
+            make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                       __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
     }
-    for (; k < nq; k += 64) D[k] = ln_quad_at(win, sb + 16 * k);
 }
 
 // ln_fill_mod: out[o + i] = out[o + (i mod Q)] for i in [P, L), where Q is a multiple of the match
