@@ -59,7 +59,8 @@ struct InflateArgs {
                                  // 2 = k_inflate_pj (segment j at j * slot),
                                  // 3 = k_inflate_segments redoing only SEGF_EXOTIC candidates
                                  //     of a mode-2 / mode-4 pass, at the same slots,
-                                 // 4 = k_inflate_lanes + k_inflate_resolve (segment j at j * slot)
+                                 // 4 = k_inflate_lanes + k_inflate_resolve (segment j at j * slot),
+                                 // 6 = k_inflate_pj_list patching the heavy candidates of mode 4
     uint32_t slot;               // mode 2: segment bytes (16384 or 32768)
     uint64_t* dbg;               // optional per-segment phase timestamps (DMX_PHASES)
 };
@@ -95,9 +96,16 @@ hipError_t launch_inflate_pj(const InflateArgs& A, uint32_t seg, hipStream_t st,
 // lane-per-segment Huffman decode (k_inflate_lanes) + wave-per-segment LZ77 resolve
 // (k_inflate_resolve); segment j lands at j * A.slot (mode 4).  tok holds
 // min(ncand * 16404, 8 * n + 20 * ncand) words; tokoff ncand + 1, ntok / caps ncand entries.
+// heavy != 0: candidates spanning more than `heavy` bytes are declined and listed in hl
+// (hl[0] = count, then ncand indices at most) for launch_inflate_pj_list.
 hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* tokoff,
-                                uint32_t* ntok, uint32_t* caps, hipStream_t st, hipEvent_t ev0,
-                                hipEvent_t ev1);
+                                uint32_t* ntok, uint32_t* caps, uint32_t heavy, uint32_t* hl,
+                                hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_heavy_count(const uint64_t* cands, uint64_t ncand, uint64_t n, uint32_t heavy, uint32_t* cnt,
+                              hipStream_t st);
+// mode 6: the workgroup decoder over the candidates listed in hl, `grid` persistent workgroups
+hipError_t launch_inflate_pj_list(const InflateArgs& A, uint32_t seg, const uint32_t* hl, uint32_t grid,
+                                  hipStream_t st, hipEvent_t ev1);
 // validation scratch: five device words, zeroed by the launch
 struct ValidateWords {
     unsigned long long kmin, bmin, umin, xmin, xcnt;

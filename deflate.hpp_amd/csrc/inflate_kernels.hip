@@ -476,13 +476,11 @@ __device__ __forceinline__ uint32_t tok_bytes(uint32_t k, uint32_t a, uint32_t d
 }
 
 template <int SEG, int NT>
-__global__ __launch_bounds__(NT) void k_inflate_pj(InflateArgs A) {
+__device__ __forceinline__ void pj_segment(const InflateArgs& A, PjSmem<SEG, NT>& S, const uint64_t j) {
     using Smem = PjSmem<SEG, NT>;
-    __shared__ __attribute__((aligned(16))) Smem S;
     constexpr int NW = NT / 64;
     const int t = threadIdx.x;
     const int wave = t >> 6;
-    const uint64_t j = blockIdx.x;
     const bool rfc = (A.flags & DMX_CFG_RFC_STRICT) != 0;
     const uint64_t obase = j * (uint64_t)SEG;
     const uint64_t end_bytes = A.misalign + A.n;
@@ -931,6 +929,34 @@ __global__ __launch_bounds__(NT) void k_inflate_pj(InflateArgs A) {
         A.recs[j].offset = obase;
     }
     DMX_PHASE(A.dbg, j, 6);
+}
+
+template <int SEG, int NT>
+__global__ __launch_bounds__(NT) void k_inflate_pj(InflateArgs A) {
+    __shared__ __attribute__((aligned(16))) PjSmem<SEG, NT> S;
+    pj_segment<SEG, NT>(A, S, blockIdx.x);
+}
+
+// Heavy-segment patch (mode 6): the candidates listed by k_lane_caps (hl[0] = count, then the
+// indices) are decoded by persistent workgroups, candidate hl[1 + k] by workgroup k mod G.
+template <int SEG, int NT>
+__global__ __launch_bounds__(NT) void k_inflate_pj_list(InflateArgs A, const uint32_t* hl) {
+    __shared__ __attribute__((aligned(16))) PjSmem<SEG, NT> S;
+    const uint32_t cnt = hl[0];
+    for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+        pj_segment<SEG, NT>(A, S, hl[1 + k]);
+        __syncthreads();  // the next candidate reuses the LDS
+    }
+}
+
+hipError_t launch_inflate_pj_list(const InflateArgs& A, uint32_t seg, const uint32_t* hl, uint32_t grid,
+                                  hipStream_t st, hipEvent_t ev1) {
+    if (seg == 16384)
+        hipLaunchKernelGGL((k_inflate_pj_list<16384, 256>), dim3(grid), dim3(256), 0, st, A, hl);
+    else
+        hipLaunchKernelGGL((k_inflate_pj_list<32768, 512>), dim3(grid), dim3(512), 0, st, A, hl);
+    if (ev1) (void)hipEventRecord(ev1, st);
+    return hipGetLastError();
 }
 
 hipError_t launch_inflate_pj(const InflateArgs& A, uint32_t seg, hipStream_t st, hipEvent_t ev0,

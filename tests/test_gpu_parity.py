@@ -225,6 +225,28 @@ def test_device_roundtrip_256MiB_mixed_and_shards(ctx):
     assert e.value.code == dmx.DMX_ERR_CAPACITY
 
 
+@pytest.mark.parametrize("kind,mib", [("text", 1), ("bmp", 24), ("mixed", 24), ("bmp", 96), ("text", 96)])
+def test_inflate_heavy_candidates_workgroup_decoder(ctx, oracle, kind, mib):
+    """Streams of few candidates send their dense segments (> 2 KiB compressed) to the workgroup
+    decoder (mode 6); at 96 MiB (3072 candidates) the route follows the heavy count.  Either way
+    the output is the input, and the 1 MiB one matches the oracle."""
+    import torch
+    n = mib << 20
+    host = torch.empty(n, dtype=torch.uint8).pin_memory()
+    dmx.corpus_into(kind, n, host.data_ptr())
+    d_in = host.cuda()
+    cap = dmx.deflate_bound(n) + 64
+    d_c = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    d_o = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    clen = ctx.deflate_device(d_in.data_ptr(), n, 2, d_c.data_ptr(), cap)
+    olen = ctx.inflate_device(d_c.data_ptr(), clen, d_o.data_ptr(), n + 64)
+    assert olen == n and torch.equal(d_o[:n], d_in)
+    assert ctx.stats().path == 4
+    if mib == 1:
+        s = d_c[:clen].cpu().numpy().tobytes()
+        assert oracle.inflate(s) == host.numpy().tobytes() == ctx.decompress(s)
+
+
 def test_device_roundtrip_1GiB_repeat_checksum(ctx):
     import torch
     n = 1 << 30
