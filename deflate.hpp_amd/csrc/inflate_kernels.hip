@@ -363,6 +363,9 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
 constexpr uint32_t PJ_LIT = 0x8000u;
 constexpr int PJ_ROUNDS = 64;
 constexpr uint32_t PJ_MINBITS = 256;
+#ifndef PJ_WARM
+#define PJ_WARM 192u  // warm-up bits before a range's first pass
+#endif
 constexpr int PJ_LL = 12;  // lit/len lookup bits
 constexpr int PJ_LD = 10;  // distance lookup bits
 
@@ -631,10 +634,27 @@ __device__ __forceinline__ void pj_segment(const InflateArgs& A, PjSmem<SEG, NT>
         if (t < 2) S.te2[t] = NT;
         __syncthreads();
         // ---- 2. first pass over the ranges (positions relative to hs) ----
-        uint32_t qc = sp, cc = 0;  // token boundary ccap of the first pass, its count
+        // Warm-up: a range's first pass starts PJ_WARM bits before the range and decodes up to
+        // it without recording, so by the range start it has usually synchronised with the
+        // true token path; its first boundary >= sp is then where the previous range's path
+        // crosses in, and no settle redo is needed (text: 16.6 settle rounds per segment
+        // without it, the redos cascading through ranges that had not synchronised).
+        uint32_t s0 = sp;
+        if (r > 0 && r < nl) {
+            uint32_t p = sp > PJ_WARM ? sp - PJ_WARM : 0u, pa = hs + p;
+            bool ok = true;
+            while (p < sp) {
+                uint32_t a, d;
+                const uint32_t k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
+                if (k == TK_BAD || k == TK_EOB) { ok = false; break; }
+                p = pa - hs;
+            }
+            if (ok && p < sp1) s0 = p;
+        }
+        uint32_t qc = s0, cc = 0;  // token boundary ccap of the first pass, its count
         uint32_t e1, cnt1 = 0, st1 = 0, nb = 0;
         {
-            uint32_t p = sp, pa = hs + sp;
+            uint32_t p = s0, pa = hs + s0;
             while (p < sp1) {
                 atomicOr(&bmap[p >> 5], 1u << (p & 31));
                 uint32_t a, d;
@@ -653,7 +673,7 @@ __device__ __forceinline__ void pj_segment(const InflateArgs& A, PjSmem<SEG, NT>
         // per round: [publish end, first ending range] | read te, want | or-barrier | redo |
         // barrier.  Every shared word is written and read on opposite sides of a barrier; the
         // first-ending-range minimum alternates between two words (one reset per round).
-        uint32_t s = sp, e = e1, cnt = cnt1, st = st1;
+        uint32_t s = s0, e = e1, cnt = cnt1, st = st1;
         uint32_t te = NT;
         bool settled = false;
         uint32_t settle_rounds = 0;
