@@ -94,8 +94,6 @@ struct Scal {  // small device-side scalars, one allocation
     uint64_t nmarkers;
     uint32_t ticket;
     uint32_t fb_err;  // block-parallel path: a copy reached before the stream start
-    uint32_t heavy;   // heavy candidates of a mid-size stream (mode 6 decision)
-    uint32_t pad_;
     InflateResult res;
     ValidateWords vw;
 };
@@ -418,43 +416,32 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
         const char* e = std::getenv("DMX_INFLATE_PATH");
         return e ? std::atoi(e) : -1;
     }();
-    // Heavy candidates (mode 6): a lane decodes about one symbol per 1000 cycles, so in a stream
-    // of few candidates the lane decoder's time is the serial decode of its densest segment
-    // (a 24 MiB bitmap: 6 ms for ~10K symbols).  Candidates spanning more than heavy_bytes
-    // compressed bytes go to the workgroup decoder instead (k_inflate_pj: the segment's bits
-    // split over 512 lanes, ~0.4 ms per dense segment on one CU): always up to 2048 candidates,
-    // and up to heavy_maxcand when at most 12 rounds of the CUs' workgroups take them (counted
-    // first).  Above that the lanes' throughput wins (a 1 GiB stream fills every SIMD).
+    // Heavy candidates (mode 6): a lane decodes about one symbol per 1000 cycles, so the lane
+    // decoder takes as long as the serial decode of the densest segment in a wave (a 24 MiB
+    // bitmap: 6 ms for ~10K symbols).  Candidates spanning more than heavy_bytes compressed
+    // bytes go to the workgroup decoder instead (k_inflate_pj: the segment's bits split over 512
+    // lanes, ~0.17 ms per dense segment on one CU): always up to 2048 candidates, beyond that
+    // when the device-side count finds at most 32 per CU (32 rounds of workgroups, ~5.5 ms;
+    // more dense segments than that keep the lanes' throughput: 1 GiB of text).
     static const uint32_t heavy_bytes = [] {
         const char* e = std::getenv("DMX_HEAVY_BYTES");
         return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 2048u;
-    }();
-    static const uint64_t heavy_maxcand = [] {
-        const char* e = std::getenv("DMX_HEAVY_MAXCAND");
-        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : 16384ull;
     }();
     const bool few_bits = n / ncand < 4096;
     uint32_t plan[8][2];
     int np = 0;
     r.status = 2;
-    uint32_t heavy = 0;
+    uint32_t heavy = 0, heavy_limit = 0;
     if (path_env == -1 || path_env == 4) {
         const uint64_t words = std::min<uint64_t>(ncand * 16404ull, 8ull * n + 20ull * ncand);  // k_lane_caps
         if (c->ltok.ensure(words * 4) && c->ltokoff.ensure((ncand + 1) * 8) &&
             c->lntok.ensure(ncand * 4) && c->lcaps.ensure(ncand * 4)) {
             plan[np][0] = 4, plan[np][1] = c->seg, np++;
-            bool route = heavy_bytes && ncand <= heavy_maxcand && c->lheavy.ensure((ncand + 1) * 4);
-            if (route && ncand > 2048) {
+            if (heavy_bytes && ncand < 0xFFFFFFF0ull && c->lheavy.ensure((ncand + 2) * 4)) {
                 if (c->ncu <= 0 && hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
                     c->ncu = 256;
-                uint32_t nh = 0;
-                HIPCHK(launch_heavy_count(c->cands.as<uint64_t>(), ncand, n, heavy_bytes, &ds->heavy, st));
-                HIPCHK(hipMemcpyAsync(&nh, &ds->heavy, 4, hipMemcpyDeviceToHost, st));
-                HIPCHK(hipStreamSynchronize(st));
-                route = nh <= 12u * (uint32_t)std::max(c->ncu, 1);
-            }
-            if (route) {
                 heavy = heavy_bytes;
+                heavy_limit = ncand <= 2048 ? 0xFFFFFFFFu : 32u * (uint32_t)std::max(c->ncu, 1);
                 plan[np][0] = 6, plan[np][1] = c->seg, np++;  // the heavy candidates
             }
             plan[np][0] = 3, plan[np][1] = c->seg, np++;  // patch the declined candidates
@@ -489,10 +476,8 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
         if (mode == 4) {
             HIPCHK(launch_inflate_lanes(A, c->ltok.as<uint32_t>(), c->ltokoff.as<uint64_t>(),
                                         c->lntok.as<uint32_t>(), c->lcaps.as<uint32_t>(), heavy,
-                                        c->lheavy.as<uint32_t>(), st, e0, e1));
+                                        heavy_limit, c->lheavy.as<uint32_t>(), st, e0, e1));
         } else if (mode == 6) {
-            if (c->ncu <= 0 && hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
-                c->ncu = 256;
             const uint32_t grid = (uint32_t)std::min<uint64_t>(r.exotic, (uint64_t)std::max(c->ncu, 1));
             HIPCHK(launch_inflate_pj_list(A, A.slot, c->lheavy.as<uint32_t>(), grid, st, e1));
         } else if (mode == 2) {

@@ -96,13 +96,12 @@ hipError_t launch_inflate_pj(const InflateArgs& A, uint32_t seg, hipStream_t st,
 // lane-per-segment Huffman decode (k_inflate_lanes) + wave-per-segment LZ77 resolve
 // (k_inflate_resolve); segment j lands at j * A.slot (mode 4).  tok holds
 // min(ncand * 16404, 8 * n + 20 * ncand) words; tokoff ncand + 1, ntok / caps ncand entries.
-// heavy != 0: candidates spanning more than `heavy` bytes are declined and listed in hl
-// (hl[0] = count, then ncand indices at most) for launch_inflate_pj_list.
+// heavy != 0: when at most `limit` candidates span more than `heavy` bytes (counted on the
+// device into hl[1]), those are declined and listed in hl (hl[0] = count, the indices from
+// hl[2] on; ncand + 2 words) for launch_inflate_pj_list.
 hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* tokoff,
-                                uint32_t* ntok, uint32_t* caps, uint32_t heavy, uint32_t* hl,
-                                hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
-hipError_t launch_heavy_count(const uint64_t* cands, uint64_t ncand, uint64_t n, uint32_t heavy, uint32_t* cnt,
-                              hipStream_t st);
+                                uint32_t* ntok, uint32_t* caps, uint32_t heavy, uint32_t limit,
+                                uint32_t* hl, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 // mode 6: the workgroup decoder over the candidates listed in hl, `grid` persistent workgroups
 hipError_t launch_inflate_pj_list(const InflateArgs& A, uint32_t seg, const uint32_t* hl, uint32_t grid,
                                   hipStream_t st, hipEvent_t ev1);

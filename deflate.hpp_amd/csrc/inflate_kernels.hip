@@ -364,7 +364,7 @@ constexpr uint32_t PJ_LIT = 0x8000u;
 constexpr int PJ_ROUNDS = 64;
 constexpr uint32_t PJ_MINBITS = 256;
 #ifndef PJ_WARM
-#define PJ_WARM 192u  // warm-up bits before a range's first pass
+#define PJ_WARM 320u  // warm-up bits before a range's first pass (128: +25 % on text, 512: +1 %)
 #endif
 constexpr int PJ_LL = 12;  // lit/len lookup bits
 constexpr int PJ_LD = 10;  // distance lookup bits
@@ -957,14 +957,15 @@ __global__ __launch_bounds__(NT) void k_inflate_pj(InflateArgs A) {
     pj_segment<SEG, NT>(A, S, blockIdx.x);
 }
 
-// Heavy-segment patch (mode 6): the candidates listed by k_lane_caps (hl[0] = count, then the
-// indices) are decoded by persistent workgroups, candidate hl[1 + k] by workgroup k mod G.
+// Heavy-segment patch (mode 6): the candidates listed by k_lane_caps (hl[0] = count, the
+// indices from hl[2] on) are decoded by persistent workgroups, candidate hl[2 + k] by workgroup
+// k mod G.
 template <int SEG, int NT>
 __global__ __launch_bounds__(NT) void k_inflate_pj_list(InflateArgs A, const uint32_t* hl) {
     __shared__ __attribute__((aligned(16))) PjSmem<SEG, NT> S;
     const uint32_t cnt = hl[0];
     for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
-        pj_segment<SEG, NT>(A, S, hl[1 + k]);
+        pj_segment<SEG, NT>(A, S, hl[2 + k]);
         __syncthreads();  // the next candidate reuses the LDS
     }
 }

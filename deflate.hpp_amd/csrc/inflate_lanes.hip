@@ -680,19 +680,20 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
 // rounded to whole 16-byte groups.  A segment of at most 32 KiB needs at most 16 Ki + 1 words:
 // a literal-run word holds up to 3 bytes and two consecutive ones hold >= 4 (a short run is
 // followed by a match), a match word >= 3 bytes, so words <= bytes / 2 + 1.
-// With heavy != 0, a candidate spanning more than `heavy` compressed bytes gets capacity 0 (the
-// lane declines it: SEGF_EXOTIC) and is appended to hl (hl[0] = count, zeroed by the caller)
-// for the workgroup decoder (mode 6): a lane decodes ~1 symbol per 1000 cycles, so a dense
-// segment alone would set the time of a small stream.
+// With heavy != 0 and at most `limit` heavy candidates in the stream (hl[1], counted by
+// k_heavy_count), a candidate spanning more than `heavy` compressed bytes gets capacity 0 (the
+// lane declines it: SEGF_EXOTIC) and is appended to the list hl[2..] (hl[0] = its length)
+// for the workgroup decoder (mode 6): a lane decodes ~1 symbol per 1000 cycles, so one dense
+// segment sets the time of a wave.
 __global__ void k_lane_caps(const uint64_t* cands, uint64_t ncand, uint64_t n, uint32_t* caps,
-                            uint32_t heavy, uint32_t* hl) {
+                            uint32_t heavy, uint32_t limit, uint32_t* hl) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= ncand) return;
     const uint64_t nxt = j + 1 < ncand ? cands[j + 1] : n;
     const uint64_t span = nxt - cands[j];
-    if (heavy && span > heavy) {
+    if (heavy && span > heavy && hl[1] <= limit) {
         caps[j] = 0;
-        hl[1 + atomicAdd(hl, 1u)] = (uint32_t)j;
+        hl[2 + atomicAdd(hl, 1u)] = (uint32_t)j;
         return;
     }
     const uint64_t bits = 8 * span;
@@ -986,24 +987,18 @@ __global__ void k_heavy_count(const uint64_t* cands, uint64_t ncand, uint64_t n,
     const uint64_t b = __ballot(nxt - cands[j] > heavy);
     if (lane_id() == 0 && b) atomicAdd(cnt, (uint32_t)__popcll(b));  // lane 0 holds the wave's first j
 }
-hipError_t launch_heavy_count(const uint64_t* cands, uint64_t ncand, uint64_t n, uint32_t heavy, uint32_t* cnt,
-                              hipStream_t st) {
-    const hipError_t e = hipMemsetAsync(cnt, 0, 4, st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_heavy_count, dim3((uint32_t)((ncand + 255) / 256)), dim3(256), 0, st, cands, ncand, n, heavy, cnt);
-    return hipGetLastError();
-}
 
 hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* tokoff,
-                                uint32_t* ntok, uint32_t* caps, uint32_t heavy, uint32_t* hl,
-                                hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+                                uint32_t* ntok, uint32_t* caps, uint32_t heavy, uint32_t limit,
+                                uint32_t* hl, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     if (ev0) (void)hipEventRecord(ev0, st);
     const uint32_t g = (uint32_t)((A.ncand + 255) / 256);
     if (heavy) {
-        const hipError_t e = hipMemsetAsync(hl, 0, 4, st);
+        const hipError_t e = hipMemsetAsync(hl, 0, 8, st);
         if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_heavy_count, dim3(g), dim3(256), 0, st, A.cands, A.ncand, A.n, heavy, hl + 1);
     }
-    hipLaunchKernelGGL(k_lane_caps, dim3(g), dim3(256), 0, st, A.cands, A.ncand, A.n, caps, heavy, hl);
+    hipLaunchKernelGGL(k_lane_caps, dim3(g), dim3(256), 0, st, A.cands, A.ncand, A.n, caps, heavy, limit, hl);
     hipError_t e = launch_scan_u32(caps, tokoff, A.ncand, tokoff + A.ncand, st);
     if (e != hipSuccess) return e;
     LaneArgs B{tok, tokoff, ntok, caps};
