@@ -163,7 +163,8 @@ typedef struct dmx_stats {
                                3 = workgroup-per-segment decoder (32 KiB slots),
                                4 = lane decoder + wave resolve (the default for libdmx
                                    streams: one lane decodes a segment's tokens, one
-                                   wavefront rebuilds its bytes),
+                                   wavefront rebuilds its bytes; dense segments of streams
+                                   with few of them go to the workgroup decoder instead),
                                5 = block-parallel decoder for streams without segment
                                    markers (zlib's, libdeflate's, the reference's own):
                                    header scan, one wavefront per unit of blocks, window
