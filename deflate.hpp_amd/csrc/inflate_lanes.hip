@@ -680,18 +680,25 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
 // rounded to whole 16-byte groups.  A segment of at most 32 KiB needs at most 16 Ki + 1 words:
 // a literal-run word holds up to 3 bytes and two consecutive ones hold >= 4 (a short run is
 // followed by a match), a match word >= 3 bytes, so words <= bytes / 2 + 1.
+// A dense candidate spans more than `heavy` compressed bytes and does not start with a stored
+// block (BTYPE 00: the lanes pass a stored segment on as one token, the resolve copies it).
+__device__ __forceinline__ bool ln_dense(const uint8_t* in, uint64_t start, uint64_t n, uint64_t span,
+                                        uint32_t heavy) {
+    return span > heavy && start < n && ((in[start] >> 1) & 3u) != 0u;
+}
+
 // With heavy != 0 and at most `limit` heavy candidates in the stream (hl[1], counted by
-// k_heavy_count), a candidate spanning more than `heavy` compressed bytes gets capacity 0 (the
+// k_heavy_count), a dense candidate (ln_dense) gets capacity 0 (the
 // lane declines it: SEGF_EXOTIC) and is appended to the list hl[2..] (hl[0] = its length)
 // for the workgroup decoder (mode 6): a lane decodes ~1 symbol per 1000 cycles, so one dense
 // segment sets the time of a wave.
-__global__ void k_lane_caps(const uint64_t* cands, uint64_t ncand, uint64_t n, uint32_t* caps,
+__global__ void k_lane_caps(const uint8_t* in, const uint64_t* cands, uint64_t ncand, uint64_t n, uint32_t* caps,
                             uint32_t heavy, uint32_t limit, uint32_t* hl) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= ncand) return;
     const uint64_t nxt = j + 1 < ncand ? cands[j + 1] : n;
     const uint64_t span = nxt - cands[j];
-    if (heavy && span > heavy && hl[1] <= limit) {
+    if (heavy && ln_dense(in, cands[j], n, span, heavy) && hl[1] <= limit) {
         caps[j] = 0;
         hl[2 + atomicAdd(hl, 1u)] = (uint32_t)j;
         return;
@@ -979,12 +986,13 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs 
     ln_resolve_one(A, j, make_uint2(rp->out_size, rp->flags), B.ntok[j], B.tok + B.tokoff[j], win);
 }
 
-// number of candidates spanning more than `heavy` bytes (*cnt zeroed by the caller)
-__global__ void k_heavy_count(const uint64_t* cands, uint64_t ncand, uint64_t n, uint32_t heavy, uint32_t* cnt) {
+// number of dense candidates (*cnt zeroed by the caller)
+__global__ void k_heavy_count(const uint8_t* in, const uint64_t* cands, uint64_t ncand, uint64_t n, uint32_t heavy,
+                              uint32_t* cnt) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= ncand) return;
     const uint64_t nxt = j + 1 < ncand ? cands[j + 1] : n;
-    const uint64_t b = __ballot(nxt - cands[j] > heavy);
+    const uint64_t b = __ballot(ln_dense(in, cands[j], n, nxt - cands[j], heavy));
     if (lane_id() == 0 && b) atomicAdd(cnt, (uint32_t)__popcll(b));  // lane 0 holds the wave's first j
 }
 
@@ -993,12 +1001,13 @@ hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* t
                                 uint32_t* hl, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     if (ev0) (void)hipEventRecord(ev0, st);
     const uint32_t g = (uint32_t)((A.ncand + 255) / 256);
+    const uint8_t* const in = reinterpret_cast<const uint8_t*>(A.in_words) + A.misalign;  // stream byte 0
     if (heavy) {
         const hipError_t e = hipMemsetAsync(hl, 0, 8, st);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_heavy_count, dim3(g), dim3(256), 0, st, A.cands, A.ncand, A.n, heavy, hl + 1);
+        hipLaunchKernelGGL(k_heavy_count, dim3(g), dim3(256), 0, st, in, A.cands, A.ncand, A.n, heavy, hl + 1);
     }
-    hipLaunchKernelGGL(k_lane_caps, dim3(g), dim3(256), 0, st, A.cands, A.ncand, A.n, caps, heavy, limit, hl);
+    hipLaunchKernelGGL(k_lane_caps, dim3(g), dim3(256), 0, st, in, A.cands, A.ncand, A.n, caps, heavy, limit, hl);
     hipError_t e = launch_scan_u32(caps, tokoff, A.ncand, tokoff + A.ncand, st);
     if (e != hipSuccess) return e;
     LaneArgs B{tok, tokoff, ntok, caps};
