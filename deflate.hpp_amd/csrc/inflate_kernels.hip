@@ -366,6 +366,12 @@ constexpr int PJ_ROUNDS = 64;
 #define PJ_MINBITS_ 192u  // (256: +7 % on text, 384: +14 %; measured with the 320-bit warm-up)
 #endif
 constexpr uint32_t PJ_MINBITS = PJ_MINBITS_;  // shortest range (bits) a lane decodes
+#ifndef PJ_LIST_NT
+#define PJ_LIST_NT 512  // lanes per workgroup of the heavy route (k_inflate_pj_list)
+#endif
+#ifndef PJ_MINBITS_1K
+#define PJ_MINBITS_1K 128u  // shortest range with 1024 lanes
+#endif
 #ifndef PJ_WARM
 #define PJ_WARM 320u  // warm-up bits before a range's first pass (128: +25 % on text, 512: +1 %)
 #endif
@@ -622,7 +628,7 @@ __device__ __forceinline__ void pj_segment(const InflateArgs& A, PjSmem<SEG, NT>
         // ranges of at least PJ_MINBITS (a few dozen tokens) so that a path started at an
         // arbitrary bit re-synchronises inside its own range; range r belongs to thread
         // (r % NW) * 64 + r / NW so that a short segment's ranges spread over every wave
-        const uint32_t nl = max(1u, min((uint32_t)NT, hlen / PJ_MINBITS));
+        const uint32_t nl = max(1u, min((uint32_t)NT, hlen / (NT >= 1024 ? PJ_MINBITS_1K : PJ_MINBITS)));
         const uint32_t r = (uint32_t)((t & 63) * NW + wave);
         const uint32_t sp = r < nl ? (uint32_t)(((uint64_t)hlen * r) / nl) : hlen;
         const uint32_t sp1 = r + 1 < nl ? (uint32_t)(((uint64_t)hlen * (r + 1)) / nl) : hlen;
@@ -978,7 +984,7 @@ hipError_t launch_inflate_pj_list(const InflateArgs& A, uint32_t seg, const uint
     if (seg == 16384)
         hipLaunchKernelGGL((k_inflate_pj_list<16384, 256>), dim3(grid), dim3(256), 0, st, A, hl);
     else
-        hipLaunchKernelGGL((k_inflate_pj_list<32768, 512>), dim3(grid), dim3(512), 0, st, A, hl);
+        hipLaunchKernelGGL((k_inflate_pj_list<32768, PJ_LIST_NT>), dim3(grid), dim3(PJ_LIST_NT), 0, st, A, hl);
     if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();
 }
