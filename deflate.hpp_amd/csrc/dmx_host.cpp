@@ -423,10 +423,10 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     // lanes, ~0.17 ms per dense segment on one CU): always up to 2048 candidates, beyond that
     // when the device-side count finds at most 32 per CU (32 rounds of workgroups, ~5.5 ms;
     // more dense segments than that keep the lanes' throughput: 1 GiB of text).
-    static const uint32_t heavy_bytes = [] {
-        const char* e = std::getenv("DMX_HEAVY_BYTES");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 2048u;
-    }();
+    // A stream of at most one candidate per CU takes one round of workgroups, which beats the
+    // lanes' ~0.3 ms floor (a wave's header, table and token phases) from 256 bytes up.
+    static const char* const heavy_env = std::getenv("DMX_HEAVY_BYTES");
+    static const uint32_t heavy_bytes = heavy_env ? (uint32_t)std::strtoul(heavy_env, nullptr, 10) : 2048u;
     const bool few_bits = n / ncand < 4096;
     uint32_t plan[8][2];
     int np = 0;
@@ -440,7 +440,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
             if (heavy_bytes && ncand < 0xFFFFFFF0ull && c->lheavy.ensure((ncand + 2) * 4)) {
                 if (c->ncu <= 0 && hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
                     c->ncu = 256;
-                heavy = heavy_bytes;
+                heavy = (!heavy_env && ncand <= (uint64_t)c->ncu) ? 256u : heavy_bytes;
                 heavy_limit = ncand <= 2048 ? 0xFFFFFFFFu : 32u * (uint32_t)std::max(c->ncu, 1);
                 plan[np][0] = 6, plan[np][1] = c->seg, np++;  // the heavy candidates
             }
