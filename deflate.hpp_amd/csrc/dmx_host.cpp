@@ -232,7 +232,7 @@ int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, 
 // runs out of token space, a copy from before the stream start): results and error codes are
 // then the serial decoder's, i.e. the reference's.
 int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_out, size_t cap,
-                      size_t* total_out, uint8_t** dev_out, hipStream_t st, bool* handled) {
+                      size_t* total_out, uint8_t** dev_out, hipStream_t st, bool* handled, uint32_t iflags) {
     *handled = false;
     Scal* ds = c->scal.as<Scal>();
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
@@ -292,7 +292,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     HIPCHK(hipMemcpyAsync(c->fbstop.p, stops.data(), K * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(c->fbt.p, tokoff.data(), (K + 1) * 8, hipMemcpyHostToDevice, st));
     HIPCHK(launch_fb_decode(words, misalign, n, c->fbs.as<uint64_t>(), c->fbstop.as<uint64_t>(), K,
-                            c->fbt.as<uint64_t>(), c->fbk.as<uint32_t>(), c->fbu.as<FbUnit>(), c->flags, st));
+                            c->fbt.as<uint64_t>(), c->fbk.as<uint32_t>(), c->fbu.as<FbUnit>(), c->flags | iflags, st));
     std::vector<FbUnit> units(K);
     HIPCHK(hipMemcpyAsync(units.data(), c->fbu.p, K * sizeof(FbUnit), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -312,6 +312,12 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         if (it == starts.end() || *it != u.end) return DMX_OK;  // chain leaves the unit starts
         k = (uint64_t)(it - starts.begin());
     }
+    // the path's own scratch first: when it does not fit, the stream still decodes on the
+    // serial decoder, which needs only the output
+    const uint64_t nch = chain.size();
+    if (!c->fbch.ensure(nch * 4) || !c->fbco.ensure(nch * 8) || !c->fbcs.ensure(nch * 8) ||
+        !c->fbimg.ensure(total * 2 + 16))
+        return DMX_OK;
     *handled = true;
     *total_out = total;
     uint8_t* out = fixed_out;
@@ -321,10 +327,6 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     } else if (total > cap) {
         return DMX_ERR_CAPACITY;
     }
-    const uint64_t nch = chain.size();
-    if (!c->fbch.ensure(nch * 4) || !c->fbco.ensure(nch * 8) || !c->fbcs.ensure(nch * 8) ||
-        !c->fbimg.ensure(total * 2 + 16))
-        return DMX_ERR_NOMEM;
     HIPCHK(hipMemcpyAsync(c->fbch.p, chain.data(), nch * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(c->fbco.p, coffs.data(), nch * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(c->fbcs.p, csizes.data(), nch * 8, hipMemcpyHostToDevice, st));
@@ -348,8 +350,10 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
 
 // Shared inflate driver.  fixed_out != nullptr: decode into the caller's device buffer of
 // `cap` bytes.  Otherwise decode into c->out, grown as needed (*dev_out receives it).
+// iflags: DMX_IFLAG_PIECE for one piece of a larger stream (dmx_inflate_piece_device).
 int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_out,
-                          size_t cap, size_t* total_out, uint8_t** dev_out, hipStream_t st) {
+                          size_t cap, size_t* total_out, uint8_t** dev_out, hipStream_t st,
+                          uint32_t iflags = 0) {
     begin_timing(c, st);
     *total_out = 0;
     if (n == 0) return DMX_ERR_OVERREAD;  // the reference throws (or faults) on empty input
@@ -403,7 +407,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     A.recs = c->recs.as<SegRecord>();
     A.status = c->status.as<unsigned long long>();
     A.ticket = &ds->ticket;
-    A.flags = c->flags;
+    A.flags = c->flags | iflags;
     A.dbg = phase_buf(c, ncand);
     InflateResult r{};
     // Plan: the lane decoder (one lane per segment decodes tokens, one wave per segment
@@ -522,7 +526,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
 
     if (path_env == -1 || path_env == 5) {
         bool handled = false;
-        const int rc = inflate_fb_locked(c, d_in, n, fixed_out, cap, total_out, dev_out, st, &handled);
+        const int rc = inflate_fb_locked(c, d_in, n, fixed_out, cap, total_out, dev_out, st, &handled, iflags);
         if (handled) {
             end_timing(c, st);
             c->stats.path = 5;
@@ -722,6 +726,17 @@ int dmx_inflate_device(dmx_ctx* c, const void* d_in, size_t n, void* d_out, size
                                  nullptr, st);
 }
 
+int dmx_inflate_piece_device(dmx_ctx* c, const void* d_in, size_t n, void* d_out, size_t cap,
+                             size_t* out_len, void* stream) {
+    if (!c || (!d_in && n) || !d_out || !out_len) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return inflate_device_locked(c, (const uint8_t*)d_in, n, (uint8_t*)d_out, cap, out_len, nullptr, st,
+                                 DMX_IFLAG_PIECE);
+}
+
 int dmx_deflate(dmx_ctx* c, const uint8_t* in, size_t n, int level, uint8_t* out, size_t cap,
                 size_t* out_len) {
     if (!c) c = dmx_default_ctx();
@@ -830,6 +845,30 @@ int dmx_segment_starts_device(dmx_ctx* c, const void* d_in, size_t n, uint64_t* 
     if (k) HIPCHK(hipMemcpyAsync(starts, c->cands.as<uint64_t>() + 1, k * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     *count = nm;
+    return DMX_OK;
+}
+
+int dmx_segment_check_device(dmx_ctx* c, const void* d_in, size_t n, const uint64_t* starts, size_t k,
+                             uint64_t* ends, void* stream) {
+    if (!c || (!d_in && n) || (k && (!starts || !ends))) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if (k == 0) return DMX_OK;
+    if (!c->cands.ensure(2 * k * 8)) return DMX_ERR_NOMEM;
+    uint64_t* d_starts = c->cands.as<uint64_t>();
+    uint64_t* d_ends = d_starts + k;
+    HIPCHK(hipMemcpyAsync(d_starts, starts, k * 8, hipMemcpyHostToDevice, st));
+    const uint8_t* in = static_cast<const uint8_t*>(d_in);
+    InflateArgs A{};
+    A.misalign = (uintptr_t)in & 3;
+    A.in_words = reinterpret_cast<const uint32_t*>(in - A.misalign);
+    A.n = n;
+    A.flags = c->flags | DMX_IFLAG_PIECE;
+    HIPCHK(launch_segment_check(A, d_starts, k, d_ends, st));
+    HIPCHK(hipMemcpyAsync(ends, d_ends, k * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
     return DMX_OK;
 }
 

@@ -43,6 +43,10 @@ enum : uint32_t {
                           // unsettled split): the wave-per-segment decoder redoes the stream
 };
 
+// InflateArgs::flags bit (internal): the stream is a piece of a larger stream (multi-GPU
+// scatter): a back-reference before its first byte is an error, not the stream-start no-op.
+constexpr uint32_t DMX_IFLAG_PIECE = 1u << 31;
+
 struct InflateArgs {
     const uint32_t* in_words;  // 4-byte aligned base at or below the stream start
     uint64_t misalign;         // stream start = in_words bytes + misalign
@@ -54,7 +58,7 @@ struct InflateArgs {
     SegRecord* recs;
     unsigned long long* status;  // ncand look-back words (zeroed)
     unsigned int* ticket;        // zeroed
-    uint32_t flags;              // DMX_CFG_RFC_STRICT
+    uint32_t flags;              // DMX_CFG_RFC_STRICT, DMX_IFLAG_PIECE
     uint32_t mode;               // 0 = speculative uniform segment sizes, 1 = decoupled look-back,
                                  // 2 = k_inflate_pj (segment j at j * slot),
                                  // 3 = k_inflate_segments redoing only SEGF_EXOTIC candidates
@@ -149,6 +153,8 @@ hipError_t launch_adler32(const uint8_t* d, uint64_t n, uint32_t init, void* scr
 hipError_t launch_crc32_raw(const uint8_t* d, uint64_t n, void* scratch, uint32_t* d_out, hipStream_t st);
 uint32_t crc32_finish(uint32_t raw, uint64_t n, uint32_t init);
 
+hipError_t launch_segment_check(const InflateArgs& A, const uint64_t* starts, uint64_t k, uint64_t* ends,
+                                hipStream_t st);
 hipError_t launch_inflate_serial(const InflateArgs& A, int count_only, InflateResult* res,
                                  hipStream_t st);
 

@@ -276,6 +276,10 @@ struct TokSink {
     __device__ bool stored(const BR&, uint64_t b0, uint32_t len) {
         if (!flush_lits()) return false;
         if (((n + k) & 1) && !push(0)) return false;
+        if (b0 - unit_byte0 > 0xFFFFFFFFull) {  // the offset word holds 32 bits: a unit spanning
+            err |= SEGF_OVERFLOW;                // more than 4 GiB goes to the serial decoder
+            return false;
+        }
         if (!push((127u << 24) | len)) return false;
         pos += len;
         return push((uint32_t)(b0 - unit_byte0));
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(64) void k_fb_decode(const uint32_t* in_words, uint
     sk.n = sk.k = sk.reg = sk.pend = sk.pendn = 0;
     sk.pos = 0;
     sk.unit_byte0 = (base + start) >> 3;
-    sk.stream_start = u == 0;
+    sk.stream_start = u == 0 && !(flags & DMX_IFLAG_PIECE);
     sk.err = 0;
     const bool rfc = (flags & DMX_CFG_RFC_STRICT) != 0;
     uint32_t err = 0;
@@ -569,13 +573,14 @@ __global__ __launch_bounds__(64) void k_fb_replay(FbReplayArgs A) {
     while (t0 < n) {
         const uint32_t ti = t0 + lane;
         const uint32_t w = ti < n ? tk[ti] : 0u;
-        const bool ism = (w >> 31) != 0;
-        const uint32_t cnt = (w >> 24) & 127;
-        const bool isst = !ism && cnt == 127 && (ti & 1) == 0;
-        // the word after a stored header is its offset: lane ti - 1 is that header
+        // the word after a stored header is its offset (any 32-bit value, bit 31 included):
+        // lane ti - 1 is that header
         const uint32_t wprev = (uint32_t)__shfl((int)w, (int)lane - 1, 64);
         const uint32_t wp = lane == 0 ? (t0 > 0 ? tk[t0 - 1] : 0u) : wprev;
-        const bool isoff = (ti & 1) && !(wp >> 31) && ((wp >> 24) & 127) == 127;
+        const bool isoff = (ti & 1) && !(wp >> 31) && ((wp >> 24) & 127) == 127 && ((ti - 1) & 1) == 0;
+        const bool ism = (w >> 31) != 0 && !isoff;
+        const uint32_t cnt = (w >> 24) & 127;
+        const bool isst = !ism && !isoff && cnt == 127 && (ti & 1) == 0;
         const bool islit = !ism && !isst && !isoff && cnt >= 1 && cnt <= 3;
         uint32_t L = ism ? (w >> 15) & 0xFFFFu : isst ? (w & 0xFFFFFFu) : islit ? cnt : 0u;
         const uint32_t d = (w & 0x7FFFu) + 1;

@@ -68,6 +68,7 @@ struct RingSink {
     uint64_t cap;
     bool count_only;
     uint32_t err;
+    bool piece;  // a reference before the first byte is an error (DMX_IFLAG_PIECE)
     __device__ bool literal(uint32_t b) {
         if (!count_only) {
             if (lane_id() == 0) {
@@ -79,7 +80,12 @@ struct RingSink {
         return true;
     }
     __device__ bool copy(uint32_t L, uint32_t dist) {
-        if (L == 0 || dist == 0 || dist > pos) return true;
+        if (L == 0 || dist == 0) return true;
+        if (dist > pos) {
+            if (!piece) return true;  // reference: nothing to copy (inflate.hpp:268-270)
+            err |= SEGF_XREF;
+            return false;
+        }
         if (!count_only) {
             const uint32_t lane = lane_id();
             const uint64_t src = pos - dist;
@@ -236,7 +242,7 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_segments(InflateArgs A) {
         stg[i] = v;
     }
     __syncthreads();
-    SegSink sk{win, 0, j == 0, 0};
+    SegSink sk{win, 0, j == 0 && !(A.flags & DMX_IFLAG_PIECE), 0};
     uint64_t end_byte = 0;
     bool fin = false;
     const bool rfc = (A.flags & DMX_CFG_RFC_STRICT) != 0;
@@ -842,7 +848,7 @@ __device__ __forceinline__ void pj_segment(const InflateArgs& A, PjSmem<SEG, NT>
                 }
                 bool mt = live && k == TK_MATCH && a && d;
                 if (mt && d > o) {  // before the segment: cross-segment or stream-start reference
-                    bad = j == 0 ? SEGF_EXOTIC : SEGF_XREF;
+                    bad = (j == 0 && !(A.flags & DMX_IFLAG_PIECE)) ? SEGF_EXOTIC : SEGF_XREF;
                     act = false;
                     mt = false;
                 }
@@ -1075,7 +1081,7 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_serial(InflateArgs A, int cou
     BitIn br;
     br.init(A.in_words, A.misalign, A.n);
     br.seek(A.misalign * 8);
-    RingSink sk{ring, 0, A.out, A.cap, count_only != 0, 0};
+    RingSink sk{ring, 0, A.out, A.cap, count_only != 0, 0, (A.flags & DMX_IFLAG_PIECE) != 0};
     uint64_t end_byte = 0;
     bool fin = false;
     const uint32_t err =
@@ -1085,6 +1091,41 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_serial(InflateArgs A, int cou
         res->status = err == 0 ? 0 : (err & SEGF_OVERREAD) ? DMX_ERR_OVERREAD : DMX_ERR_DATA;
         res->fin_index = 0;
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// dmx_segment_check_device: for each given start, the one segment that begins there, decoded
+// by the exact wave decoder in piece mode (no reference before the start, <= 32 KiB of
+// output); ends[i] = the stream byte after its closing empty stored block (or after its BFINAL
+// block), ~0 when it does not decode.  Validates multi-GPU cut points (shard.py).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(IF_NT) void k_segment_check(InflateArgs A, const uint64_t* starts, uint64_t k,
+                                                         uint64_t* ends) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[SEG_CAP + 16];
+    __shared__ Tables T;
+    const uint64_t i = blockIdx.x;
+    if (i >= k) return;
+    if (threadIdx.x == 0) T.fixed_loaded = 0;
+    __syncthreads();
+    const uint64_t start = starts[i];
+    uint64_t end = ~0ull;
+    if (start < A.n) {
+        SegSink sk{win, 0, false, 0};
+        BitIn br;
+        br.init(A.in_words, A.misalign, A.n);
+        br.seek((A.misalign + start) * 8);
+        uint64_t end_byte = 0;
+        bool fin = false;
+        const uint32_t err = inflate_blocks(br, T, sk, (A.flags & DMX_CFG_RFC_STRICT) != 0, true, &end_byte, &fin);
+        if (!err) end = end_byte - A.misalign;
+    }
+    if (threadIdx.x == 0) ends[i] = end;
+}
+
+hipError_t launch_segment_check(const InflateArgs& A, const uint64_t* starts, uint64_t k, uint64_t* ends,
+                                hipStream_t st) {
+    if (k) hipLaunchKernelGGL(k_segment_check, dim3((uint32_t)k), dim3(IF_NT), 0, st, A, starts, k, ends);
+    return hipGetLastError();
 }
 
 hipError_t launch_inflate_segments(const InflateArgs& A, hipStream_t st, hipEvent_t ev0,

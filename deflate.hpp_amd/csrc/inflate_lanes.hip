@@ -517,7 +517,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
         bool v0 = false, v1 = false;
         // one symbol; returns false once the lane's block has ended (EOB or a flag)
         const uint32_t E8 = 8 * br.E;
-        const uint32_t xref_fl = j != 0 ? (uint32_t)SEGF_XREF : 0u;
+        const uint32_t xref_fl = (j != 0 || (A.flags & DMX_IFLAG_PIECE)) ? (uint32_t)SEGF_XREF : 0u;
         // The 64-bit window at bp lives in registers; each step reads the next 64 bits (from
         // two word pairs addressed by the old bp, so the LDS latency overlaps the table lookups)
         // and funnels them in after consuming the symbol.

@@ -34,7 +34,8 @@ EXPORTS = [
     "dmx_deflate_device", "dmx_inflate_device", "dmx_set_timing", "dmx_last_stats",
     "dmx_corpus_generate", "dmx_adler32_device", "dmx_crc32_device", "dmx_adler32", "dmx_crc32",
     "dmx_framed_bound", "dmx_deflate_zlib", "dmx_deflate_gzip", "dmx_inflate_zlib", "dmx_inflate_gzip",
-    "dmx_deflate_file", "dmx_inflate_file", "dmx_segment_starts_device",
+    "dmx_deflate_file", "dmx_inflate_file", "dmx_segment_starts_device", "dmx_inflate_piece_device",
+    "dmx_segment_check_device",
 ]
 
 
@@ -99,6 +100,9 @@ def lib():
                                    ctypes.POINTER(sz)]
     L.dmx_inflate_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(sz)]
     L.dmx_segment_starts_device.argtypes = [vp, vp, sz, ctypes.POINTER(ctypes.c_uint64), sz, ctypes.POINTER(sz), vp]
+    L.dmx_inflate_piece_device.argtypes = [vp, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
+    L.dmx_segment_check_device.argtypes = [vp, vp, sz, ctypes.POINTER(ctypes.c_uint64), sz,
+                                           ctypes.POINTER(ctypes.c_uint64), vp]
     L.dmx_framed_bound.argtypes = [sz]
     L.dmx_framed_bound.restype = sz
     for f in ("dmx_deflate_zlib", "dmx_deflate_gzip"):
@@ -287,6 +291,26 @@ class Context:
                                       ctypes.byref(out_len), ctypes.c_void_p(stream) if stream else None)
         _check(rc, "inflate_device")
         return out_len.value
+
+    def inflate_piece_device(self, d_in, n, d_out, cap, stream=None):
+        """inflate_device for one piece of a larger stream: a reference before the piece start
+        raises (DMX_ERR_DATA) instead of copying nothing (multi-GPU scatter, shard.py)."""
+        out_len = ctypes.c_size_t()
+        rc = lib().dmx_inflate_piece_device(self.h, ctypes.c_void_p(d_in), n, ctypes.c_void_p(d_out), cap,
+                                            ctypes.byref(out_len), ctypes.c_void_p(stream) if stream else None)
+        _check(rc, "inflate_piece_device")
+        return out_len.value
+
+    def segment_check_device(self, d_in, n, starts, stream=None):
+        """End byte of the segment at each start (None where it does not decode in piece mode)."""
+        k = len(starts)
+        if not k:
+            return []
+        a = (ctypes.c_uint64 * k)(*starts)
+        e = (ctypes.c_uint64 * k)()
+        _check(lib().dmx_segment_check_device(self.h, ctypes.c_void_p(d_in), n, a, k, e,
+                                              ctypes.c_void_p(stream) if stream else None), "segment_check")
+        return [None if x == 0xFFFFFFFFFFFFFFFF else x for x in e]
 
     def segment_starts_device(self, d_in, n, stream=None):
         """Candidate segment starts (bytes after each 00 00 FF FF) of a device-resident stream."""

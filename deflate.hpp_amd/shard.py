@@ -6,8 +6,14 @@ whose final block carries BFINAL.  The stream is the byte concatenation of the s
 order; the one exchange step is a gather of the compressed shards to rank 0 over
 torch.distributed (RCCL over xGMI on MI355X nodes, gloo for the CPU tests):
 
-  1. all_gather of the per-rank compressed byte counts,
+  1. all_gather of the per-rank compressed byte counts (and rank 0's output capacity, so that
+     every rank sees a too-small buffer and raises together instead of one rank leaving the
+     collective),
   2. rank 0 receives every shard at its prefix offset (batched P2P), others send.
+
+deflate_gather() pipelines this: the shard is compressed in sub-shards, and each sub-shard's
+bytes go to rank 0 (into a staging slot) while the next one compresses; rank 0 packs the slots
+into the stream at the end.
 """
 import torch
 import torch.distributed as dist
@@ -21,82 +27,202 @@ def shard_range(total, rank, world, align):
     return b, min(total, b + per)
 
 
-def gather_sizes(clen, device):
+def _all_gather_ints(vals, device):
     world = dist.get_world_size()
-    sz = torch.tensor([clen], dtype=torch.int64, device=device)
-    sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
-    dist.all_gather(sizes, sz)
-    return [int(s.item()) for s in sizes]
+    t = torch.tensor(vals, dtype=torch.int64, device=device)
+    parts = [torch.zeros(len(vals), dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [[int(x) for x in p.tolist()] for p in parts]
+
+
+def gather_sizes(clen, device):
+    return [s[0] for s in _all_gather_ints([clen], device)]
+
+
+def _p2p(ops):
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
 
 
 def gather_stream(local, clen, out=None):
     """Gather the compressed shards (local[:clen] on every rank) into out on rank 0.
 
     Returns the total stream length on every rank; on rank 0 out[:total] holds the stream.
+    Raises ValueError on EVERY rank when rank 0's out is missing or too small.
     """
     rank, world = dist.get_rank(), dist.get_world_size()
-    sizes = gather_sizes(clen, local.device)
+    cap = out.numel() if (rank == 0 and out is not None) else -1
+    st = _all_gather_ints([clen, cap], local.device)
+    sizes = [s[0] for s in st]
     total = sum(sizes)
+    if total and st[0][1] < total:
+        raise ValueError("rank 0 needs an output buffer of at least the total stream size")
     if world == 1:
-        if out is not None:
+        if clen:
             out[:clen].copy_(local[:clen])
         return total
     if rank == 0:
-        if out is None or out.numel() < total:
-            raise ValueError("rank 0 needs an output buffer of at least the total stream size")
         offs = [sum(sizes[:r]) for r in range(world)]
         out[: sizes[0]].copy_(local[: sizes[0]])
         ops = [dist.P2POp(dist.irecv, out[offs[r]: offs[r] + sizes[r]], r) for r in range(1, world) if sizes[r]]
     else:
         ops = [dist.P2POp(dist.isend, local[:clen], 0)] if clen else []
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+    _p2p(ops)
     return total
+
+
+def deflate_gather(ctx, d_in, n, level, out=None, sub=4, align=32768):
+    """Compress this rank's device-resident shard d_in[:n] and gather every rank's stream on
+    rank 0, the transfers pipelined behind the compression.
+
+    The shard is cut into `sub` sub-shards (multiples of `align`), each compressed NOT_FINAL
+    (the last rank's last one final) into a staging slot; after sub-shard k, every rank sends
+    its length and then its bytes to rank 0 (asynchronous P2P) and goes on compressing k + 1.
+    Rank 0 posts the payload receives as soon as the lengths of step k are in, into per-rank
+    staging slots, and packs the pieces into out[:total] at the end (rank order, then k).
+    ctx: dmx.Context on this rank's GPU.  Returns (total stream bytes, this rank's bytes) on
+    every rank; raises ValueError on every rank when rank 0's out is too small.
+    """
+    import dmx
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = d_in.device
+    last = rank == world - 1
+    cuts = [min(n, -(-(n * k // sub) // align) * align) for k in range(sub + 1)]
+    cuts[-1] = n
+    slot = dmx.deflate_bound(max([1] + [b - a for a, b in zip(cuts, cuts[1:])])) + 64
+    stage = torch.empty(sub * slot, dtype=torch.uint8, device=dev)
+    lens = [0] * sub
+    rlens = [[0] * sub for _ in range(world)]
+    rstage = [None] * world
+    if rank == 0:
+        for r in range(1, world):
+            rstage[r] = torch.empty(sub * slot, dtype=torch.uint8, device=dev)
+    pend, keep = [], []
+    for k in range(sub):
+        a, b = cuts[k], cuts[k + 1]
+        L = 0
+        if b > a:
+            L = ctx.deflate_device(d_in.data_ptr() + a, b - a, level, stage.data_ptr() + k * slot, slot,
+                                   not_final=not (last and k == sub - 1))
+        lens[k] = L
+        if world == 1:
+            continue
+        if rank == 0:
+            got = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+            _p2p([dist.P2POp(dist.irecv, got[r], r) for r in range(1, world)])
+            ops = []
+            for r in range(1, world):
+                Lr = int(got[r].item())
+                rlens[r][k] = Lr
+                if Lr:
+                    ops.append(dist.P2POp(dist.irecv, rstage[r][k * slot: k * slot + Lr], r))
+            if ops:
+                pend += dist.batch_isend_irecv(ops)
+        else:
+            lt = torch.tensor([L], dtype=torch.int64, device=dev)
+            keep.append(lt)
+            ops = [dist.P2POp(dist.isend, lt, 0)]
+            if L:
+                ops.append(dist.P2POp(dist.isend, stage[k * slot: k * slot + L], 0))
+            pend += dist.batch_isend_irecv(ops)
+    for q in pend:
+        q.wait()
+    mine = sum(lens)
+    cap = out.numel() if (rank == 0 and out is not None) else -1
+    st = _all_gather_ints([mine, cap], dev) if world > 1 else [[mine, cap]]
+    total = sum(x[0] for x in st)
+    if total and st[0][1] < total:
+        raise ValueError("rank 0 needs an output buffer of at least the total stream size")
+    if rank == 0:
+        rlens[0] = lens
+        rstage[0] = stage
+        o = 0
+        for r in range(world):
+            for k in range(sub):
+                L = rlens[r][k]
+                if L:
+                    out[o: o + L].copy_(rstage[r][k * slot: k * slot + L])
+                    o += L
+    return total, mine
 
 
 # ---------------------------------------------------------------------------------------------
 # inflate across ranks (SURVEY 8(e), "Inflate (our streams)"): rank 0 indexes the segment
-# markers, cuts the stream into one contiguous piece per rank at segment starts, sends each rank
-# its piece, every rank decodes its piece locally, and the decoded pieces are gathered back to
-# rank 0 at their prefix offsets.
+# markers, picks one cut per rank among them -- only starts whose segment decodes to a closing
+# marker (check) -- sends each rank its piece, every rank decodes its piece locally (pieces
+# after the first in piece mode: a reference before the piece is an error, never silently
+# dropped), and the decoded pieces are gathered back to rank 0 at their prefix offsets.
 # ---------------------------------------------------------------------------------------------
 FINAL_EMPTY = (0x03, 0x00)  # an empty final fixed-Huffman block: closes a NOT_FINAL piece
+CHECK_NEAREST = 8           # candidates tried per cut, nearest to its target first
 
 
-def split_points(starts, total, world):
+def split_points(starts, total, world, valid=None):
     """Piece boundaries [0, c_1, ..., c_{world-1}, total]: c_r is the candidate segment start
-    nearest r * total / world (boundaries strictly increase; a rank may get an empty piece)."""
+    nearest r * total / world among those valid(start) accepts (boundaries strictly increase;
+    a rank may get an empty piece)."""
     import bisect
     cuts = [0]
     for r in range(1, world):
         target = r * total // world
         i = bisect.bisect_left(starts, target)
+        order = sorted((j for j in range(max(0, i - CHECK_NEAREST), min(len(starts), i + CHECK_NEAREST))),
+                       key=lambda j: (abs(starts[j] - target), starts[j]))
         best = None
-        for j in (i - 1, i):
-            if 0 <= j < len(starts) and starts[j] > cuts[-1] and starts[j] < total:
-                if best is None or abs(starts[j] - target) < abs(best - target):
-                    best = starts[j]
+        for j in order:
+            s = starts[j]
+            if cuts[-1] < s < total and (valid is None or valid(s)):
+                best = s
+                break
         cuts.append(best if best is not None else cuts[-1])
     cuts.append(total)
     return cuts
 
 
-def scatter_inflate(stream, clen, decode, starts=None, out=None):
+def pick_cuts(starts, total, world, check=None):
+    """split_points with the candidates near each target proven first by check(list of starts)
+    -> list of end bytes (None: the segment does not decode) -- one batched call."""
+    import bisect
+    starts = sorted(starts)
+    if check is None:
+        return split_points(starts, total, world)
+    near = set()
+    for r in range(1, world):
+        i = bisect.bisect_left(starts, r * total // world)
+        near.update(starts[max(0, i - CHECK_NEAREST): i + CHECK_NEAREST])
+    near = sorted(s for s in near if 0 < s < total)
+    ends = check(near) if near else []
+    # the segment must end where a segment starts (its closing marker), or at the stream end
+    # (its BFINAL block): a garbage start that stops early on some lenient block never does
+    known = set(starts)
+    ok = {s for s, e in zip(near, ends) if e is not None and s < e and (e in known or e == total)}
+    return split_points(starts, total, world, valid=lambda s: s in ok)
+
+
+def scatter_inflate(stream, clen, decode, starts=None, out=None, check=None, gather=True):
     """Inflate one stream held by rank 0 (stream[:clen]) on all ranks.
 
-    decode(piece) -> 1-D uint8 tensor of decoded bytes, raising on a decode error (libdmx's
-    inflate_device on a GPU; tests pass a checker).  starts: rank 0's candidate segment starts
-    (Context.segment_starts_device).  Returns (total decoded bytes, ok); on rank 0, out[:total]
-    receives the decoded stream.  A false candidate (00 00 FF FF inside stored data) makes the
-    piece before it fail; then every rank agrees on ok == False and rank 0 decodes the stream
-    whole, so the result never depends on the split.
+    decode(piece, first) -> 1-D uint8 tensor of decoded bytes, raising on a decode error; first
+    is False for every piece but rank 0's, which must then be decoded in piece mode (libdmx's
+    inflate_piece_device; tests pass a checker).  starts: rank 0's candidate segment starts
+    (Context.segment_starts_device).  check: rank 0's cut-point proof (Context.
+    segment_check_device), None to cut at raw candidates.  Returns (total decoded bytes, ok);
+    on rank 0, out[:total] receives the decoded stream.  ok == False: a piece failed (a false
+    candidate), every rank saw it, and rank 0 decoded the stream whole -- the result never
+    depends on the split.  A stream that does not decode at all, or an out that is too small,
+    raises on every rank.  gather=False leaves every rank's decoded piece where it was decoded
+    (decode's own buffer; bench.py at N > 1): no byte goes back to rank 0 and out is unused
+    except for the whole-stream fallback.
     """
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = stream.device
     cut = torch.zeros(world + 1, dtype=torch.int64, device=dev)
     if rank == 0:
-        cut.copy_(torch.tensor(split_points(sorted(starts or []), clen, world), dtype=torch.int64))
+        try:
+            cut.copy_(torch.tensor(pick_cuts(starts or [], clen, world, check), dtype=torch.int64))
+        except Exception:  # no split (rank 0 alone decodes) rather than a rank left in the collective
+            cut.copy_(torch.tensor([0] + [clen] * world, dtype=torch.int64))
     dist.broadcast(cut, 0)
     cuts = [int(x) for x in cut.tolist()]
     lo, hi = cuts[rank], cuts[rank + 1]
@@ -108,9 +234,7 @@ def scatter_inflate(stream, clen, decode, starts=None, out=None):
                if cuts[r + 1] > cuts[r]]
     else:
         ops = [dist.P2POp(dist.irecv, piece[: hi - lo], 0)] if hi > lo else []
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+    _p2p(ops)
     plen = hi - lo
     if closes and plen:
         piece[plen: plen + 2].copy_(torch.tensor(FINAL_EMPTY, dtype=torch.uint8))
@@ -118,35 +242,45 @@ def scatter_inflate(stream, clen, decode, starts=None, out=None):
     dec, ok = None, 1
     if plen:
         try:
-            dec = decode(piece[:plen])
+            dec = decode(piece[:plen], rank == 0)
         except Exception:
             ok = 0
-    state = torch.tensor([ok, 0 if dec is None else dec.numel()], dtype=torch.int64, device=dev)
-    states = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(states, state)
-    oks = [int(s[0].item()) for s in states]
-    sizes = [int(s[1].item()) for s in states]
+    cap = out.numel() if (rank == 0 and out is not None) else -1
+    st = _all_gather_ints([ok, 0 if dec is None else dec.numel(), cap], dev)
+    oks = [s[0] for s in st]
+    sizes = [s[1] for s in st]
     if not all(oks):
-        total = 0
+        total = -1
         if rank == 0:
-            full = decode(stream[:clen])
-            total = full.numel()
-            if out is not None:
-                out[:total].copy_(full)
+            try:
+                full = decode(stream[:clen], True)
+                total = full.numel()
+                if total <= cap:
+                    if total:
+                        out[:total].copy_(full)
+                else:
+                    total = -2
+            except Exception:
+                total = -1
         t = torch.tensor([total], dtype=torch.int64, device=dev)
         dist.broadcast(t, 0)
-        return int(t.item()), False
-    total = sum(sizes)
-    if rank == 0:
-        if out is None or out.numel() < total:
+        total = int(t.item())
+        if total == -2:
             raise ValueError("rank 0 needs an output buffer of at least the decoded size")
+        if total < 0:
+            raise RuntimeError("scatter_inflate: the stream does not decode")
+        return total, False
+    total = sum(sizes)
+    if not gather:
+        return total, True
+    if total and st[0][2] < total:
+        raise ValueError("rank 0 needs an output buffer of at least the decoded size")
+    if rank == 0:
         offs = [sum(sizes[:r]) for r in range(world)]
         if sizes[0]:
             out[: sizes[0]].copy_(dec)
         ops = [dist.P2POp(dist.irecv, out[offs[r]: offs[r] + sizes[r]], r) for r in range(1, world) if sizes[r]]
     else:
         ops = [dist.P2POp(dist.isend, dec, 0)] if sizes[rank] else []
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+    _p2p(ops)
     return total, True

@@ -121,6 +121,24 @@ int dmx_inflate_device(dmx_ctx* ctx, const void* d_in, size_t n, void* d_out, si
 int dmx_segment_starts_device(dmx_ctx* ctx, const void* d_in, size_t n, uint64_t* starts, size_t cap,
                               size_t* count, void* stream);
 
+/* One piece of a larger stream cut at a segment start (multi-GPU inflate, shard.py): exactly
+ * dmx_inflate_device, except that a back-reference reaching before the piece's first byte is
+ * DMX_ERR_DATA.  At a stream's true start the reference copies nothing for such a distance
+ * (inflate.hpp:268-270) and dmx_inflate_device does the same; inside a stream whose window
+ * carries across the cut (zlib's sync flush) that rule would drop bytes without an error. */
+int dmx_inflate_piece_device(dmx_ctx* ctx, const void* d_in, size_t n, void* d_out, size_t cap,
+                             size_t* out_len, void* stream);
+
+/* Cut-point check for multi-GPU inflate: for each of k candidate starts (host array, stream
+ * byte offsets, e.g. from dmx_segment_starts_device) the one segment beginning there is decoded
+ * by the exact decoder in piece mode; ends[i] (host array) = the byte just past its closing
+ * empty stored block "00 00 FF FF" (or past its BFINAL block), or UINT64_MAX when it does not
+ * decode (a "00 00 FF FF" inside stored data, more than 32 KiB of output, a reference before
+ * the start).  A start whose segment ends on a marker is a block boundary the decoder reaches
+ * with an empty window; shard.py cuts only there. */
+int dmx_segment_check_device(dmx_ctx* ctx, const void* d_in, size_t n, const uint64_t* starts, size_t k,
+                             uint64_t* ends, void* stream);
+
 /* ---- checksums and containers (not in the reference) -------------------
  * The reference's decompressZlib (inflate.hpp:326-361) skips the 2-byte header and ignores the
  * Adler-32 (SURVEY A-9); inflate.hpp's decompressZlib keeps exactly that.  These entry points

@@ -46,6 +46,9 @@
 #define ORACLE_ERR_NOMEM (-3)
 
 #define ORACLE_RFC 1u
+/* Test-side stand-in for dmx_inflate_piece_device: the input is one piece of a larger stream,
+ * so a distance reaching before its first byte is an error instead of a no-op. */
+#define ORACLE_PIECE 2u
 
 typedef struct {
     const uint8_t* d;
@@ -269,7 +272,7 @@ static void fixed_trees(htree* lit, htree* dist) {
 }
 
 /* decompressHuffmanBlock (inflate.hpp:226-275) */
-static int huff_block(bitrd* b, obuf* o, const htree* lit, const htree* dist) {
+static int huff_block(bitrd* b, obuf* o, const htree* lit, const htree* dist, int piece) {
     for (;;) {
         int s, e;
         if ((e = ht_decode(lit, b, 15, 0, &s))) return e;
@@ -296,7 +299,11 @@ static int huff_block(bitrd* b, obuf* o, const htree* lit, const htree* dist) {
                 distance += extra;
             }
         }
-        if (distance == 0 || distance > o->n) continue; /* copies nothing (inflate.hpp:268) */
+        if (distance == 0 || length == 0) continue;
+        if (distance > o->n) { /* copies nothing (inflate.hpp:268) */
+            if (piece) return ORACLE_ERR_DATA;
+            continue;
+        }
         size_t src = o->n - distance;
         for (uint32_t j = 0; j < length; j++) {
             if ((e = ob_push(o, o->p[src + j]))) return e;
@@ -305,9 +312,17 @@ static int huff_block(bitrd* b, obuf* o, const htree* lit, const htree* dist) {
 }
 
 /* realDecompress (inflate.hpp:277-322) + decompress(void*, size_t) (inflate.hpp:363-374).
- * flags: ORACLE_RFC. On success *out is malloc'd (caller frees with oracle_free). */
+ * flags: ORACLE_RFC, ORACLE_PIECE. On success *out is malloc'd (caller frees with oracle_free). */
+int oracle_inflate2(const uint8_t* in, size_t n, uint32_t flags, uint8_t** out, size_t* out_len,
+                    size_t* consumed);
 int oracle_inflate(const uint8_t* in, size_t n, uint32_t flags, uint8_t** out, size_t* out_len) {
-    int rfc = (flags & ORACLE_RFC) != 0;
+    return oracle_inflate2(in, n, flags, out, out_len, NULL);
+}
+
+/* the same; *consumed (optional) = input bytes up to the end of the final block */
+int oracle_inflate2(const uint8_t* in, size_t n, uint32_t flags, uint8_t** out, size_t* out_len,
+                    size_t* consumed) {
+    int rfc = (flags & ORACLE_RFC) != 0, piece = (flags & ORACLE_PIECE) != 0;
     bitrd b = {in, n, 0, 0};
     obuf o = {NULL, 0, 0};
     htree flit, fdist;
@@ -326,13 +341,13 @@ int oracle_inflate(const uint8_t* in, size_t n, uint32_t flags, uint8_t** out, s
             if (e) break;
             b.off += len;
         } else if (type == 1) {
-            if ((e = huff_block(&b, &o, &flit, &fdist))) break;
+            if ((e = huff_block(&b, &o, &flit, &fdist, piece))) break;
         } else if (type == 2) {
             htree lit, dist;
             memset(&lit, 0, sizeof lit);
             memset(&dist, 0, sizeof dist);
             e = decode_dynamic(&b, &lit, &dist, rfc);
-            if (!e) e = huff_block(&b, &o, &lit, &dist);
+            if (!e) e = huff_block(&b, &o, &lit, &dist, piece);
             ht_free(&lit);
             ht_free(&dist);
             if (e) break;
@@ -349,6 +364,7 @@ int oracle_inflate(const uint8_t* in, size_t n, uint32_t flags, uint8_t** out, s
     }
     *out = o.p ? o.p : (uint8_t*)malloc(1);
     *out_len = o.n;
+    if (consumed) *consumed = b.off + (b.bit ? 1 : 0);
     return ORACLE_OK;
 }
 

@@ -27,23 +27,43 @@ def _buf(data):
 
 class Oracle:
     RFC = 1
+    PIECE = 2
 
     def __init__(self, path=ORACLE_SO):
         self.lib = ctypes.CDLL(path)
         self.lib.oracle_inflate.argtypes = [_u8p, ctypes.c_size_t, ctypes.c_uint32,
                                             ctypes.POINTER(_u8p), ctypes.POINTER(ctypes.c_size_t)]
         self.lib.oracle_inflate.restype = ctypes.c_int
+        self.lib.oracle_inflate2.argtypes = self.lib.oracle_inflate.argtypes + [ctypes.POINTER(ctypes.c_size_t)]
+        self.lib.oracle_inflate2.restype = ctypes.c_int
         self.lib.oracle_free.argtypes = [ctypes.c_void_p]
 
-    def inflate(self, data, rfc=False):
+    def inflate(self, data, rfc=False, piece=False):
         b, n = _buf(data)
         out = _u8p()
         ln = ctypes.c_size_t()
-        rc = self.lib.oracle_inflate(b, n, self.RFC if rfc else 0, ctypes.byref(out), ctypes.byref(ln))
+        fl = (self.RFC if rfc else 0) | (self.PIECE if piece else 0)
+        rc = self.lib.oracle_inflate(b, n, fl, ctypes.byref(out), ctypes.byref(ln))
         if rc != 0:
             raise CheckerError(rc)
         try:
             return ctypes.string_at(out, ln.value)
+        finally:
+            self.lib.oracle_free(out)
+
+
+    def inflate_consumed(self, data, piece=False):
+        """(decoded bytes, input bytes consumed up to the end of the final block)."""
+        b, n = _buf(data)
+        out = _u8p()
+        ln = ctypes.c_size_t()
+        used = ctypes.c_size_t()
+        rc = self.lib.oracle_inflate2(b, n, self.PIECE if piece else 0, ctypes.byref(out), ctypes.byref(ln),
+                                      ctypes.byref(used))
+        if rc != 0:
+            raise CheckerError(rc)
+        try:
+            return ctypes.string_at(out, ln.value), used.value
         finally:
             self.lib.oracle_free(out)
 

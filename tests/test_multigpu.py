@@ -115,43 +115,90 @@ def _gather_worker(rank, world, port, level, q):
     dist.destroy_process_group()
 
 
-def _scatter_worker(rank, world, port, name, q):
+def _oracle_decode(orc):
+    def decode(piece, first):  # the checker stands in for the GPU inflate on this CPU-only host
+        return torch.frombuffer(bytearray(orc.inflate(piece.numpy().tobytes(), piece=not first)),
+                                dtype=torch.uint8)
+    return decode
+
+
+def _oracle_check(orc, s):
+    """Stand-in for Context.segment_check_device: the segment at c must decode in piece mode up
+    to the first 00 00 FF FF after it (or to the stream end, as the final segment)."""
+    def check(cands):
+        ends = []
+        for c in cands:
+            m = s.find(b"\x00\x00\xff\xff", c)
+            e = m + 4 if m >= 0 else len(s)
+            piece = s[c:e] + (b"\x03\x00" if m >= 0 else b"")
+            try:  # the decode must end exactly at the piece's end (no early BFINAL in garbage)
+                _, used = orc.inflate_consumed(piece, piece=True)
+                ends.append(e if used == len(piece) else None)
+            except Exception:
+                ends.append(None)
+        return ends
+    return check
+
+
+def _scatter_case(name):
+    """(stream, candidate starts) of a named case."""
+    import zlib
+    if name == "corrupt-split":  # a false marker as the only cut: the pieces fail, rank 0 decodes whole
+        s = _read("mixed1M_L0_shard0.deflate") + _read("mixed1M_L0_shard1.deflate")
+        return s, [len(s) // 2 + 7]
+    if name == "false-marker":  # stored data holding 00 00 FF FF next to every cut target
+        import dmx
+        data = bytearray(dmx.corpus("random", 12 * SEG + 999, offset=5))
+        for i in range(1000, len(data) - 8, 4 * 1024 + 3):
+            data[i:i + 4] = b"\x00\x00\xff\xff"
+        s = stored_shard(bytes(data), final=True)
+        return s, _markers(s)
+    if name == "sync-flush":  # zlib sync flush: markers at real block boundaries, window carried over
+        import dmx
+        d = dmx.corpus("text", 6 * SEG, offset=3)
+        z = zlib.compressobj(6, zlib.DEFLATED, -15)
+        s = b"".join(z.compress(d[i:i + SEG]) + z.flush(zlib.Z_SYNC_FLUSH) for i in range(0, len(d), SEG)) + z.flush()
+        return s, _markers(s)
+    if name == "garbage":  # not a deflate stream at all: every rank must raise, none may hang
+        return bytes(range(256)) * 64, [1000, 5000]
+    s = _read(name)
+    return s, _markers(s)
+
+
+def _scatter_worker(rank, world, port, name, use_check, out_cap, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle_bind import Oracle
     orc = Oracle()
-
-    def decode(piece):  # the checker stands in for the GPU inflate on this CPU-only host
-        return torch.frombuffer(bytearray(orc.inflate(piece.numpy().tobytes())), dtype=torch.uint8)
-
-    if name == "corrupt-split":  # a false marker as the cut: the pieces fail, rank 0 decodes whole
-        s = _read("mixed1M_L0_shard0.deflate") + _read("mixed1M_L0_shard1.deflate")
-        starts = [len(s) // 2 + 7]
-    else:
-        s = _read(name)
-        starts = _markers(s)
+    s, starts = _scatter_case(name)
     stream = torch.frombuffer(bytearray(s), dtype=torch.uint8) if rank == 0 else torch.empty(0, dtype=torch.uint8)
-    out = torch.empty(4 << 20, dtype=torch.uint8) if rank == 0 else None
-    total, ok = shard.scatter_inflate(stream, len(s) if rank == 0 else 0, decode,
-                                      starts=starts if rank == 0 else None, out=out)
-    if rank == 0:
-        q.put((bytes(out[:total].numpy()), ok))
+    out = torch.empty(out_cap, dtype=torch.uint8) if rank == 0 else None
+    try:
+        total, ok = shard.scatter_inflate(stream, len(s) if rank == 0 else 0, _oracle_decode(orc),
+                                          starts=starts if rank == 0 else None, out=out,
+                                          check=_oracle_check(orc, s) if use_check else None)
+        res = (bytes(out[:total].numpy()), ok)
+    except Exception as e:  # every rank reports (a rank that hung would time the test out)
+        res = ("raised", type(e).__name__)
+    q.put((rank, res))
     dist.destroy_process_group()
 
 
-def _run(target, world, *args):
+def _run(target, world, *args, all_ranks=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
     for p in procs:
         p.start()
-    res = q.get(timeout=180)
+    res = [q.get(timeout=180) for _ in range(world if all_ranks else 1)]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    return res
+    if all_ranks:
+        return dict(res)
+    return res[0]
 
 
 @pytest.mark.parametrize("level", [0, 2])
@@ -171,13 +218,16 @@ def test_gather_of_libdmx_shards(oracle, level):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_scatter_inflate_libdmx_stream(oracle, world):
-    """SURVEY 8(e) inflate: rank 0 cuts a libdmx stream at segment starts, every rank decodes its
-    piece, the pieces gather back to rank 0 bit-exact."""
+@pytest.mark.parametrize("use_check", [False, True])
+def test_scatter_inflate_libdmx_stream(oracle, world, use_check):
+    """SURVEY 8(e) inflate: rank 0 cuts a libdmx stream at segment starts (raw candidates, or only
+    those the segment check proves), every rank decodes its piece, the pieces gather back to
+    rank 0 bit-exact."""
     import hashlib
     m = _dmx_manifest()
     full = next(s for s in m["streams"] if s["file"] == "mixed1M_L2.deflate")
-    dec, ok = _run(_scatter_worker, world, "mixed1M_L2.deflate")
+    res = _run(_scatter_worker, world, "mixed1M_L2.deflate", use_check, 4 << 20, all_ranks=True)
+    dec, ok = res[0]
     assert ok
     assert hashlib.sha256(dec).hexdigest() == full["out_sha256"]
 
@@ -186,9 +236,83 @@ def test_scatter_inflate_false_marker_falls_back(oracle):
     """A cut at a 00 00 FF FF that is not a segment start: the piece before it over-reads, all
     ranks see the failure, rank 0 decodes the stream whole (same bytes)."""
     s = _read("mixed1M_L0_shard0.deflate") + _read("mixed1M_L0_shard1.deflate")
-    dec, ok = _run(_scatter_worker, 2, "corrupt-split")
+    dec, ok = _run(_scatter_worker, 2, "corrupt-split", False, 4 << 20, all_ranks=True)[0]
     assert not ok
     assert dec == oracle.inflate(s)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_scatter_inflate_false_markers_still_split(oracle, world):
+    """00 00 FF FF inside stored data next to every cut target: the segment check rejects those
+    candidates, the cuts move to proven segment starts, the split still happens (ok) and the
+    bytes are exact; without the check a false cut is taken and the run falls back."""
+    s, _ = _scatter_case("false-marker")
+    dec, ok = _run(_scatter_worker, world, "false-marker", True, 1 << 20, all_ranks=True)[0]
+    assert ok and dec == oracle.inflate(s)
+    dec, ok = _run(_scatter_worker, world, "false-marker", False, 1 << 20, all_ranks=True)[0]
+    assert dec == oracle.inflate(s)
+
+
+@pytest.mark.parametrize("use_check", [False, True])
+def test_scatter_inflate_sync_flush_stream_never_drops_bytes(oracle, use_check):
+    """a zlib Z_SYNC_FLUSH stream has 00 00 FF FF at real block boundaries but its
+    window carries across them.  Pieces after the first decode in piece mode, so a reference
+    before the cut fails instead of silently copying nothing: the result is exact either way
+    (the check refuses the cuts, or the pieces fail and rank 0 decodes whole)."""
+    s, _ = _scatter_case("sync-flush")
+    want = oracle.inflate(s)
+    dec, ok = _run(_scatter_worker, 2, "sync-flush", use_check, 1 << 20, all_ranks=True)[0]
+    assert dec == want
+    if not use_check:
+        assert not ok
+
+
+def test_scatter_inflate_errors_raise_on_every_rank():
+    """a stream that does not decode, or an output buffer that is too small, raises on
+    every rank (no rank left blocking in a collective)."""
+    res = _run(_scatter_worker, 2, "garbage", False, 1 << 20, all_ranks=True)
+    assert res[0][0] == "raised" and res[1][0] == "raised"
+    res = _run(_scatter_worker, 3, "mixed1M_L2.deflate", False, 1000, all_ranks=True)
+    assert all(r[0] == "raised" and r[1] == "ValueError" for r in res.values())
+
+
+class _HostDeflate:
+    """CPU stand-in for dmx.Context.deflate_device: stored segments in libdmx's layout, read
+    from and written to host pointers (torch CPU tensors)."""
+
+    def deflate_device(self, d_in, n, level, d_out, cap, not_final=False):
+        import ctypes
+        s = stored_shard(ctypes.string_at(d_in, n), final=not not_final)
+        assert len(s) <= cap
+        ctypes.memmove(d_out, s, len(s))
+        return len(s)
+
+
+def _deflate_gather_worker(rank, world, port, total, sub, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import dmx
+    data = dmx.corpus("mixed", total)
+    b, e = shard.shard_range(total, rank, world, SEG)
+    d_in = torch.frombuffer(bytearray(data[b:e] or b"\0"), dtype=torch.uint8)
+    out = torch.empty(2 * total + 4096, dtype=torch.uint8) if rank == 0 else None
+    n, mine = shard.deflate_gather(_HostDeflate(), d_in, e - b, 0, out=out, sub=sub)
+    q.put((rank, bytes(out[:n].numpy()) if rank == 0 else mine))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,sub", [(2, 3), (3, 4)])
+def test_deflate_gather_pipelined(oracle, world, sub):
+    """The pipelined gather (sub-shards sent while the next compresses) assembles the same
+    single valid stream as the one-shot gather: the oracle decodes it to the corpus."""
+    import dmx
+    total = 11 * SEG + 777
+    res = _run(_deflate_gather_worker, world, total, sub, all_ranks=True)
+    stream = res[0]
+    assert oracle.inflate(stream) == dmx.corpus("mixed", total)
+    assert len(stream) == sum(v if r else 0 for r, v in res.items()) + \
+        len(stream) - sum(v for r, v in res.items() if r)
 
 
 def test_split_points():
