@@ -61,6 +61,7 @@ struct dmx_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     DevBuf in, out, slots, sizes, offs, scal, cands, tiles, tileoffs, recs, status, dbg;
+    DevBuf rtmp, rchain;                 // chain repair: scratch output, chain / offsets / sizes
     DevBuf ltok, ltokoff, lntok, lcaps;  // lane decoder token lists (mode 4)
     DevBuf lheavy;                       // heavy-candidate list for the workgroup decoder (mode 6)
     int ncu = 0;                         // compute units (mode 6 grid)
@@ -468,50 +469,59 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     // no marker in a large stream: not libdmx's segment layout, the block-parallel path next
     if (ncand == 1 && n > 65536 && path_env == -1) np = 0;
     if (path_env == 5) np = 0;
-    for (int pi = 0; pi < np; pi++) {
-        const uint32_t mode = plan[pi][0];
-        if (mode == 3 && (r.exotic == 0 || r.exotic > ncand / 8)) continue;  // nothing / too many
-        if (mode == 6 && r.exotic == 0) continue;
-        A.mode = mode;
-        A.slot = plan[pi][1];
-        // main-kernel window: from the first pass's launch to the end of the last pass run
-        hipEvent_t e0 = (c->timing && pi == 0) ? c->ev[1] : nullptr, e1 = c->timing ? c->ev[2] : nullptr;
-        if (mode != 3 && mode != 6) lead_mode = mode;
-        if (mode == 4) {
-            HIPCHK(launch_inflate_lanes(A, c->ltok.as<uint32_t>(), c->ltokoff.as<uint64_t>(),
-                                        c->lntok.as<uint32_t>(), c->lcaps.as<uint32_t>(), heavy,
-                                        heavy_limit, c->lheavy.as<uint32_t>(), st, e0, e1));
-        } else if (mode == 6) {
-            const uint32_t grid = (uint32_t)std::min<uint64_t>(r.exotic, (uint64_t)std::max(c->ncu, 1));
-            HIPCHK(launch_inflate_pj_list(A, A.slot, c->lheavy.as<uint32_t>(), grid, st, e1));
-        } else if (mode == 2) {
-            HIPCHK(launch_inflate_pj(A, A.slot, st, e0, e1));
-        } else {
-            HIPCHK(hipMemsetAsync(A.status, 0, ncand * 8, st));
-            HIPCHK(hipMemsetAsync(&ds->ticket, 0, 4, st));
-            HIPCHK(launch_inflate_segments(A, st, e0, e1));
-        }
-        HIPCHK(launch_inflate_validate(A, &ds->vw, &ds->res, st));
-        if (A.dbg) phase_dump(c, "inflate", ncand, st);
-        HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        if (std::getenv("DMX_RECS")) {  // developer aid: per-candidate outcome of this pass
-            std::vector<SegRecord> h(ncand);
-            (void)hipMemcpy(h.data(), A.recs, ncand * sizeof(SegRecord), hipMemcpyDeviceToHost);
-            uint64_t fl[8] = {0}, shown = 0;
-            for (uint64_t i = 0; i < ncand; i++) {
-                for (int b = 0; b < 8; b++) fl[b] += (h[i].flags >> b) & 1;
-                if ((h[i].flags & ~1u) && shown++ < 8)
-                    std::fprintf(stderr, "dmx: mode %u cand %llu flags %u size %u end %llu next %llu\n", mode,
-                                 (unsigned long long)i, h[i].flags, h[i].out_size,
-                                 (unsigned long long)h[i].end_byte, (unsigned long long)(i + 1 < ncand ? 0 : 0));
+    // the plan's passes into A.out / A.cap; returns the last validation result
+    auto run_plan = [&](InflateResult& r) -> int {
+        r.status = 2;
+        for (int pi = 0; pi < np; pi++) {
+            const uint32_t mode = plan[pi][0];
+            if (mode == 3 && (r.exotic == 0 || r.exotic > ncand / 8)) continue;  // nothing / too many
+            if (mode == 6 && r.exotic == 0) continue;
+            A.mode = mode;
+            A.slot = plan[pi][1];
+            // main-kernel window: from the first pass's launch to the end of the last pass run
+            hipEvent_t e0 = (c->timing && pi == 0) ? c->ev[1] : nullptr, e1 = c->timing ? c->ev[2] : nullptr;
+            if (mode != 3 && mode != 6) lead_mode = mode;
+            if (mode == 4) {
+                HIPCHK(launch_inflate_lanes(A, c->ltok.as<uint32_t>(), c->ltokoff.as<uint64_t>(),
+                                            c->lntok.as<uint32_t>(), c->lcaps.as<uint32_t>(), heavy,
+                                            heavy_limit, c->lheavy.as<uint32_t>(), st, e0, e1));
+            } else if (mode == 6) {
+                const uint32_t grid = (uint32_t)std::min<uint64_t>(r.exotic, (uint64_t)std::max(c->ncu, 1));
+                HIPCHK(launch_inflate_pj_list(A, A.slot, c->lheavy.as<uint32_t>(), grid, st, e1));
+            } else if (mode == 2) {
+                HIPCHK(launch_inflate_pj(A, A.slot, st, e0, e1));
+            } else {
+                HIPCHK(hipMemsetAsync(A.status, 0, ncand * 8, st));
+                HIPCHK(hipMemsetAsync(&ds->ticket, 0, 4, st));
+                HIPCHK(launch_inflate_segments(A, st, e0, e1));
             }
-            std::fprintf(stderr, "dmx: mode %u ncand %llu status %u flags fin %llu data %llu over %llu ovf %llu xref %llu tmo %llu exo %llu\n",
-                         mode, (unsigned long long)ncand, r.status, (unsigned long long)fl[0], (unsigned long long)fl[1],
-                         (unsigned long long)fl[2], (unsigned long long)fl[3], (unsigned long long)fl[4],
-                         (unsigned long long)fl[5], (unsigned long long)fl[6]);
+            HIPCHK(launch_inflate_validate(A, &ds->vw, &ds->res, st));
+            if (A.dbg) phase_dump(c, "inflate", ncand, st);
+            HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            if (std::getenv("DMX_RECS")) {  // developer aid: per-candidate outcome of this pass
+                std::vector<SegRecord> h(ncand);
+                (void)hipMemcpy(h.data(), A.recs, ncand * sizeof(SegRecord), hipMemcpyDeviceToHost);
+                uint64_t fl[8] = {0}, shown = 0;
+                for (uint64_t i = 0; i < ncand; i++) {
+                    for (int b = 0; b < 8; b++) fl[b] += (h[i].flags >> b) & 1;
+                    if ((h[i].flags & ~1u) && shown++ < 8)
+                        std::fprintf(stderr, "dmx: mode %u cand %llu flags %u size %u end %llu\n", mode,
+                                     (unsigned long long)i, h[i].flags, h[i].out_size,
+                                     (unsigned long long)h[i].end_byte);
+                }
+                std::fprintf(stderr, "dmx: mode %u ncand %llu status %u flags fin %llu data %llu over %llu ovf %llu xref %llu tmo %llu exo %llu\n",
+                             mode, (unsigned long long)ncand, r.status, (unsigned long long)fl[0], (unsigned long long)fl[1],
+                             (unsigned long long)fl[2], (unsigned long long)fl[3], (unsigned long long)fl[4],
+                             (unsigned long long)fl[5], (unsigned long long)fl[6]);
+            }
+            if (r.status != 1) break;  // 1: not this layout
         }
-        if (r.status != 1) break;  // 1: not this layout
+        return DMX_OK;
+    };
+    {
+        const int rc = run_plan(r);
+        if (rc != DMX_OK) return rc;
     }
     c->stats.segments = ncand;
     c->stats.in_bytes = n;
@@ -522,6 +532,75 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
         *total_out = r.total;
         if (dev_out) *dev_out = out;
         return r.total > cap ? DMX_ERR_CAPACITY : DMX_OK;
+    }
+    // Chain repair.  A "00 00 FF FF" inside stored data (random data: once per ~4 GiB) is a
+    // candidate no segment starts at, so the candidate chain skips it and every later segment
+    // sits one slot too far; the whole stream used to go to the serial decoder (hours at
+    // multi-GiB sizes).  The records say where each segment ends: the host walks the chain
+    // from candidate 0 (each segment's end must be a candidate start, up to the first BFINAL),
+    // the segments are decoded into a scratch buffer at their slots if the first decode did
+    // not hold every slot, and one kernel moves the chain's segments to their offsets.
+    if (r.status == 2 && lead_mode == 4 && parallel_ok && ncand > 1) {
+        std::vector<SegRecord> h(ncand);
+        std::vector<uint64_t> hc(ncand);
+        HIPCHK(hipMemcpyAsync(h.data(), A.recs, ncand * sizeof(SegRecord), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(hc.data(), A.cands, ncand * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        std::vector<uint64_t> chain, coffs;
+        std::vector<uint32_t> csz;
+        uint64_t tot = 0, k = 0;
+        bool ok = false;
+        for (;;) {
+            const SegRecord& s = h[k];
+            if (s.flags & ~SEGF_FINAL) break;
+            chain.push_back(k);
+            coffs.push_back(tot);
+            csz.push_back(s.out_size);
+            tot += s.out_size;
+            if (s.flags & SEGF_FINAL) { ok = true; break; }
+            const auto it = std::lower_bound(hc.begin() + k + 1, hc.end(), s.end_byte);
+            if (it == hc.end() || *it != s.end_byte) break;
+            k = (uint64_t)(it - hc.begin());
+        }
+        const uint64_t slot = A.slot ? A.slot : c->seg;
+        if (ok && chain.size() < ncand) {
+            if (fixed_out && tot > cap) return DMX_ERR_CAPACITY;
+            uint8_t* dst = fixed_out ? fixed_out : out;
+            const uint64_t need = (chain.back() + 1) * slot;
+            const uint8_t* src = out;
+            uint8_t* place = dst;  // where the kernel writes; then copied to dst if scratch
+            if (need > A.cap) {  // slots past the buffer were not written: decode again into
+                                 // scratch that holds every slot, place into dst
+                if (!c->rtmp.ensure(ncand * slot)) return DMX_ERR_NOMEM;
+                A.out = c->rtmp.as<uint8_t>();
+                A.cap = ncand * slot;
+                InflateResult r2{};
+                const int rc = run_plan(r2);
+                if (rc != DMX_OK) return rc;
+                src = A.out;
+            } else {  // every slot is in `out` (== dst): place into scratch, copy back
+                if (!c->rtmp.ensure(tot ? tot : 1)) return DMX_ERR_NOMEM;
+                place = c->rtmp.as<uint8_t>();
+            }
+            const uint64_t nch = chain.size();
+            if (!c->rchain.ensure(nch * 20)) return DMX_ERR_NOMEM;
+            uint64_t* dch = c->rchain.as<uint64_t>();
+            uint64_t* doffs = dch + nch;
+            uint32_t* dsz = reinterpret_cast<uint32_t*>(doffs + nch);
+            HIPCHK(hipMemcpyAsync(dch, chain.data(), nch * 8, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(doffs, coffs.data(), nch * 8, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(dsz, csz.data(), nch * 4, hipMemcpyHostToDevice, st));
+            HIPCHK(launch_place_segments(src, (uint32_t)slot, dch, doffs, dsz, nch, place, st));
+            if (place != dst && tot) HIPCHK(hipMemcpyAsync(dst, place, tot, hipMemcpyDeviceToDevice, st));
+            if (c->timing) (void)hipEventRecord(c->ev[2], st);
+            HIPCHK(hipStreamSynchronize(st));
+            end_timing(c, st);
+            c->stats.path = 4;
+            c->stats.out_bytes = tot;
+            *total_out = tot;
+            if (dev_out) *dev_out = dst;
+            return DMX_OK;
+        }
     }
 
     if (path_env == -1 || path_env == 5) {
@@ -683,7 +762,7 @@ void dmx_destroy(dmx_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->in, &c->out, &c->slots, &c->sizes, &c->offs, &c->scal, &c->cands,
                       &c->tiles, &c->tileoffs, &c->recs, &c->status, &c->dbg, &c->ltok,
-                      &c->ltokoff, &c->lntok, &c->lcaps, &c->lheavy, &c->fbc, &c->fbh, &c->fbo, &c->fbl,
+                      &c->ltokoff, &c->lntok, &c->lcaps, &c->lheavy, &c->rtmp, &c->rchain, &c->fbc, &c->fbh, &c->fbo, &c->fbl,
                       &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg, &c->fbstop,
                       &c->ck})
         b->release();

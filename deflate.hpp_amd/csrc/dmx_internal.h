@@ -153,6 +153,8 @@ hipError_t launch_adler32(const uint8_t* d, uint64_t n, uint32_t init, void* scr
 hipError_t launch_crc32_raw(const uint8_t* d, uint64_t n, void* scratch, uint32_t* d_out, hipStream_t st);
 uint32_t crc32_finish(uint32_t raw, uint64_t n, uint32_t init);
 
+hipError_t launch_place_segments(const uint8_t* src, uint32_t slot, const uint64_t* chain, const uint64_t* offs,
+                                 const uint32_t* sizes, uint64_t nch, uint8_t* dst, hipStream_t st);
 hipError_t launch_segment_check(const InflateArgs& A, const uint64_t* starts, uint64_t k, uint64_t* ends,
                                 hipStream_t st);
 hipError_t launch_inflate_serial(const InflateArgs& A, int count_only, InflateResult* res,

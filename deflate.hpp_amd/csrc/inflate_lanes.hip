@@ -996,6 +996,34 @@ __global__ void k_heavy_count(const uint8_t* in, const uint64_t* cands, uint64_t
     if (lane_id() == 0 && b) atomicAdd(cnt, (uint32_t)__popcll(b));  // lane 0 holds the wave's first j
 }
 
+// Chain repair (dmx_host.cpp, rare): segment chain[k] was written at chain[k] * slot of src;
+// it goes to dst + offs[k] (sizes[k] bytes).  One workgroup per segment, 16-byte copies when
+// both sides are aligned.
+__global__ __launch_bounds__(256) void k_place_segments(const uint8_t* src, uint32_t slot, const uint64_t* chain,
+                                                         const uint64_t* offs, const uint32_t* sizes,
+                                                         uint64_t nch, uint8_t* dst) {
+    const uint64_t k = blockIdx.x;
+    if (k >= nch) return;
+    const uint8_t* s = src + chain[k] * (uint64_t)slot;
+    uint8_t* d = dst + offs[k];
+    const uint32_t n = sizes[k];
+    if ((((uintptr_t)s | (uintptr_t)d) & 15) == 0) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(s);
+        uint4* d4 = reinterpret_cast<uint4*>(d);
+        for (uint32_t i = threadIdx.x; i < n / 16; i += 256) d4[i] = s4[i];
+        for (uint32_t i = (n & ~15u) + threadIdx.x; i < n; i += 256) d[i] = s[i];
+    } else {
+        for (uint32_t i = threadIdx.x; i < n; i += 256) d[i] = s[i];
+    }
+}
+
+hipError_t launch_place_segments(const uint8_t* src, uint32_t slot, const uint64_t* chain, const uint64_t* offs,
+                                 const uint32_t* sizes, uint64_t nch, uint8_t* dst, hipStream_t st) {
+    if (nch) hipLaunchKernelGGL(k_place_segments, dim3((uint32_t)nch), dim3(256), 0, st, src, slot, chain, offs, sizes,
+                                nch, dst);
+    return hipGetLastError();
+}
+
 hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* tokoff,
                                 uint32_t* ntok, uint32_t* caps, uint32_t heavy, uint32_t limit,
                                 uint32_t* hl, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {

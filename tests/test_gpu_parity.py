@@ -318,3 +318,29 @@ def test_c4_eight_shards_of_1GiB_mixed_on_one_gpu(ctx, oracle):
     olen = ctx.inflate_device(full.data_ptr(), full.numel(), d_out.data_ptr(), n + 64)
     assert olen == n and torch.equal(d_out[:n], d_in)
     assert ctx.stats().path == 4
+
+
+@pytest.mark.parametrize("device_api", [False, True])
+def test_inflate_false_markers_chain_repair(ctx, oracle, device_api):
+    """00 00 FF FF inside stored segments (random data holds one per ~4 GiB) are candidates no
+    segment starts at: the chain repair walks the segments' end bytes past them and places the
+    segments at their true offsets, still on the lane path (4), bit-exact -- through the host
+    API (slots in the context's buffer) and the device API (exact-size output: the segments
+    past the caller's buffer are decoded again into scratch)."""
+    import torch
+    rng = random.Random(9)
+    blob = bytearray(rng.randbytes(8 << 20))
+    for i in range(40000, len(blob) - 8, 1 << 20):
+        blob[i:i + 4] = b"\x00\x00\xff\xff"
+    blob = bytes(blob)
+    s = ctx.compress(blob, 2)
+    assert s.count(b"\x00\x00\xff\xff") > len(blob) // 32768
+    if device_api:
+        d_s = torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda()
+        d_o = torch.empty(len(blob), dtype=torch.uint8, device="cuda")
+        assert ctx.inflate_device(d_s.data_ptr(), len(s), d_o.data_ptr(), len(blob)) == len(blob)
+        assert d_o.cpu().numpy().tobytes() == blob
+    else:
+        assert ctx.decompress(s) == blob
+    assert ctx.stats().path == 4
+    assert oracle.inflate(s) == blob
