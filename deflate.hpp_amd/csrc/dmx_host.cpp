@@ -51,6 +51,7 @@ struct DevBuf {
 };
 
 constexpr uint32_t kSegCap = 32768;  // LDS window of k_inflate_segments
+constexpr uint64_t LN_OUT_CAP_BYTES = 32768;  // largest segment output of the lane decoder
 
 }  // namespace
 
@@ -516,6 +517,10 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
                              (unsigned long long)fl[5], (unsigned long long)fl[6]);
             }
             if (r.status != 1) break;  // 1: not this layout
+            // the lane pass decoded every candidate but the segment sizes are not uniform (a
+            // shard ending on a short segment, 16 KiB segments): the chain repair below
+            // places them, the other passes would only decode everything again
+            if (lead_mode == 4 && r.exotic == 0 && (mode == 4 || mode == 6 || mode == 3)) break;
         }
         return DMX_OK;
     };
@@ -536,11 +541,12 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     // Chain repair.  A "00 00 FF FF" inside stored data (random data: once per ~4 GiB) is a
     // candidate no segment starts at, so the candidate chain skips it and every later segment
     // sits one slot too far; the whole stream used to go to the serial decoder (hours at
-    // multi-GiB sizes).  The records say where each segment ends: the host walks the chain
+    // multi-GiB sizes).  Segments of other sizes than the slot (a short segment in the middle,
+    // 16 KiB segments) are placed the same way.  The records say where each segment ends: the host walks the chain
     // from candidate 0 (each segment's end must be a candidate start, up to the first BFINAL),
     // the segments are decoded into a scratch buffer at their slots if the first decode did
     // not hold every slot, and one kernel moves the chain's segments to their offsets.
-    if (r.status == 2 && lead_mode == 4 && parallel_ok && ncand > 1) {
+    if (r.status != 0 && lead_mode == 4 && parallel_ok && ncand > 1) {
         std::vector<SegRecord> h(ncand);
         std::vector<uint64_t> hc(ncand);
         HIPCHK(hipMemcpyAsync(h.data(), A.recs, ncand * sizeof(SegRecord), hipMemcpyDeviceToHost, st));
@@ -562,15 +568,22 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
             if (it == hc.end() || *it != s.end_byte) break;
             k = (uint64_t)(it - hc.begin());
         }
-        const uint64_t slot = A.slot ? A.slot : c->seg;
-        if (ok && chain.size() < ncand) {
+        uint64_t slot = A.slot ? A.slot : c->seg;
+        if (ok) {
             if (fixed_out && tot > cap) return DMX_ERR_CAPACITY;
             uint8_t* dst = fixed_out ? fixed_out : out;
             const uint64_t need = (chain.back() + 1) * slot;
+            const uint32_t maxsz = *std::max_element(csz.begin(), csz.end());
             const uint8_t* src = out;
             uint8_t* place = dst;  // where the kernel writes; then copied to dst if scratch
-            if (need > A.cap) {  // slots past the buffer were not written: decode again into
-                                 // scratch that holds every slot, place into dst
+            if (need > A.cap || maxsz > slot) {
+                // slots past the buffer were not written, or segments larger than the slot
+                // overlapped: decode again into scratch with 32 KiB slots, place into dst
+                if (maxsz > slot) {
+                    slot = LN_OUT_CAP_BYTES;
+                    for (int pi = 0; pi < np; pi++)
+                        if (plan[pi][0] == 4 || plan[pi][0] == 6 || plan[pi][0] == 3) plan[pi][1] = (uint32_t)slot;
+                }
                 if (!c->rtmp.ensure(ncand * slot)) return DMX_ERR_NOMEM;
                 A.out = c->rtmp.as<uint8_t>();
                 A.cap = ncand * slot;

@@ -535,6 +535,9 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             win = window_at(bp, ring2[pr & 15], ring2[(pr + 1) & 15]);
         }
         auto step = [&]() -> bool {
+#ifdef DMX_LN_COUNT
+            n_iter++;  // diagnostic build: steps per lane (DMX_PHASES slot 8)
+#endif
             const uint32_t pr = bp >> 6;
             const uint64_t nq0 = ring2[(pr + 1) & 15], nq1 = ring2[(pr + 2) & 15];
             // lit/len symbol, then the distance decoded from the same window (used for lengths)
@@ -612,9 +615,21 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
         };
         static_assert(LN_PERIOD == 3, "steps per period below");
         for (;;) {
+#ifdef DMX_LN_COUNT
+            const uint64_t ts0 = __builtin_amdgcn_s_memtime();
             stage(S0, v0, tq0);
+            n_top += (uint32_t)(__builtin_amdgcn_s_memtime() - ts0);  // cycles in stage (slot 9)
+#else
+            stage(S0, v0, tq0);
+#endif
             if (!step() || !step() || !step()) break;
+#ifdef DMX_LN_COUNT
+            const uint64_t ts1 = __builtin_amdgcn_s_memtime();
             stage(S1, v1, tq1);
+            n_top += (uint32_t)(__builtin_amdgcn_s_memtime() - ts1);
+#else
+            stage(S1, v1, tq1);
+#endif
             if (!step() || !step() || !step()) break;
         }
         endbit = bp;

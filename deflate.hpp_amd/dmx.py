@@ -174,6 +174,18 @@ class Context:
         _check(lib().dmx_deflate(self.h, data, len(data), level, out, cap, ctypes.byref(n)), "deflate")
         return out.raw[: n.value]
 
+    def compress_raw_not_final(self, data, level=2):
+        """One shard of a larger stream (DMX_DEFLATE_NOT_FINAL: no BFINAL, ends byte-aligned on
+        an empty stored block), through the device API."""
+        import torch
+        data = bytes(data)
+        d_in = torch.frombuffer(bytearray(data or b"\0"), dtype=torch.uint8).cuda()
+        cap = deflate_bound(len(data)) + 64
+        d_out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        n = self.deflate_device(d_in.data_ptr(), len(data), level, d_out.data_ptr(), cap, not_final=True)
+        torch.cuda.synchronize()
+        return d_out[:n].cpu().numpy().tobytes()
+
     def decompress(self, data, cap=None):
         """inflate::decompress(void*, size_t) -> bytes; with cap: the (void*,size_t,void*,size_t)
         overload (returns at most cap bytes)."""

@@ -21,6 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "deflate.hpp_amd"))
+sys.path.insert(0, HERE)
 from oracle_bind import Reference, CheckerError  # noqa: E402
 
 import ctypes  # noqa: E402
@@ -169,6 +170,7 @@ def main():
                            "stream_sha256": sha(c3), "out_len": len(c3out), "out_sha256": sha(c3out),
                            "equals_original": c3out == bmp, "how": "reference inflate::decompress of "
                            "zlib.compressobj(1, DEFLATED, -15) of dmx.corpus('bmp', 25165962)"}
+    quirk_manifest(ref, man)
     # 10. corpus checksums for the generator
     man["corpus_sha256_1MiB"] = {k: sha(dmx.corpus(k, 1 << 20)) for k in ("zeros", "repeat", "random", "text", "mixed")}
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
@@ -177,5 +179,29 @@ def main():
     print(f"{len(man['vectors'])} vectors, {tot / 1e6:.2f} MB under tests/golden")
 
 
+def quirk_manifest(ref, man):
+    """11. the reference's quirks in the middle of a large marker-poor stream (path 5):
+    tests/golden/quirk_streams.py builds it (zlib level 1 + the crafted quirk section); too
+    large to commit, so tests regenerate it and check its SHA-256 first."""
+    import quirk_streams as Q
+    text = dmx.corpus("text", (2 << 20) + 4096, offset=7777)
+    s1, sec, b = Q.path5_stream(text)
+    hist = ref.decompress(s1 + sec + b"\x03\x00")
+    s = Q.finish_path5(s1, sec, b, hist)
+    out = ref.decompress(s)
+    man["quirk_path5"] = {"text_offset": 7777, "text_len": len(text), "stream_len": len(s), "stream_sha256": sha(s),
+                          "out_len": len(out), "out_sha256": sha(out), "section_len": len(sec),
+                          "how": "reference inflate::decompress of quirk_streams.path5_stream (zlib-1 halves, "
+                                 "sync flush, quirk section Q1..Q5, preset-dictionary second half)"}
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--quirks"]:  # only (re)write the quirk entry of the existing manifest
+        mp = os.path.join(HERE, "manifest.json")
+        m = json.load(open(mp))
+        quirk_manifest(Reference(), m)
+        with open(mp, "w") as f:
+            json.dump(m, f, indent=1)
+        print(m["quirk_path5"])
+    else:
+        main()

@@ -344,3 +344,72 @@ def test_inflate_false_markers_chain_repair(ctx, oracle, device_api):
         assert ctx.decompress(s) == blob
     assert ctx.stats().path == 4
     assert oracle.inflate(s) == blob
+
+
+# ---------------------------------------------------------------------------------------
+# the reference's quirks where the fast paths run
+# ---------------------------------------------------------------------------------------
+def _quirk_module():
+    import sys
+    sys.path.insert(0, GOLD)
+    import quirk_streams
+    return quirk_streams
+
+
+def test_inflate_quirks_mid_stream_block_parallel_path(ctx, oracle):
+    """Bad-NLEN stored block, BTYPE-3 block, a 258-byte copy from 32 KiB back at a block start,
+    an A-11 and an A-12 dynamic header, in the middle of a zlib-1 stream of 2 MiB of output:
+    decoded on the block-parallel path 5, bit-exact with the compiled reference (SHA from
+    make_golden.py)."""
+    Q = _quirk_module()
+    q = MAN["quirk_path5"]
+    text = dmx.corpus("text", q["text_len"], offset=q["text_offset"])
+    s1, sec, b = Q.path5_stream(text)
+    s = Q.finish_path5(s1, sec, b, oracle.inflate(s1 + sec + b"\x03\x00"))
+    assert sha(s) == q["stream_sha256"], "zlib produced another stream"
+    out = ctx.decompress(s)
+    path = ctx.stats().path
+    assert len(out) == q["out_len"] and sha(out) == q["out_sha256"]
+    assert path == 5, f"decoded on path {path}"
+
+
+@pytest.mark.parametrize("far", [False, True])
+def test_inflate_quirks_in_libdmx_layout(ctx, oracle, far):
+    """The same quirk section spliced as one more segment into a 2 MiB libdmx stream (segment
+    layout, 00 00 FF FF markers).  far=False: the section decodes alone; the lanes decline it
+    and the exact wave decoder patches it, the stream stays on path 4.  far=True: its copy
+    reaches 32 KiB back into the segment before (a cross-segment reference, which libdmx never
+    writes): the segment paths refuse it and a whole-stream decoder takes over.  Both bit-exact
+    with the oracle."""
+    Q = _quirk_module()
+    d = dmx.corpus("text", 2 << 20, offset=31337)
+    s = ctx.compress(d, 2)
+    sec = Q.quirk_section(dmx.corpus("text", 4096, offset=99), far=far)
+    st, cut = Q.splice_into_segments(s, len(s) // 2, sec)
+    want = oracle.inflate(st)
+    out = ctx.decompress(st)
+    path = ctx.stats().path
+    assert out == want
+    if not far:
+        assert path == 4, f"decoded on path {path}"
+    else:
+        assert path in (2, 5), f"decoded on path {path}"
+
+
+def test_inflate_nonuniform_segments_stay_on_lanes(ctx, oracle):
+    """Shards of unaligned sizes compressed NOT_FINAL and concatenated put short segments in the
+    middle of the stream: the lane pass decodes them all and the chain repair places them (path
+    4), bit-exact.  A context with 16 KiB slots decodes a stream of 32 KiB segments on a
+    segment-parallel path (not the serial decoder)."""
+    d = dmx.corpus("mixed", 3 << 20, offset=4242)
+    cuts = [0, 100000, 300001, 1500000, len(d)]
+    s = b"".join(ctx.compress_raw_not_final(d[a:b]) if i < len(cuts) - 2 else ctx.compress(d[a:b], 2)
+                 for i, (a, b) in enumerate(zip(cuts, cuts[1:])))
+    assert ctx.decompress(s) == d
+    assert ctx.stats().path == 4
+    assert oracle.inflate(s) == d
+    c16 = dmx.Context(segment_bytes=16384)
+    full = ctx.compress(d, 2)
+    assert c16.decompress(full) == d
+    assert c16.stats().path in (3, 4)
+    c16.close()

@@ -89,3 +89,23 @@ def test_oracle_equals_compiled_reference_on_fresh_streams(oracle):
             z = zlib.compressobj(lvl, zlib.DEFLATED, -15)
             s = z.compress(data) + z.flush()
             assert oracle.inflate(s) == ref.decompress(s) == data
+
+
+def test_oracle_quirk_path5_stream_matches_reference():
+    """The quirk section (bad NLEN, BTYPE 3, far copy at a block start, A-11, A-12) in the
+    middle of a 2 MiB-output zlib-1 stream: the oracle gives the compiled reference's SHA-256
+    (tests/golden/quirk_streams.py, manifest 'quirk_path5')."""
+    import hashlib
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import dmx
+    import quirk_streams as Q
+    from oracle_bind import Oracle
+    q = json.load(open(os.path.join(GOLD, "manifest.json")))["quirk_path5"]
+    orc = Oracle()
+    text = dmx.corpus("text", q["text_len"], offset=q["text_offset"])
+    s1, sec, b = Q.path5_stream(text)
+    s = Q.finish_path5(s1, sec, b, orc.inflate(s1 + sec + b"\x03\x00"))
+    assert len(s) == q["stream_len"] and hashlib.sha256(s).hexdigest() == q["stream_sha256"]
+    out = orc.inflate(s)
+    assert len(out) == q["out_len"] and hashlib.sha256(out).hexdigest() == q["out_sha256"]

@@ -9,7 +9,7 @@ import torch  # noqa: E402
 import dmx  # noqa: E402
 ctx = dmx.Context(segment_bytes=int(os.environ.get("DMX_SEG", "32768")))
 ctx.set_timing(True)
-n = 256 << 20
+n = int(os.environ.get("DMX_MIB", "256")) << 20
 for kind in os.environ.get("DMX_KINDS", "repeat,text,zeros").split(","):
     host = torch.empty(n, dtype=torch.uint8).pin_memory()
     dmx.corpus_into(kind, n, host.data_ptr())
