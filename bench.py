@@ -4,9 +4,14 @@
 Metric (BASELINE.json): "GB/s deflate+inflate on 1 GiB buffer at 1/2/4/8 MI355X; ratio vs
 reference".  One step = deflate of a 1 GiB device-resident shard per GPU (level 2, the
 reference's "fast" level, configs[1]: 1 GiB zero/repeat synthetic buffer) followed by
-inflate of the produced stream back into HBM; with N > 1 GPUs the compressed shards are also
-gathered to rank 0 over RCCL (the north_star's "final bitstream gather").  value = total
-uncompressed bytes of all ranks / max-over-ranks step time.
+inflate of the produced stream back into HBM.  With N > 1 GPUs a step is the
+distributed round trip of ONE stream: every rank compresses its shard in sub-shards whose
+bytes travel to rank 0 over RCCL while the next sub-shard compresses (the north_star's "final
+bitstream gather", shard.deflate_gather); rank 0 indexes the gathered stream's segment starts,
+proves the cut candidates (dmx_segment_check_device) and scatters one piece per rank; every
+rank inflates its piece (pieces after the first in piece mode), and the decoded bytes stay
+where they were decoded (shard.scatter_inflate, gather=False).  value = total uncompressed
+bytes of all ranks / max-over-ranks step time.
 
   python bench.py                          # N=1, defaults (+ the per-config sub-records)
   torchrun --nproc-per-node N bench.py --gpus N [--strong]
@@ -68,6 +73,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip the per-config sub-records")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--sub", type=int, default=4, help="N > 1: sub-shards per rank in the pipelined gather")
     return p.parse_args()
 
 
@@ -143,7 +149,13 @@ class Runner:
         self.bound = dmx.deflate_bound(n) + 64
         self.d_in = torch.empty(n + 64, dtype=torch.uint8, device=dev)
         self.d_comp = torch.empty(self.bound, dtype=torch.uint8, device=dev)
-        self.d_out = torch.empty(n + 64, dtype=torch.uint8, device=dev)
+        self.out_cap = n + 64
+        self.d_out = torch.empty(self.out_cap, dtype=torch.uint8, device=dev)
+
+    def grow_out(self, cap):
+        """N > 1: a rank decodes a piece of the whole stream, whose size follows the cuts."""
+        self.out_cap = cap
+        self.d_out = self.torch.empty(cap, dtype=self.torch.uint8, device=self.dev)
 
     def load(self, kind, offset):
         torch = self.torch
@@ -175,6 +187,74 @@ class Runner:
 
     def verify(self, olen):
         return olen == self.n and bool(self.torch.equal(self.d_out[: self.n], self.d_in[: self.n]))
+
+
+class _NoEvent:
+    """Stand-in for torch.cuda.Event on a CPU device (the gloo tests of dist_step)."""
+
+    def record(self, *a):
+        pass
+
+    def elapsed_time(self, other):
+        return 0.0
+
+
+def dist_step(torch, ctx, dev, run, level, gathered, sub, stream):
+    """One distributed round trip (N > 1, see the module doc); returns (events, stream bytes,
+    this rank's decoded bytes, ok of the split)."""
+    import torch.distributed as dist
+    rank = dist.get_rank()
+    ev = [torch.cuda.Event(enable_timing=True) if dev.type == "cuda" else _NoEvent() for _ in range(3)]
+    ev[0].record(stream)
+    total, _ = shard.deflate_gather(ctx, run.d_in, run.n, level, out=gathered, sub=sub)
+    ev[1].record(stream)
+    # the packed stream and the pieces are written by torch copies: the codec runs on torch's
+    # stream so it reads them after those copies
+    sh = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else None
+    starts, check = None, None
+    if rank == 0:
+        starts = ctx.segment_starts_device(gathered.data_ptr(), total, stream=sh)
+        check = lambda c: ctx.segment_check_device(gathered.data_ptr(), total, c, stream=sh)  # noqa: E731
+    got = [0]
+
+    def decode(piece, first):
+        fn = ctx.inflate_device if first else ctx.inflate_piece_device
+        olen = fn(piece.data_ptr(), piece.numel(), run.d_out.data_ptr(), run.out_cap, stream=sh)
+        got[0] = olen
+        return run.d_out[:olen]
+
+    src = gathered if rank == 0 else torch.empty(0, dtype=torch.uint8, device=dev)
+    _, ok = shard.scatter_inflate(src, total if rank == 0 else 0, decode, starts=starts,
+                                  out=run.d_out if rank == 0 else None, check=check, gather=False,
+                                  balance="count")
+    ev[2].record(stream)
+    return ev, total, got[0], ok
+
+
+def dist_verify(torch, dist, run, corpus, olen, ok, dev, total_n):
+    """Each rank's decoded piece against the corpus bytes at its output offset (outside the
+    timed region); a fallen-back split is checked whole on rank 0."""
+    rank = dist.get_rank()
+    # a fallen-back split decoded the whole stream on rank 0 (the other ranks' pieces are moot)
+    sizes = shard.gather_sizes(olen if (ok or rank == 0) else 0, dev)
+    off = sum(sizes[:rank])
+    good = True
+    m = sizes[rank]
+    if sum(sizes) != total_n:
+        good = False
+    step = 256 << 20
+    host = torch.empty(min(step, max(m, 1)), dtype=torch.uint8)
+    if dev.type == "cuda":
+        host = host.pin_memory()
+    for b in range(0, m, step):
+        k = min(step, m - b)
+        dmx.corpus_into(corpus, k, host.data_ptr(), offset=off + b)
+        if not torch.equal(run.d_out[b:b + k], host[:k].to(dev)):
+            good = False
+            break
+    t = torch.tensor([1 if good else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
 
 
 def summarize(recs, n):
@@ -282,36 +362,52 @@ def main():
     run = Runner(torch, ctx, dev, n, stream)
     run.load(a.corpus, offset)
     last = rank == world - 1
-    gathered = None
-    if world > 1 and rank == 0:
-        gathered = torch.empty(world * run.bound, dtype=torch.uint8, device=dev)
-    gather = (lambda buf, clen: shard.gather_stream(buf, clen, gathered)) if world > 1 else None
-
-    for _ in range(a.warmup):
-        run.step(a.level, not_final=not last, gather=gather)
-    # correctness of the round trip (outside the timed region)
-    _, clen, olen, _, _ = run.step(a.level, not_final=not last, gather=gather)
-    ok = run.verify(olen)
-
-    recs = []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        recs.append(run.step(a.level, not_final=not last, gather=gather))
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
     total_bytes = a.bytes if a.strong else world * n
-    if world > 1:
+    recs = []
+    split_ok = True
+    if world == 1:
+        for _ in range(a.warmup):
+            run.step(a.level)
+        # correctness of the round trip (outside the timed region)
+        _, clen, olen, _, _ = run.step(a.level)
+        ok = run.verify(olen)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            recs.append(run.step(a.level))
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+    else:
+        # the whole stream lands on rank 0; every rank's decoded piece is sized by the cuts
+        gathered = torch.empty(world * run.bound + 64, dtype=torch.uint8, device=dev) if rank == 0 else None
+        run.grow_out(total_bytes + 64 if rank == 0 else 2 * max(n, 1) + (64 << 20))
+        for _ in range(a.warmup):
+            dist_step(torch, ctx, dev, run, a.level, gathered, a.sub, stream)
+        _, _, olen, split_ok = dist_step(torch, ctx, dev, run, a.level, gathered, a.sub, stream)
+        torch.cuda.synchronize(dev)
+        ok = dist_verify(torch, dist, run, a.corpus, olen, split_ok, dev, total_bytes)
+        dist_recs = []
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            dist_recs.append(dist_step(torch, ctx, dev, run, a.level, gathered, a.sub, stream))
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        elapsed = time.perf_counter() - t0
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = bool(okt.item())
+        split_ok = all(r[3] for r in dist_recs)
+        t_dg = sum(r[0][0].elapsed_time(r[0][1]) for r in dist_recs) / len(dist_recs)
+        t_si = sum(r[0][1].elapsed_time(r[0][2]) for r in dist_recs) / len(dist_recs)
+        # kernel times and the roofline: this rank's shard as one local round trip, after the
+        # timed region (the distributed step launches per sub-shard and per piece)
+        run.grow_out(n + 64)
+        for _ in range(2):
+            run.step(a.level)
+        recs = [run.step(a.level) for _ in range(3)]
+        torch.cuda.synchronize(dev)
 
     # practical HBM ceiling: a device-to-device copy of the shard, after the timed
     # region, on torch's current stream where its events are recorded; bytes = N read + N written
@@ -378,6 +474,17 @@ def main():
                          "d2d_copy_GBps": round(d2d_gbps, 1)},
             "cpu_baseline": None,
         }
+        if world > 1:
+            res.update({
+                "deflate_GBps": round(total_bytes / (t_dg * 1e-3) / 1e9, 4),
+                "inflate_GBps": round(total_bytes / (t_si * 1e-3) / 1e9, 4),
+                "gather_ms": None,
+                "distributed": {"deflate_gather_ms": round(t_dg, 4), "scatter_inflate_ms": round(t_si, 4),
+                                "sub_shards": a.sub, "split_ok": split_ok,
+                                "note": "one stream: sub-shard deflate with the gather to rank 0 pipelined "
+                                        "behind it (RCCL P2P), proven cuts, piece-mode inflate on every rank; "
+                                        "decoded bytes stay on the rank that decoded them; kernel_ms / roofline "
+                                        "from a local round trip of rank 0's shard after the timed region"}})
     if world == 1 and not a.no_extras:
         # sub-records (outside the timed region): the other corpora, C3 and C5
         extras = {}

@@ -158,14 +158,22 @@ FINAL_EMPTY = (0x03, 0x00)  # an empty final fixed-Huffman block: closes a NOT_F
 CHECK_NEAREST = 8           # candidates tried per cut, nearest to its target first
 
 
-def split_points(starts, total, world, valid=None):
+def _target(starts, total, world, r, balance):
+    """Where cut r aims: r / world of the stream's bytes, or (balance == "count") the start of
+    the (r / world)-th candidate segment -- equal output for libdmx's equal-size segments."""
+    if balance == "count" and starts:
+        return starts[min(len(starts) - 1, r * len(starts) // world)]
+    return r * total // world
+
+
+def split_points(starts, total, world, valid=None, balance="bytes"):
     """Piece boundaries [0, c_1, ..., c_{world-1}, total]: c_r is the candidate segment start
-    nearest r * total / world among those valid(start) accepts (boundaries strictly increase;
+    nearest its target (_target) among those valid(start) accepts (boundaries strictly increase;
     a rank may get an empty piece)."""
     import bisect
     cuts = [0]
     for r in range(1, world):
-        target = r * total // world
+        target = _target(starts, total, world, r, balance)
         i = bisect.bisect_left(starts, target)
         order = sorted((j for j in range(max(0, i - CHECK_NEAREST), min(len(starts), i + CHECK_NEAREST))),
                        key=lambda j: (abs(starts[j] - target), starts[j]))
@@ -180,16 +188,16 @@ def split_points(starts, total, world, valid=None):
     return cuts
 
 
-def pick_cuts(starts, total, world, check=None):
+def pick_cuts(starts, total, world, check=None, balance="bytes"):
     """split_points with the candidates near each target proven first by check(list of starts)
     -> list of end bytes (None: the segment does not decode) -- one batched call."""
     import bisect
     starts = sorted(starts)
     if check is None:
-        return split_points(starts, total, world)
+        return split_points(starts, total, world, balance=balance)
     near = set()
     for r in range(1, world):
-        i = bisect.bisect_left(starts, r * total // world)
+        i = bisect.bisect_left(starts, _target(starts, total, world, r, balance))
         near.update(starts[max(0, i - CHECK_NEAREST): i + CHECK_NEAREST])
     near = sorted(s for s in near if 0 < s < total)
     ends = check(near) if near else []
@@ -197,10 +205,10 @@ def pick_cuts(starts, total, world, check=None):
     # (its BFINAL block): a garbage start that stops early on some lenient block never does
     known = set(starts)
     ok = {s for s, e in zip(near, ends) if e is not None and s < e and (e in known or e == total)}
-    return split_points(starts, total, world, valid=lambda s: s in ok)
+    return split_points(starts, total, world, valid=lambda s: s in ok, balance=balance)
 
 
-def scatter_inflate(stream, clen, decode, starts=None, out=None, check=None, gather=True):
+def scatter_inflate(stream, clen, decode, starts=None, out=None, check=None, gather=True, balance="bytes"):
     """Inflate one stream held by rank 0 (stream[:clen]) on all ranks.
 
     decode(piece, first) -> 1-D uint8 tensor of decoded bytes, raising on a decode error; first
@@ -213,14 +221,15 @@ def scatter_inflate(stream, clen, decode, starts=None, out=None, check=None, gat
     depends on the split.  A stream that does not decode at all, or an out that is too small,
     raises on every rank.  gather=False leaves every rank's decoded piece where it was decoded
     (decode's own buffer; bench.py at N > 1): no byte goes back to rank 0 and out is unused
-    except for the whole-stream fallback.
+    except for the whole-stream fallback.  balance: cut targets by stream bytes, or by
+    candidate count ("count": equal output for libdmx's equal-size segments).
     """
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = stream.device
     cut = torch.zeros(world + 1, dtype=torch.int64, device=dev)
     if rank == 0:
         try:
-            cut.copy_(torch.tensor(pick_cuts(starts or [], clen, world, check), dtype=torch.int64))
+            cut.copy_(torch.tensor(pick_cuts(starts or [], clen, world, check, balance), dtype=torch.int64))
         except Exception:  # no split (rank 0 alone decodes) rather than a rank left in the collective
             cut.copy_(torch.tensor([0] + [clen] * world, dtype=torch.int64))
     dist.broadcast(cut, 0)

@@ -322,3 +322,67 @@ def test_split_points():
     assert shard.split_points([], 100, 3) == [0, 0, 0, 100]
     c = shard.split_points(starts, 100, 8)
     assert c[0] == 0 and c[-1] == 100 and all(a <= b for a, b in zip(c, c[1:]))
+
+
+class _HostCodec(_HostDeflate):
+    """CPU stand-in for the dmx.Context entry points bench.dist_step calls, on host pointers:
+    stored-segment deflate, the oracle as inflate (piece mode for pieces), a byte search for the
+    segment starts and the oracle for the cut check."""
+
+    def __init__(self):
+        from oracle_bind import Oracle
+        self.orc = Oracle()
+
+    def _inflate(self, d_in, n, d_out, cap, piece):
+        import ctypes
+        out = self.orc.inflate(ctypes.string_at(d_in, n), piece=piece)
+        if len(out) > cap:
+            raise RuntimeError("capacity")
+        ctypes.memmove(d_out, out, len(out))
+        return len(out)
+
+    def inflate_device(self, d_in, n, d_out, cap, stream=None):
+        return self._inflate(d_in, n, d_out, cap, False)
+
+    def inflate_piece_device(self, d_in, n, d_out, cap, stream=None):
+        return self._inflate(d_in, n, d_out, cap, True)
+
+    def segment_starts_device(self, d_in, n, stream=None):
+        import ctypes
+        return _markers(ctypes.string_at(d_in, n))
+
+    def segment_check_device(self, d_in, n, starts, stream=None):
+        import ctypes
+        return _oracle_check(self.orc, ctypes.string_at(d_in, n))(starts)
+
+
+def _bench_worker(rank, world, port, per, sub, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import dmx
+    dev = torch.device("cpu")
+    run = bench.Runner(torch, _HostCodec(), dev, per, None)
+    run.d_in[:per].copy_(torch.frombuffer(bytearray(dmx.corpus("mixed", per, offset=rank * per)), dtype=torch.uint8))
+    total_n = world * per
+    gathered = torch.empty(world * run.bound + 64, dtype=torch.uint8) if rank == 0 else None
+    run.grow_out(total_n + 64 if rank == 0 else 2 * per + 4096)
+    _, clen, olen, ok = bench.dist_step(torch, run.ctx, dev, run, 0, gathered, sub, None)
+    good = bench.dist_verify(torch, dist, run, "mixed", olen, ok, dev, total_n)
+    q.put((rank, (clen, olen, ok, good)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_distributed_step(world):
+    """bench.py's N > 1 step on gloo with host stand-ins for the GPU codec: pipelined deflate +
+    gather of one stream, proven cuts, piece-mode inflate on every rank; the decoded pieces
+    together are the whole input (dist_verify), and the split held (ok)."""
+    per = 7 * SEG + 1000
+    res = _run(_bench_worker, world, per, 3, all_ranks=True)
+    assert all(v[3] for v in res.values()), res
+    assert all(v[2] for v in res.values()), res
+    assert sum(v[1] for v in res.values()) == world * per
