@@ -1184,6 +1184,72 @@ struct ChunkReader {
     }
 };
 
+// A writer thread takes the compressed chunks in order: chunk k's D2H into pinned buffer
+// k % 2 was recorded on an event by the producer; the writer waits for the event and writes
+// the bytes, then frees the buffer for chunk k + 2.  The producer meanwhile compresses the
+// next chunk, so the D2H and the file write of chunk k overlap the compression of k + 1.
+struct ChunkWriter {
+    FILE* f;
+    uint8_t* buf[2];
+    hipEvent_t ev[2];
+    size_t len[2] = {0, 0};
+    bool full[2] = {false, false};
+    bool failed = false, stop = false;
+    size_t next = 0, queued = 0;  // next chunk to write, chunks handed over
+    std::mutex m;
+    std::condition_variable cv;
+    std::thread th;
+    ChunkWriter(FILE* f_, uint8_t* b0, uint8_t* b1, hipEvent_t e0, hipEvent_t e1)
+        : f(f_), buf{b0, b1}, ev{e0, e1} {
+        th = std::thread([this] { run(); });
+    }
+    ~ChunkWriter() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            stop = true;
+        }
+        cv.notify_all();
+        th.join();
+    }
+    void run() {
+        for (;;) {
+            size_t k, n;
+            {
+                std::unique_lock<std::mutex> g(m);
+                cv.wait(g, [&] { return full[next & 1] || stop; });
+                if (!full[next & 1]) return;  // stop with nothing queued
+                k = next;
+                n = len[k & 1];
+            }
+            bool ok = hipEventSynchronize(ev[k & 1]) == hipSuccess;
+            ok = ok && (n == 0 || std::fwrite(buf[k & 1], 1, n, f) == n);
+            std::lock_guard<std::mutex> g(m);
+            if (!ok) failed = true;
+            full[k & 1] = false;
+            next++;
+            cv.notify_all();
+        }
+    }
+    // waits until buffer k % 2 is free (chunk k - 2 written); false after a write error
+    bool acquire(size_t k) {
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [&] { return !full[k & 1] || failed; });
+        return !failed;
+    }
+    void hand_over(size_t k, size_t n) {
+        std::lock_guard<std::mutex> g(m);
+        len[k & 1] = n;
+        full[k & 1] = true;
+        queued = k + 1;
+        cv.notify_all();
+    }
+    bool drain() {  // all handed-over chunks written
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [&] { return next == queued || failed; });
+        return !failed;
+    }
+};
+
 int64_t file_size(FILE* f) {
     if (std::fseek(f, 0, SEEK_END) != 0) return -1;
     const long long n = ftello(f);
@@ -1211,28 +1277,33 @@ int dmx_deflate_file(dmx_ctx* c, const char* in_path, const char* out_path, int 
     if (!dg.ok) return DMX_ERR_DEVICE;
     const size_t K = kFileChunk;
     const size_t bound = dmx_deflate_bound(K);
-    Pinned hin0(K), hin1(K), hout(bound);
-    DevBuf din[2], dout;
-    if (!hin0.p || !hin1.p || !hout.p || !din[0].ensure(K) || !din[1].ensure(K) || !dout.ensure(bound)) {
+    Pinned hin0(K), hin1(K), hout0(bound), hout1(bound);
+    DevBuf din[2], dout[2];
+    auto release_all = [&] {
         for (auto& d : din) d.release();
-        dout.release();
+        for (auto& d : dout) d.release();
+    };
+    if (!hin0.p || !hin1.p || !hout0.p || !hout1.p || !din[0].ensure(K) || !din[1].ensure(K) ||
+        !dout[0].ensure(bound) || !dout[1].ensure(bound)) {
+        release_all();
         return DMX_ERR_NOMEM;
     }
     hipStream_t cs = nullptr;
-    hipEvent_t ev[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr}, evo[2] = {nullptr, nullptr};
     int rc = DMX_OK;
     if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) rc = DMX_ERR_DEVICE;
-    for (auto& e : ev)
-        if (rc == DMX_OK && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = DMX_ERR_DEVICE;
+    for (auto* e : {&ev[0], &ev[1], &evo[0], &evo[1]})
+        if (rc == DMX_OK && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) rc = DMX_ERR_DEVICE;
     size_t written = 0;
     if (rc == DMX_OK && N == 0) {  // empty file: one empty final block, as dmx_deflate
         size_t len = 0;
-        rc = deflate_device_locked(c, nullptr, 0, level, 0, dout.as<uint8_t>(), bound, &len, c->stream);
-        if (rc == DMX_OK && hipMemcpy(hout.p, dout.p, len, hipMemcpyDeviceToHost) != hipSuccess) rc = DMX_ERR_DEVICE;
-        if (rc == DMX_OK && std::fwrite(hout.p, 1, len, fo.f) != len) rc = DMX_ERR_ARG;
+        rc = deflate_device_locked(c, nullptr, 0, level, 0, dout[0].as<uint8_t>(), bound, &len, c->stream);
+        if (rc == DMX_OK && hipMemcpy(hout0.p, dout[0].p, len, hipMemcpyDeviceToHost) != hipSuccess) rc = DMX_ERR_DEVICE;
+        if (rc == DMX_OK && std::fwrite(hout0.p, 1, len, fo.f) != len) rc = DMX_ERR_ARG;
         written = len;
     } else if (rc == DMX_OK) {
         ChunkReader rd(fi.f, (size_t)N, K, hin0.u8(), hin1.u8());
+        ChunkWriter wr(fo.f, hout0.u8(), hout1.u8(), evo[0], evo[1]);
         const size_t nch = rd.nchunks;
         // copy chunk k + 1 in on the copy stream while chunk k compresses on the context stream
         auto h2d = [&](size_t k) -> int {
@@ -1249,22 +1320,26 @@ int dmx_deflate_file(dmx_ctx* c, const char* in_path, const char* out_path, int 
             if (hipStreamWaitEvent(c->stream, ev[k & 1], 0) != hipSuccess) { rc = DMX_ERR_DEVICE; break; }
             const size_t n = std::min(K, (size_t)N - k * K);
             size_t len = 0;
+            // output buffers k % 2 are free once chunk k - 2 is written (its D2H is done then)
+            if (!wr.acquire(k)) { rc = DMX_ERR_ARG; break; }
             rc = deflate_device_locked(c, din[k & 1].as<uint8_t>(), n, level, k + 1 < nch ? DMX_DEFLATE_NOT_FINAL : 0,
-                                       dout.as<uint8_t>(), bound, &len, c->stream);
+                                       dout[k & 1].as<uint8_t>(), bound, &len, c->stream);
             if (rc != DMX_OK) break;
             rd.release(k);  // the H2D of chunk k is complete (the deflate waited for it)
-            if (hipMemcpyAsync(hout.p, dout.p, len, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-                hipStreamSynchronize(c->stream) != hipSuccess) { rc = DMX_ERR_DEVICE; break; }
-            if (std::fwrite(hout.p, 1, len, fo.f) != len) { rc = DMX_ERR_ARG; break; }
+            // D2H on the copy stream (after the deflate, which synchronized), written by the
+            // writer thread while chunk k + 1 compresses
+            if ((len && hipMemcpyAsync(k & 1 ? hout1.p : hout0.p, dout[k & 1].p, len, hipMemcpyDeviceToHost, cs) != hipSuccess) ||
+                hipEventRecord(evo[k & 1], cs) != hipSuccess) { rc = DMX_ERR_DEVICE; break; }
+            wr.hand_over(k, len);
             written += len;
         }
+        if (!wr.drain() && rc == DMX_OK) rc = DMX_ERR_ARG;
         (void)hipStreamSynchronize(cs);
     }
-    for (auto& e : ev)
+    for (auto* e : {ev[0], ev[1], evo[0], evo[1]})
         if (e) (void)hipEventDestroy(e);
     if (cs) (void)hipStreamDestroy(cs);
-    for (auto& d : din) d.release();
-    dout.release();
+    release_all();
     if (in_bytes) *in_bytes = (size_t)N;
     if (out_bytes) *out_bytes = written;
     return rc;

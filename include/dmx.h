@@ -85,13 +85,16 @@ void dmx_free(void* p);
 
 /* Replaces deflate::compress(std::string, std::string, int)      deflate.hpp:755-777
  *          inflate::decompress(std::string, std::string)          inflate.hpp:390-408
- * Streaming file I/O: 64 MiB chunks through two pinned buffers; a reader thread overlaps the
- * disk reads with the H2D copies, and (deflate) the H2D of chunk k + 1 with the compression of
- * chunk k (each chunk a NOT_FINAL shard, the last one final; the concatenation is one stream).
- * Inflate streams the compressed file into HBM, decodes it as one stream, and overlaps the
- * D2H of each output chunk with the file write of the previous one.  Unlike the reference
- * (correct only for files <= 32 KiB, SURVEY A-8) any size works.  Sizes are reported through
- * the optional out-parameters. */
+ * Streaming file I/O in 64 MiB chunks.  Deflate: a reader thread fills two pinned buffers,
+ * the H2D of chunk k + 1 and the D2H + file write of chunk k - 1 (a writer thread) overlap the
+ * compression of chunk k; each chunk is a NOT_FINAL shard, the last one final, so the file is
+ * one stream; device memory is bounded (2 x 64 MiB in, 2 x bound out).  Inflate: the
+ * compressed file streams into HBM (disk reads overlapping the H2D copies), decodes as one
+ * stream, and the D2H of each output chunk overlaps the file write of the previous one; it
+ * holds the whole compressed file and the whole output in HBM (plus the decoder's scratch),
+ * so files beyond the device's memory are not supported.  Unlike the reference (correct only
+ * for files <= 32 KiB, SURVEY A-8) any size that fits works.  Sizes are reported through the
+ * optional out-parameters. */
 int dmx_deflate_file(dmx_ctx* ctx, const char* in_path, const char* out_path, int level,
                      size_t* in_bytes, size_t* out_bytes);
 int dmx_inflate_file(dmx_ctx* ctx, const char* in_path, const char* out_path, size_t* out_bytes);
