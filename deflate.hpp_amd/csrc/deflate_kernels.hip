@@ -58,6 +58,10 @@ constexpr int DF_DIST_MAXBITS = DMX_DIST_MAXBITS;
 #define DMX_L3_DEPTH 16
 #endif
 constexpr int DF_L3_DEPTH = DMX_L3_DEPTH;  // level 3: candidate-chain links searched per position
+#ifndef DMX_L3_LONG
+#define DMX_L3_LONG 16
+#endif
+constexpr uint32_t DF_L3_LONG = DMX_L3_LONG;  // level 3: a first link this long ends the chain search
 #ifndef DMX_L3_ROUND
 #define DMX_L3_ROUND 128
 #endif
@@ -1110,17 +1114,28 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                 if (d0) {
                     const uint32_t hi = min(p / DF_CHUNK * DF_CHUNK + DF_CHUNK, nb);
                     const uint32_t maxl = min(258u, hi - p);
-                    uint32_t bl = 2, q = p - d0;
-                    for (int hop = 0; hop < DF_L3_DEPTH; hop++) {
+                    // The first link: its length up to DF_L3_LONG bytes; a first link that long
+                    // ends the search (periodic data, an image row: every link is that long,
+                    // and the parse measures the chosen one in full).  Then a link can only be
+                    // longer if the 4 bytes ending at offset bl match as well (zlib's scan_end
+                    // test, widened): one word compare per link, the full length only for the
+                    // links that pass.
+                    uint32_t q = p - d0;
+                    uint32_t bl = matchlen(S.data32, p, q, min(maxl, DF_L3_LONG));
+                    if (bl >= 3) bd = d0;
+                    else bl = 2;  // (a fingerprint collision: no match yet)
+                    uint32_t tail = bl >= 3 ? ld32u(S.data32, p + bl - 3) : 0u;
+                    for (int hop = 1; hop < DF_L3_DEPTH && bl < maxl && bl < DF_L3_LONG; hop++) {
+                        const uint32_t dq = S.cand[q];
+                        if (!dq) break;
+                        q -= dq;
+                        if (bl >= 3 && ld32u(S.data32, q + bl - 3) != tail) continue;
                         const uint32_t L = matchlen(S.data32, p, q, maxl);
                         if (L > bl) {
                             bl = L;
                             bd = p - q;
-                            if (L >= maxl) break;
+                            tail = ld32u(S.data32, p + bl - 3);
                         }
-                        const uint32_t dq = S.cand[q];
-                        if (!dq) break;
-                        q -= dq;
                     }
                 }
                 if (k & 1) best[k / 2] |= bd << 16;
