@@ -53,6 +53,19 @@ REF_NOTES = {"text": "reference L2 stream is lossy (SURVEY A-1)",
              "mixed": "reference L2 stream is invalid (SURVEY A-3)",
              "bmp": "reference L2 stream is invalid (SURVEY A-3)"}
 REF_RATIO_L3_TEXT = 2.5741  # reference L3 on the 1 MiB text prefix
+PROFILE_TAG = "r03"  # tools/profile_all.sh writes profiles/<tag>_kstats_*.csv and traffic.json
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def traffic_of(key_prefix, kernels):
+    """HBM bytes per launch from profiles/traffic.json (tools/profile_all.sh) for each kernel
+    that has an entry under key_prefix + kernel; None when none has."""
+    try:
+        tj = json.load(open(TRAFFIC_JSON))
+    except Exception:
+        return None
+    got = {k: tj[key_prefix + k] for k in kernels if key_prefix + k in tj}
+    return got or None
 
 
 def parse():
@@ -296,6 +309,7 @@ def corpus_record(run, kind, level, steps):
     run.torch.cuda.synchronize(run.dev)
     s = summarize(recs, run.n)
     n = run.n
+    inf_k = ["k_inflate_lanes", "k_inflate_resolve", "k_inflate_pj_list"]
     return {"bytes": n, "level": level, "roundtrip_ok": ok,
             "roundtrip_GBps": round(n / ((s["t_def"] + s["t_inf"]) * 1e-3) / 1e9, 3),
             "deflate_GBps": round(n / (s["t_def"] * 1e-3) / 1e9, 3),
@@ -307,7 +321,11 @@ def corpus_record(run, kind, level, steps):
             "kernel_ms": {"k_deflate_segments": round(s["k_def"], 4),
                           INF_KERNEL.get(s["path"], "k_inflate_segments"): round(s["k_inf"], 4)},
             "inflate_path": s["path"],
-            "roofline_frac": {"deflate": round(s["frac_def"], 5), "inflate": round(s["frac_inf"], 5)}}
+            "alg_bytes": s["alg"],
+            "roofline_frac": {"deflate": round(s["frac_def"], 5), "inflate": round(s["frac_inf"], 5)},
+            "traffic": {"deflate": traffic_of(f"{kind}:{n}:{level}:", ["k_deflate_segments"]),
+                        "inflate": traffic_of(f"{kind}:{n}:{level}:", inf_k)},
+            "profile": f"profiles/{PROFILE_TAG}_kstats_{kind}_L{level}.csv"}
 
 
 def c3_record(torch, ctx, dev, stream):
@@ -336,6 +354,9 @@ def c3_record(torch, ctx, dev, stream):
                      "inflate_GBps": round(C3_N / (med * 1e-3) / 1e9, 3), "path": int(ctx.stats().path),
                      "roofline_frac": round((C3_N + len(st)) / (med * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
                      "bit_exact": ok}
+    res["zlib1"]["traffic"] = traffic_of("c3_zlib1:", ["k_fb_scan", "k_fb_compact", "k_fb_decode", "k_fb_replay",
+                                                       "k_fb_tails", "k_fb_final"])
+    res["zlib1"]["profile"] = f"profiles/{PROFILE_TAG}_kstats_c3_zlib1.csv"
     return res
 
 

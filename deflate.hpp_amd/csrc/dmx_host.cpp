@@ -68,7 +68,7 @@ struct dmx_ctx {
     int ncu = 0;                         // compute units (mode 6 grid)
     // block-parallel path (path 5): scan counts / hits / offsets, hit list, unit starts, token
     // offsets and words, unit records, chain (unit index, offset, size), 16-bit image
-    DevBuf fbc, fbh, fbo, fbl, fbs, fbt, fbk, fbu, fbch, fbco, fbcs, fbimg, fbstop;
+    DevBuf fbc, fbh, fbo, fbl, fbs, fbt, fbk, fbu, fbch, fbco, fbcs, fbimg, fbstop, fbwin, fbopen;
     DevBuf ck;  // checksum scratch (checksum.hip) + the 4-byte result at its start
     bool timing = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -233,6 +233,15 @@ int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, 
 // stream to the serial decoder (no chain from bit 0 to a BFINAL block, a unit that errors or
 // runs out of token space, a copy from before the stream start): results and error codes are
 // then the serial decoder's, i.e. the reference's.
+// DMX_FB_SERIAL=1: path 5 decodes every unit with one wavefront (A/B reference for k_fb_pdecode)
+static bool fb_serial_only() {
+    static const bool v = [] {
+        const char* e = std::getenv("DMX_FB_SERIAL");
+        return e && *e == '1';
+    }();
+    return v;
+}
+
 int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_out, size_t cap,
                       size_t* total_out, uint8_t** dev_out, hipStream_t st, bool* handled, uint32_t iflags) {
     *handled = false;
@@ -272,8 +281,9 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     const uint64_t nbits = 8ull * n;
     // a unit stops after passing the next strong start (or on landing on any start): stops[k];
     // token words: at most one per bit up to where it can stop, plus room for the block that
-    // crosses that start; a weak unit (a stored block, usually) gets its span to the next start
-    // and slack for a short block behind it.  16-B groups.
+    // crosses that start; a weak unit (a stored block -- two words -- then possibly fixed-code
+    // blocks up to the next dynamic one) gets 64 Ki words, and overflowing them sends the
+    // stream to the serial decoder.  16-B groups.
     std::vector<uint64_t> stops(K), tokoff(K + 1);
     uint64_t next_strong = ~0ull >> 1;  // no strong start after: never stop on passing one
     for (uint64_t k = K; k-- > 0;) {
@@ -282,9 +292,8 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     }
     tokoff[0] = 0;
     for (uint64_t k = 0; k < K; k++) {
-        const uint64_t reach = strong[k] ? std::min<uint64_t>(stops[k], nbits) : (k + 1 < K ? starts[k + 1] : nbits);
         // (a strong unit's stop has bit 63 clear: std::min, not the host min(int, int))
-        const uint64_t words = (reach - starts[k]) + 4096 + (strong[k] ? 0u : 16384u);
+        const uint64_t words = strong[k] ? std::min<uint64_t>(stops[k], nbits) - starts[k] + 4096 : 4096 + 65536;
         tokoff[k + 1] = tokoff[k] + ((words + 63) & ~63ull);
     }
     if (!c->fbs.ensure(K * 8) || !c->fbt.ensure((K + 1) * 8) || !c->fbk.ensure(tokoff[K] * 4) ||
@@ -293,8 +302,27 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     HIPCHK(hipMemcpyAsync(c->fbs.p, starts.data(), K * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(c->fbstop.p, stops.data(), K * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(c->fbt.p, tokoff.data(), (K + 1) * 8, hipMemcpyHostToDevice, st));
+    static const bool fb_debug = [] {  // developer aid: unit outcomes, chain breaks
+        const char* e = std::getenv("DMX_FB_DEBUG");
+        return e && *e;
+    }();
+    uint32_t* dstats = nullptr;
+    if (fb_debug && c->fbopen.ensure(64)) {
+        dstats = c->fbopen.as<uint32_t>();
+        HIPCHK(hipMemsetAsync(dstats, 0, 40, st));
+    }
     HIPCHK(launch_fb_decode(words, misalign, n, c->fbs.as<uint64_t>(), c->fbstop.as<uint64_t>(), K,
-                            c->fbt.as<uint64_t>(), c->fbk.as<uint32_t>(), c->fbu.as<FbUnit>(), c->flags | iflags, st));
+                            c->fbt.as<uint64_t>(), c->fbk.as<uint32_t>(), c->fbu.as<FbUnit>(), c->flags | iflags,
+                            !fb_serial_only(), dstats, st));
+    if (dstats) {
+        uint32_t hs[10];
+        HIPCHK(hipMemcpyAsync(hs, dstats, 40, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        std::fprintf(stderr, "dmx fb: %llu units: %u lane-parallel, %u serial, %u serial after a parallel block, %u weak; "
+                     "serial because: header %u, unsettled %u, no end of block %u, bad end %u, capacity %u, "
+                     "stream-start copy %u\n",
+                     (unsigned long long)K, hs[0], hs[1], hs[2], hs[3], hs[4], hs[5], hs[6], hs[7], hs[8], hs[9]);
+    }
     std::vector<FbUnit> units(K);
     HIPCHK(hipMemcpyAsync(units.data(), c->fbu.p, K * sizeof(FbUnit), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -302,16 +330,24 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     std::vector<uint32_t> chain;
     std::vector<uint64_t> coffs, csizes;
     uint64_t total = 0, k = 0;
+    auto chain_break = [&](const char* why, uint64_t k) {
+        if (fb_debug)
+            std::fprintf(stderr, "dmx fb: chain breaks at unit %llu of %llu (%s): start %llu end %llu size %llu flags %u strong %d\n",
+                         (unsigned long long)k, (unsigned long long)K, why, (unsigned long long)units[k].start,
+                         (unsigned long long)units[k].end, (unsigned long long)units[k].size, units[k].flags,
+                         (int)strong[k]);
+        return DMX_OK;
+    };
     for (;;) {
         const FbUnit& u = units[k];
-        if (u.flags & ~SEGF_FINAL) return DMX_OK;
+        if (u.flags & ~SEGF_FINAL) return chain_break("unit error", k);
         chain.push_back((uint32_t)k);
         coffs.push_back(total);
         csizes.push_back(u.size);
         total += u.size;
         if (u.flags & SEGF_FINAL) break;
         const auto it = std::lower_bound(starts.begin() + k + 1, starts.end(), u.end);
-        if (it == starts.end() || *it != u.end) return DMX_OK;  // chain leaves the unit starts
+        if (it == starts.end() || *it != u.end) return chain_break("end is no unit start", k);
         k = (uint64_t)(it - starts.begin());
     }
     // the path's own scratch first: when it does not fit, the stream still decodes on the
@@ -333,9 +369,17 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     HIPCHK(hipMemcpyAsync(c->fbco.p, coffs.data(), nch * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(c->fbcs.p, csizes.data(), nch * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(&ds->fb_err, 0, 4, st));
+    // the parallel window hand-off when its scratch fits (nch * 128 KiB), else the serial one
+    uint32_t *win = nullptr, *open = nullptr;
+    const uint64_t went = fb_window_entries(nch);
+    if (went && !fb_serial_only() && c->fbwin.ensure(went * 4) && c->fbopen.ensure(fb_window_rounds(nch) * 4)) {
+        win = c->fbwin.as<uint32_t>();
+        open = c->fbopen.as<uint32_t>();
+    }
     HIPCHK(launch_fb_resolve(d_in, c->fbs.as<uint64_t>(), c->fbch.as<uint32_t>(), c->fbco.as<uint64_t>(),
                              c->fbcs.as<uint64_t>(), nch, c->fbt.as<uint64_t>(), c->fbk.as<uint32_t>(),
-                             c->fbu.as<FbUnit>(), c->fbimg.as<uint16_t>(), total, out, &ds->fb_err, st));
+                             c->fbu.as<FbUnit>(), c->fbimg.as<uint16_t>(), total, out, &ds->fb_err, win, open,
+                             st));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     uint32_t ferr = 0;
     HIPCHK(hipMemcpyAsync(&ferr, &ds->fb_err, 4, hipMemcpyDeviceToHost, st));
@@ -776,7 +820,7 @@ void dmx_destroy(dmx_ctx* c) {
     for (DevBuf* b : {&c->in, &c->out, &c->slots, &c->sizes, &c->offs, &c->scal, &c->cands,
                       &c->tiles, &c->tileoffs, &c->recs, &c->status, &c->dbg, &c->ltok,
                       &c->ltokoff, &c->lntok, &c->lcaps, &c->lheavy, &c->rtmp, &c->rchain, &c->fbc, &c->fbh, &c->fbo, &c->fbl,
-                      &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg, &c->fbstop,
+                      &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg, &c->fbstop, &c->fbwin, &c->fbopen,
                       &c->ck})
         b->release();
     for (auto& e : c->ev)

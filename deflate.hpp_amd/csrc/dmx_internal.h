@@ -117,7 +117,7 @@ hipError_t launch_inflate_validate(const InflateArgs& A, ValidateWords* W, Infla
                                    hipStream_t st);
 
 // block-parallel inflate of arbitrary streams (inflate_blocks.hip, path 5)
-struct FbUnit {         // per-unit record written by k_fb_decode
+struct FbUnit {         // per-unit record written by k_fb_pdecode / k_fb_decode
     uint64_t start;     // stream bit of the unit's first block
     uint64_t end;       // stream bit just past its last block
     uint64_t size;      // output bytes
@@ -137,14 +137,18 @@ hipError_t launch_fb_compact(const uint32_t* counts, const uint64_t* offs, const
 hipError_t launch_fb_decode(const uint32_t* in_words, uint64_t misalign, uint64_t n,
                             const uint64_t* starts, const uint64_t* stops, uint64_t nunits,
                             const uint64_t* tokoff, uint32_t* tok, FbUnit* units, uint32_t flags,
-                            hipStream_t st);
-// replay + serial window hand-off + final resolve; *err (zeroed by the caller) becomes nonzero
-// when a copy reaches before the stream start
+                            bool parallel, uint32_t* stats, hipStream_t st);
+// replay + window hand-off + final resolve; *err (zeroed by the caller) becomes nonzero when a
+// copy reaches before the stream start.  win (fb_window_entries(nchain) words, 0 = not
+// available) and open (fb_window_rounds(nchain) words): the parallel hand-off; win == nullptr:
+// the serial one (k_fb_tails)
+uint64_t fb_window_entries(uint64_t nchain);
+uint32_t fb_window_rounds(uint64_t nchain);
 hipError_t launch_fb_resolve(const uint8_t* stream, const uint64_t* starts, const uint32_t* chain,
                              const uint64_t* offs, const uint64_t* sizes, uint64_t nchain,
                              const uint64_t* tokoff, const uint32_t* tok, const FbUnit* units,
                              uint16_t* img, uint64_t total, uint8_t* out, uint32_t* err,
-                             hipStream_t st);
+                             uint32_t* win, uint32_t* open, hipStream_t st);
 // checksums (checksum.hip): scratch of checksum_scratch_bytes(n) bytes; results land in device
 // memory (*d_out).  CRC-32: the zero-start register; crc32_finish applies start value and xor.
 uint64_t checksum_scratch_bytes(uint64_t n);

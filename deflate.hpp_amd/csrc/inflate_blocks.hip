@@ -39,10 +39,11 @@
 
 namespace dmx {
 
-constexpr uint32_t FB_SCAN_BITS = 32768;  // bit offsets tested per wavefront (4 KiB of stream)
+constexpr uint32_t FB_SCAN_BITS = 16384;  // bit offsets tested per wavefront (2 KiB of stream)
+constexpr uint32_t FB_STEP = 2048;        // offsets per prefilter step (32 per lane)
 constexpr uint32_t FB_STAGE_WORDS = FB_SCAN_BITS / 32 + 128;  // + 4096 bits of header lookahead
-constexpr uint32_t FB_HITS = 12;          // hits kept per scan chunk (stored headers in zero
-                                          // padding are found at several offsets)
+constexpr uint32_t FB_HITS = 48;          // hits kept per scan chunk (zlib at memLevel 1-2 writes
+                                          // blocks of a few hundred bytes)
 constexpr uint32_t FB_RING = 32768;       // replay window (entries of 16 bits)
 constexpr uint64_t FB_HIT_STORED = 1ull << 62;  // hit flag: a stored-block header
 constexpr uint32_t FB_GROUP_MAX = 8192;   // output entries per replay group (see k_fb_replay)
@@ -131,9 +132,38 @@ __device__ bool fb_check_lengths(const uint32_t* w, uint32_t p, uint64_t pl, uin
     return eob && kl == 32768 && (kd == 32768 || nd <= 1);
 }
 
+// One wavefront per FB_SCAN_BITS offsets, in three stages so that each test runs on full waves:
+//   0. prefilter, 32 offsets per lane at once with 64-bit word arithmetic on the staged bits:
+//      BTYPE 2, HLIT <= 29, HDIST <= 29 (~21 % of random offsets pass); byte-aligned offsets with
+//      BTYPE 0 get the stored-header test (LEN / NLEN = ~LEN, data inside the stream) directly;
+//   1. the survivors, queued in offset order, one per lane: a complete precode whose last sent
+//      length is nonzero (~0.5 % pass);
+//   2. those, queued again, one per lane: fb_check_lengths.
+// Hits come out in offset order; the chunk keeps its first FB_HITS.
+__device__ __forceinline__ bool fb_precode(uint32_t h, const uint32_t* stg, uint32_t q, uint64_t* pl_out) {
+    const uint32_t hclen = ((h >> 13) & 15) + 4;
+    const uint32_t x0 = fb_bits(stg, q + 17), x1 = fb_bits(stg, q + 49);
+    const uint64_t x = (uint64_t)x0 | ((uint64_t)x1 << 32);
+    uint64_t pl = 0;
+    uint32_t kr = 0, lastl = 0;
+    for (uint32_t i = 0; i < 19; i++) {
+        if (i < hclen) {
+            const uint32_t l = (uint32_t)(x >> (3 * i)) & 7;
+            pl |= (uint64_t)l << (3 * kPerm[i]);
+            kr += l ? 128u >> l : 0u;
+            lastl = l;
+        }
+    }
+    *pl_out = pl;
+    // zlib / libdeflate / libdmx send HCLEN up to the last nonzero length (>= 4)
+    return kr == 128 && (lastl != 0 || hclen == 4);
+}
+
 __global__ __launch_bounds__(64) void k_fb_scan(const uint32_t* in_words, uint64_t misalign,
                                                  uint64_t n, uint32_t* counts, uint64_t* hits) {
     __shared__ uint32_t stg[FB_STAGE_WORDS + 2];
+    __shared__ uint32_t q1[FB_STEP + 64];  // offsets r (bit 31: a stored-block hit)
+    __shared__ uint32_t q2[128];
     const uint32_t lane = threadIdx.x;
     const uint64_t c = blockIdx.x;
     // stage words of the aligned image: bit 0 of word 0 = stream bit b0 - sh
@@ -155,54 +185,111 @@ __global__ __launch_bounds__(64) void k_fb_scan(const uint32_t* in_words, uint64
     }
     __syncthreads();
     const uint64_t nbits = 8 * n;
-    uint32_t found = 0;
-    for (uint32_t it = 0; it < FB_SCAN_BITS / 64 && found < FB_HITS; it++) {
-        const uint32_t r = it * 64 + lane;  // offset tested by this lane, relative to b0
-        const uint64_t sb = b0 + r;         // stream bit
+    uint32_t found = 0, n1 = 0, n2 = 0;
+    const uint64_t below = (1ull << lane) - 1ull;
+    // stage 2 on q2[0, m): hits in order; the rest of q2 moves down
+    auto drain2 = [&](uint32_t m) {
         bool hit = false, stored = false;
-        if (sb + 17 + 12 < nbits) {
-            const uint32_t q = sh + r;      // staged-image bit
-            const uint32_t h = fb_bits(stg, q);
-            if (((h >> 1) & 3) == 0) {
-                // stored block: LEN and NLEN = ~LEN at the next byte boundary, data inside the
-                // stream (zlib writes these for incompressible runs; without them a unit ending
-                // before a stored block had no unit to continue the chain).  A header in zero
-                // padding is found at several offsets; the chain takes the one the unit before
-                // ends at, the others only cost parallelism.
-                const uint64_t bb = (sb + 3 + 7) & ~7ull;  // stream bit of LEN
-                if (bb + 32 <= nbits) {
-                    const uint32_t ln = fb_bits(stg, q + (uint32_t)(bb - sb));
-                    hit = stored = ((ln ^ (ln >> 16)) & 0xFFFFu) == 0xFFFFu && bb / 8 + 4 + (ln & 0xFFFFu) <= n;
-                }
-            }
-            const uint32_t hlit = (h >> 3) & 31, hdist = (h >> 8) & 31, hclen = ((h >> 13) & 15) + 4;
-            if (((h >> 1) & 3) == 2 && hlit <= 29 && hdist <= 29) {
-                const uint32_t x0 = fb_bits(stg, q + 17), x1 = fb_bits(stg, q + 49);
-                const uint64_t x = (uint64_t)x0 | ((uint64_t)x1 << 32);
-                uint64_t pl = 0;
-                uint32_t kr = 0, lastl = 0;
-                for (uint32_t i = 0; i < 19; i++) {
-                    if (i < hclen) {
-                        const uint32_t l = (uint32_t)(x >> (3 * i)) & 7;
-                        pl |= (uint64_t)l << (3 * kPerm[i]);
-                        kr += l ? 128u >> l : 0u;
-                        lastl = l;
-                    }
-                }
-                // zlib / libdeflate / libdmx send HCLEN up to the last nonzero length (>= 4)
-                if (kr == 128 && (lastl != 0 || hclen == 4))
-                    hit = fb_check_lengths(stg, q + 17 + 3 * hclen, pl, hlit + 257, hdist + 1,
-                                           (FB_STAGE_WORDS - 1) * 32);
+        uint32_t r = 0;
+        if (lane < m) {
+            const uint32_t e = q2[lane];
+            r = e & 0x7FFFFFFFu;
+            stored = (e >> 31) != 0;
+            if (stored) {
+                hit = true;
+            } else {
+                const uint32_t q = sh + r;
+                const uint32_t h = fb_bits(stg, q);
+                uint64_t pl;
+                (void)fb_precode(h, stg, q, &pl);
+                hit = fb_check_lengths(stg, q + 17 + 3 * (((h >> 13) & 15) + 4), pl, ((h >> 3) & 31) + 257,
+                                       ((h >> 8) & 31) + 1, (FB_STAGE_WORDS - 1) * 32);
             }
         }
-        const uint64_t m = __ballot(hit);
-        if (m) {
-            const uint32_t before = __popcll(m & ((1ull << lane) - 1ull));
-            if (hit && found + before < FB_HITS)
-                hits[c * FB_HITS + found + before] = sb | (stored ? FB_HIT_STORED : 0ull);
-            found += __popcll(m);
+        const uint64_t hm = __ballot(hit);
+        const uint32_t before = __popcll(hm & below);
+        if (hit && found + before < FB_HITS)
+            hits[c * FB_HITS + found + before] = (b0 + r) | (stored ? FB_HIT_STORED : 0ull);
+        found += __popcll(hm);
+        const uint32_t rest = n2 - m;
+        const uint32_t mv = lane < rest ? q2[m + lane] : 0u;
+        wave_sync();
+        if (lane < rest) q2[lane] = mv;
+        wave_sync();
+        n2 = rest;
+    };
+    // stage 1 on q1[0, m): survivors to q2 (in order); the rest of q1 moves down
+    auto drain1 = [&](uint32_t m) {
+        bool pass = false;
+        uint32_t e = 0;
+        if (lane < m) {
+            e = q1[lane];
+            if (e >> 31) {
+                pass = true;
+            } else {
+                const uint32_t q = sh + e;
+                uint64_t pl;
+                pass = fb_precode(fb_bits(stg, q), stg, q, &pl);
+            }
         }
+        const uint64_t pm = __ballot(pass);
+        if (pass) q2[n2 + __popcll(pm & below)] = e;
+        n2 += __popcll(pm);
+        const uint32_t rest = n1 - m;
+        wave_sync();
+        for (uint32_t i = lane; i < rest; i += 64) q1[i] = q1[m + i];  // (m = 64: no pass
+                                                  // writes an entry that it or a later pass reads)
+        wave_sync();
+        n1 = rest;
+        if (n2 >= 64) drain2(64);
+    };
+    for (uint32_t step = 0; step < FB_SCAN_BITS / FB_STEP && found < FB_HITS; step++) {
+        const uint32_t o = step * FB_STEP + lane * 32;  // this lane's first offset (relative to b0)
+        const uint32_t q = sh + o, i = q >> 5, k = q & 31;
+        const uint32_t s0 = stg[i], s1 = stg[i + 1], s2 = stg[i + 2];
+        const uint64_t v = (uint64_t)__builtin_amdgcn_alignbit(s1, s0, k) |
+                           ((uint64_t)__builtin_amdgcn_alignbit(s2, s1, k) << 32);
+        uint64_t m = ~(v >> 1) & (v >> 2);                     // BTYPE 2
+        m &= ~((v >> 4) & (v >> 5) & (v >> 6) & (v >> 7));     // HLIT <= 29
+        m &= ~((v >> 9) & (v >> 10) & (v >> 11) & (v >> 12));  // HDIST <= 29
+        uint32_t dyn = (uint32_t)m;
+        uint32_t sto = (uint32_t)(~(v >> 1) & ~(v >> 2)) & 0x01010101u;  // BTYPE 0, byte-aligned
+        // offsets whose header would read past the stream end
+        const uint64_t sb = b0 + o;
+        const uint32_t nval = sb + 29 >= nbits ? 0u : (nbits - sb - 29 >= 32 ? 32u : (uint32_t)(nbits - sb - 29));
+        const uint32_t vmask = nval >= 32 ? 0xFFFFFFFFu : ((1u << nval) - 1u);
+        dyn &= vmask;
+        sto &= vmask;
+        // stored block at a byte boundary (where a stored block after another stored block
+        // starts): LEN and NLEN = ~LEN at the next byte boundary, data inside the stream.  These
+        // let runs of stored blocks (incompressible data) decode unit by unit.  A stored block
+        // after a Huffman block starts at any bit; the unit before simply decodes it too (a
+        // strong unit only stops on landing on a start or past its stop).  Only aligned offsets:
+        // the offsets inside a header's zero padding and just before it all look like stored
+        // headers, and would crowd the chunk's FB_HITS out.
+        uint32_t sh_ok = 0;
+        for (uint32_t t = sto; t; t &= t - 1) {
+            const uint32_t bi = __builtin_ctz(t);
+            const uint64_t bb = sb + bi + 8;  // stream bit of LEN
+            if (bb + 32 <= nbits) {
+                const uint32_t ln = fb_bits(stg, q + bi + 8);
+                if (((ln ^ (ln >> 16)) & 0xFFFFu) == 0xFFFFu && bb / 8 + 4 + (ln & 0xFFFFu) <= n) sh_ok |= 1u << bi;
+            }
+        }
+        const uint32_t all = dyn | sh_ok;
+        const uint32_t cnt = __builtin_popcount(all);
+        const uint32_t incl = wave_incl_scan(cnt);
+        uint32_t pos = n1 + incl - cnt;
+        for (uint32_t t = all; t; t &= t - 1) {
+            const uint32_t bi = __builtin_ctz(t);
+            q1[pos++] = (o + bi) | ((sh_ok >> bi) & 1u ? 0x80000000u : 0u);
+        }
+        n1 += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        wave_sync();
+        while (n1 >= 64) drain1(64);
     }
+    while (n1) drain1(n1 < 64 ? n1 : 64u);
+    if (n2 && found < FB_HITS) drain2(n2);
     if (lane == 0) counts[c] = min(found, FB_HITS);
 }
 
@@ -394,57 +481,70 @@ struct RingWords {
 };
 __device__ __forceinline__ RingWords reader_words(const RingIn& br) { return RingWords{br.ring}; }
 
-__global__ __launch_bounds__(64) void k_fb_decode(const uint32_t* in_words, uint64_t misalign,
-                                                   uint64_t n, const uint64_t* starts,
-                                                   const uint64_t* stops, uint64_t nunits,
-                                                   const uint64_t* tokoff, uint32_t* tok,
-                                                   FbUnit* units, uint32_t flags) {
-    __shared__ Tables T;
-    __shared__ uint32_t ring[FB_RW];
-    const uint64_t u = blockIdx.x;
-    if (u >= nunits) return;
+struct FbDecodeArgs {
+    const uint32_t* in_words;
+    uint64_t misalign, n;
+    const uint64_t* starts;
+    const uint64_t* stops;
+    uint64_t nunits;
+    const uint64_t* tokoff;
+    uint32_t* tok;
+    FbUnit* units;
+    uint32_t flags;
+    uint32_t* stats;  // optional (DMX_FB_DEBUG): units decoded lane-parallel, serially from the
+                      // start, serially after a parallel first block, weak units
+};
+
+// One wavefront: realDecompress (inflate.hpp:277-322) for unit u from stream bit `from`
+// (relative to stream bit 0), appending to a token list that already holds n0 words for bytes0
+// output bytes; the unit's record is written at the end.  first: the block at `from` is the
+// unit's first, decoded before any stop check.
+__device__ __attribute__((noinline)) void fb_serial(const FbDecodeArgs& A, uint64_t u, Tables& T, uint32_t* ring, uint64_t from,
+                          uint32_t n0, uint64_t bytes0, bool first) {
     if (lane_id() == 0) T.fixed_loaded = 0;
     wave_sync();
-    const uint64_t start = starts[u];
+    const uint64_t start = A.starts[u];
     // A unit ends after the first block that lands exactly on another unit's start, or that
     // passes the next dynamic-header start (stored-header starts can be false: passing one
     // inside a block is no reason to stop, landing on one is a chain link).
-    // A unit at a stored-header start (bit 63 of its stop) decodes stored blocks only and ends
-    // before the first other block: such a start can be false, and a false one then costs one
-    // bounded copy instead of a run of Huffman decoding over arbitrary bits.
-    const bool weak = (stops[u] >> 63) != 0;
-    const uint64_t stop = stops[u] & ~(1ull << 63);
+    // A unit at a stored-header start (bit 63 of its stop) decodes stored and fixed-code blocks
+    // and ends before the first dynamic block (whose start is a scanned hit): such a start can
+    // be false, and a false one then costs a bounded copy, or at most a fixed-code decode up to
+    // the next dynamic-header start.  (Fixed blocks are not scanned, so a stored block followed
+    // by fixed ones -- zlib's small blocks -- needs the weak unit to carry on through them.)
+    const bool weak = (A.stops[u] >> 63) != 0;
+    const uint64_t stop = A.stops[u] & ~(1ull << 63);
     uint64_t jn = u + 1;  // first unit start not below the current position
     uint64_t end_at = 0;  // (weak units) stream bit of the first block they leave undecoded
-    const uint64_t base = misalign * 8;  // stream bit 0 in the aligned image
+    const uint64_t base = A.misalign * 8;  // stream bit 0 in the aligned image
     RingIn br;
-    br.init(in_words, misalign, n, ring);
-    br.seek(base + start);
+    br.init(A.in_words, A.misalign, A.n, ring);
+    br.seek(base + from);
     TokSink sk;
-    sk.tk = tok + tokoff[u];
-    sk.cap = (uint32_t)(tokoff[u + 1] - tokoff[u]);
-    sk.n = sk.k = sk.reg = sk.pend = sk.pendn = 0;
-    sk.pos = 0;
+    sk.tk = A.tok + A.tokoff[u];
+    sk.cap = (uint32_t)(A.tokoff[u + 1] - A.tokoff[u]);
+    sk.n = n0;
+    sk.k = sk.reg = sk.pend = sk.pendn = 0;
+    sk.pos = bytes0;
     sk.unit_byte0 = (base + start) >> 3;
-    sk.stream_start = u == 0 && !(flags & DMX_IFLAG_PIECE);
+    sk.stream_start = u == 0 && !(A.flags & DMX_IFLAG_PIECE);
     sk.err = 0;
-    const bool rfc = (flags & DMX_CFG_RFC_STRICT) != 0;
+    const bool rfc = (A.flags & DMX_CFG_RFC_STRICT) != 0;
     uint32_t err = 0;
     bool fin = false;
-    // realDecompress (inflate.hpp:277-322) until the next unit's start or BFINAL
-    for (bool first = true;; first = false) {
-        if (!first) {
+    for (bool f = first;; f = false) {
+        if (!f) {
             const uint64_t pos = br.abspos() - base;
             if (pos >= stop) break;
-            while (jn < nunits && starts[jn] < pos) jn++;
-            if (jn < nunits && starts[jn] == pos) break;
+            while (jn < A.nunits && A.starts[jn] < pos) jn++;
+            if (jn < A.nunits && A.starts[jn] == pos) break;
         }
         const uint64_t hpos = br.abspos();
         br.ensure(3);
         const uint32_t bfinal = br.bits(1);
         const uint32_t btype = br.bits(2);
         if (br.over()) { err = SEGF_OVERREAD; break; }
-        if (weak && btype != 0) {
+        if (weak && btype == 2) {
             end_at = hpos;
             break;
         }
@@ -487,7 +587,391 @@ __global__ __launch_bounds__(64) void k_fb_decode(const uint32_t* in_words, uint
         r.size = sk.pos;
         r.ntok = sk.n;
         r.flags = err | (fin ? SEGF_FINAL : 0u);
-        units[u] = r;
+        A.units[u] = r;
+    }
+}
+
+// the serial decoder alone, one wavefront per unit (DMX_FB_SERIAL=1: A/B reference)
+__global__ __launch_bounds__(64) void k_fb_decode(FbDecodeArgs A) {
+    __shared__ Tables T;
+    __shared__ uint32_t ring[FB_RW];
+    const uint64_t u = blockIdx.x;
+    if (u >= A.nunits) return;
+    fb_serial(A, u, T, ring, A.starts[u], 0, 0, true);
+}
+
+// ---------------------------------------------------------------------------------------
+// k_fb_pdecode: one workgroup of FBP_NT lanes per unit.  A unit whose first block is Huffman
+// coded (fixed or dynamic) and whose bits up to the next dynamic-header start fit the staging
+// buffer has that block decoded lane-parallel, the k_inflate_pj way:
+//   1. wave 0 reads the block header from the staged words, the workgroup fills 32-bit tables;
+//   2. the block body [hs, he) (he = the unit's stop) is split into ranges of >= FBP_MINBITS
+//      bits; each lane warms up FBP_WARM bits before its range (Huffman decoding re-synchronises
+//      within a few tokens), then decodes through its range marking token starts and counting
+//      token words and output bytes;
+//   3. settle: a lane whose start is not where the previous range's path crossed in re-decodes
+//      from there until it meets one of its own token starts (normally nobody, or one round);
+//   4. ranges past the first one that reaches end-of-block are dropped; lanes that moved recount;
+//   5. exclusive scans of words and bytes, then every lane writes its range's token words (the
+//      TokSink format: literal runs of up to 3, matches) at its word offset.
+// The unit then ends where the serial decoder would end it (BFINAL, the stop, or landing on
+// another unit start); otherwise wave 0 continues with fb_serial from the block's end.  Anything
+// the parallel pass cannot vouch for -- a stored, weak or oversized unit, a header error, no
+// end-of-block before `he`, a bad code, no settlement, a copy from before the stream start in
+// unit 0 -- makes wave 0 decode the whole unit with fb_serial instead, so results and error
+// codes are the serial decoder's.
+// ---------------------------------------------------------------------------------------
+constexpr int FBP_NT = 1024;
+constexpr uint32_t FBP_IN = 14336;    // staged words (a block body of up to ~56 KB: zlib's
+                                      // blocks of 16 K symbols at up to ~27 bits each)
+constexpr uint32_t FBP_MINBITS = 128;  // shortest range a lane decodes
+constexpr uint32_t FBP_WARM = 320;     // warm-up bits before a range
+constexpr int FBP_ROUNDS = 1024;  // a settle cascade (data that re-synchronises slowly) still
+                                   // beats the serial decoder by far
+struct FbpSmem {
+    uint32_t in[FBP_IN + 8];  // stream words [ws, ws + nst), zero after; fb_serial's ring later
+    uint32_t bmap[FBP_IN];    // token starts of the first pass (bit p = body bit p)
+    uint32_t llut[1 << PJ_LL];
+    uint32_t dlut[1 << PJ_LD];
+    Tables T;
+    uint32_t endp[FBP_NT];    // where range r's path crossed into range r + 1
+    uint32_t wcnt[FBP_NT];    // words of range r, then its exclusive word offset
+    uint32_t bcnt[FBP_NT];    // output bytes of range r, then its exclusive byte offset
+    uint32_t part[2][FBP_NT / 64];
+    uint32_t te2[2];
+    uint32_t kind;            // 0 parallel, 1 serial from the unit start, 2 serial continuation,
+                              // 3 an error the serial decoder would report (S.err), 4 again
+    uint32_t btype, bfinal, hs, nst, words, bytes, err;
+    uint64_t ws, he, hecap, endbit;
+};
+static_assert(sizeof(FbpSmem) <= 160 * 1024, "LDS");
+
+// wave 0 of k_fb_pdecode: the block's code tables from the staged words (out of line: the
+// header reader's registers would otherwise spill in the 1024-lane kernel)
+__device__ __attribute__((noinline)) uint32_t fbp_header(Tables& T, uint32_t btype, const uint32_t* in,
+                                                         uint64_t ws, uint32_t nst, uint64_t* hp,
+                                                         uint64_t end_bits, bool rfc) {
+    if (btype == 1) {
+        load_fixed(T);
+        return 0;
+    }
+    const StagedWords src{in, ws, nst};
+    return fast_header(src, hp, end_bits, T, rfc, false);
+}
+
+__global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
+    __shared__ __attribute__((aligned(16))) FbpSmem S;
+    constexpr int NW = FBP_NT / 64;
+    const int t = threadIdx.x;
+    const int wave = t >> 6;
+    const uint64_t u = blockIdx.x;
+    const uint64_t start = A.starts[u];
+    const bool weak = (A.stops[u] >> 63) != 0;
+    const uint64_t stop = A.stops[u] & ~(1ull << 63);
+    const uint64_t base = A.misalign * 8;
+    const uint64_t end_bytes = A.misalign + A.n;
+    const uint64_t nwords = (end_bytes + 3) / 4;
+    const uint64_t nbits = 8 * A.n;
+    const bool rfc = (A.flags & DMX_CFG_RFC_STRICT) != 0;
+    const bool stream_start = u == 0 && !(A.flags & DMX_IFLAG_PIECE);
+    // ---- 1. block type, staging window ----
+    if (t == 0) {
+        uint32_t kind = 1;
+        const uint64_t b = base + start;
+        const uint32_t w0 = A.in_words[b >> 5];
+        const uint32_t w1 = (b >> 5) + 1 < nwords ? A.in_words[(b >> 5) + 1] : 0u;
+        const uint32_t h = __builtin_amdgcn_alignbit(w1, w0, (uint32_t)(b & 31));
+        const uint32_t btype = (h >> 1) & 3;
+        // The block must end by he: first the stop (the next dynamic-header start), then -- if
+        // no end of block comes before it: a false header hit inside the block -- as far as the
+        // staging reaches.  Staged: as many words as fit.
+        const uint64_t ws = b >> 5;
+        const uint64_t hecap = min(nbits, (ws + FBP_IN - 16) * 32 - base);
+        if (!weak && (btype == 1 || btype == 2) && start + 3 < hecap) {
+            kind = 0;
+            S.ws = ws;
+            S.nst = (uint32_t)(min(ws + FBP_IN - 13, nwords) - ws);
+            S.he = min(stop, hecap);
+            S.hecap = hecap;
+        }
+        S.kind = kind;
+        S.btype = btype;
+        S.bfinal = h & 1;
+    }
+    __syncthreads();
+    if (S.kind == 0) {
+        const uint64_t ws = S.ws;
+        const uint32_t nst = S.nst;
+        for (uint32_t i = t; i < nst + 8; i += FBP_NT) {
+            uint32_t v = 0;
+            if (i < nst) {
+                const uint64_t wi = ws + i;
+                v = A.in_words[wi];
+                const uint64_t lim = end_bytes - 4 * wi;
+                if (lim < 4) v &= (1u << (8 * lim)) - 1u;
+            }
+            S.in[i] = v;
+        }
+        __syncthreads();
+        if (wave == 0) {
+            uint64_t hp = base + start + 3;
+            const uint32_t err = fbp_header(S.T, S.btype, S.in, ws, nst, &hp, end_bytes * 8, rfc);
+            if (lane_id() == 0) {
+                const uint64_t hs = hp - ws * 32;
+                if (err) {  // the serial decoder fails here too: the unit's record says so
+                    S.kind = 3;
+                    S.err = err;
+                } else if (base + S.hecap - ws * 32 <= hs) {
+                    S.kind = 1;
+                    if (A.stats) atomicAdd(&A.stats[4], 1u);
+                } else if (base + S.he - ws * 32 <= hs) {
+                    S.he = S.hecap;  // the stop lies inside the header
+                }
+                S.hs = (uint32_t)hs;
+            }
+        }
+        __syncthreads();
+        if (S.kind == 0) {
+            fill_lut32_wg<PJ_LL, false>(S.llut, S.T.lm, S.T.lsorted, t, FBP_NT);
+            fill_lut32_wg<PJ_LD, true>(S.dlut, S.T.dm, S.T.dsorted, t, FBP_NT);
+        }
+        __syncthreads();
+    }
+    for (int attempt = 0; attempt < 2 && S.kind == 0; attempt++) {
+        const uint32_t* win = S.in;
+        const uint32_t hs = S.hs, hlen = (uint32_t)(base + S.he - S.ws * 32 - hs);
+        const uint32_t nl = max(1u, min((uint32_t)FBP_NT, hlen / FBP_MINBITS));
+        const uint32_t r = (uint32_t)((t & 63) * NW + wave);
+        const uint32_t sp = r < nl ? (uint32_t)(((uint64_t)hlen * r) / nl) : hlen;
+        const uint32_t sp1 = r + 1 < nl ? (uint32_t)(((uint64_t)hlen * (r + 1)) / nl) : hlen;
+        const uint32_t cw = hlen / 32 + 2;
+        for (uint32_t i = t; i < cw; i += FBP_NT) S.bmap[i] = 0;
+        if (t < 2) S.te2[t] = FBP_NT;
+        __syncthreads();
+        // ---- 2. warm-up, first pass ----
+        uint32_t s0 = sp;
+        if (r > 0 && r < nl) {
+            uint32_t p = sp > FBP_WARM ? sp - FBP_WARM : 0u, pa = hs + p;
+            bool ok = true;
+            while (p < sp) {
+                uint32_t a, d;
+                const uint32_t k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
+                if (k == TK_BAD || k == TK_EOB) { ok = false; break; }
+                p = pa - hs;
+            }
+            if (ok && p < sp1) s0 = p;
+        }
+        uint32_t e1, st1 = 0, w1 = 0, b1 = 0;
+        {
+            uint32_t p = s0, pa = hs + s0, pn = 0;
+            while (p < sp1) {
+                atomicOr(&S.bmap[p >> 5], 1u << (p & 31));
+                uint32_t a, d;
+                const uint32_t k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
+                if (k == TK_BAD) { st1 = 2; break; }
+                p = pa - hs;
+                if (k == TK_EOB) { st1 = 1; break; }
+                if (k == TK_LIT) {
+                    if (pn == 3) { w1++; pn = 0; }
+                    pn++;
+                    b1++;
+                } else if (a && d) {
+                    w1 += pn ? 2u : 1u;
+                    pn = 0;
+                    b1 += a;
+                }
+            }
+            if (pn) w1++;
+            e1 = p;
+        }
+        // ---- 3. settle the range starts (k_inflate_pj's protocol) ----
+        uint32_t s = s0, e = e1, st = st1;
+        uint32_t te = FBP_NT;
+        bool settled = false;
+        for (int round = 0; round <= FBP_ROUNDS; round++) {
+            S.endp[r] = e;
+            if (st) atomicMin(&S.te2[round & 1], r);
+            if (t == 0) S.te2[(round + 1) & 1] = FBP_NT;
+            __syncthreads();
+            te = S.te2[round & 1];
+            const uint32_t want = r == 0 ? 0 : S.endp[r - 1];
+            const bool redo = r > 0 && r <= te && want != s;
+            if (!__syncthreads_or(redo)) {
+                settled = true;
+                break;
+            }
+            if (round == FBP_ROUNDS) break;
+            if (redo) {
+                s = want;
+                uint32_t p = want, pa = hs + want, stn = 0;
+                bool merged = false;
+                for (;;) {
+                    if (p >= sp1) break;
+                    if (p >= sp && ((S.bmap[p >> 5] >> (p & 31)) & 1u)) {
+                        merged = true;
+                        break;
+                    }
+                    uint32_t a, d;
+                    const uint32_t k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
+                    if (k == TK_BAD) { stn = 2; break; }
+                    p = pa - hs;
+                    if (k == TK_EOB) { stn = 1; break; }
+                }
+                e = merged ? e1 : p;
+                st = merged ? st1 : stn;
+            }
+            __syncthreads();
+        }
+        // ---- 4. the block's end; recount ranges that moved ----
+        if (t == 0 && !settled) {
+            S.kind = 1;
+            if (A.stats) atomicAdd(&A.stats[5], 1u);
+        } else if (t == 0 && te >= (uint32_t)FBP_NT) {
+            // no end of block before he: again up to the staging's end, else serially
+            S.kind = S.he < S.hecap ? 4u : 1u;
+            if (S.kind == 4) S.he = S.hecap;
+            if (A.stats) atomicAdd(&A.stats[6], 1u);
+        }
+        if (r == te && settled) {
+            // a code that decodes to nothing, or an end past the stream: the serial decoder
+            // stops with this error too
+            const uint64_t pe_abs = S.ws * 32 + hs + e;
+            if (st != 1 || pe_abs > end_bytes * 8) {
+                S.kind = 3;
+                S.err = st != 1 ? SEGF_ERR_DATA : SEGF_OVERREAD;
+                if (A.stats) atomicAdd(&A.stats[7], 1u);
+            }
+            S.endbit = pe_abs - base;
+        }
+        __syncthreads();
+        const uint32_t kk = S.kind;
+        if (kk != 0) {
+            __syncthreads();  // every lane has read it
+            if (kk == 4 && t == 0) S.kind = 0;
+            __syncthreads();
+            continue;
+        }
+        if (r <= te && s != s0) {
+            uint32_t p = s, pa = hs + s, pn = 0;
+            w1 = b1 = 0;
+            while (p < sp1) {
+                uint32_t a, d;
+                const uint32_t k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
+                p = pa - hs;
+                if (k == TK_BAD || k == TK_EOB) break;
+                if (k == TK_LIT) {
+                    if (pn == 3) { w1++; pn = 0; }
+                    pn++;
+                    b1++;
+                } else if (a && d) {
+                    w1 += pn ? 2u : 1u;
+                    pn = 0;
+                    b1 += a;
+                }
+            }
+            if (pn) w1++;
+        }
+        // ---- 5. scans, then the token words ----
+        S.wcnt[r] = r <= te ? w1 : 0u;
+        S.bcnt[r] = r <= te ? b1 : 0u;
+        __syncthreads();
+        const uint32_t cwv = S.wcnt[t], cbv = S.bcnt[t];
+        const uint32_t iw = wave_incl_scan(cwv), ib = wave_incl_scan(cbv);
+        if ((t & 63) == 63) {
+            S.part[0][wave] = iw;
+            S.part[1][wave] = ib;
+        }
+        __syncthreads();
+        uint32_t bw = 0, bb = 0, tw = 0, tb = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            const uint32_t x = S.part[0][w], y = S.part[1][w];
+            bw += w < wave ? x : 0u;
+            bb += w < wave ? y : 0u;
+            tw += x;
+            tb += y;
+        }
+        __syncthreads();  // every lane has read its counts
+        S.wcnt[t] = bw + iw - cwv;
+        S.bcnt[t] = bb + ib - cbv;
+        const uint32_t cap = (uint32_t)(A.tokoff[u + 1] - A.tokoff[u]);
+        if (t == 0) {
+            S.words = tw;
+            S.bytes = tb;
+            if (tw > cap) {
+                S.kind = 1;
+                if (A.stats) atomicAdd(&A.stats[8], 1u);
+            }
+        }
+        __syncthreads();
+        if (S.kind == 0 && r <= te) {
+            uint32_t* tk = A.tok + A.tokoff[u] + S.wcnt[r];
+            uint32_t o = S.bcnt[r];
+            uint32_t p = s, pa = hs + s, pn = 0, pend = 0, nw = 0;
+            bool drop = false;
+            while (p < sp1) {
+                uint32_t a, d;
+                const uint32_t k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
+                p = pa - hs;
+                if (k == TK_BAD || k == TK_EOB) break;
+                if (k == TK_LIT) {
+                    if (pn == 3) {
+                        tk[nw++] = (3u << 24) | pend;
+                        pn = pend = 0;
+                    }
+                    pend |= a << (8 * pn);
+                    pn++;
+                    o++;
+                } else if (a && d) {
+                    if (stream_start && d > o) drop = true;  // the reference copies nothing
+                    if (pn) {
+                        tk[nw++] = (pn << 24) | pend;
+                        pn = pend = 0;
+                    }
+                    tk[nw++] = 0x80000000u | (a << 15) | (d - 1);
+                    o += a;
+                }
+            }
+            if (pn) tk[nw++] = (pn << 24) | pend;
+            if (drop) {
+                S.kind = 1;
+                if (A.stats) atomicAdd(&A.stats[9], 1u);
+            }
+        }
+        __syncthreads();
+        // the unit ends after this block unless the serial decoder would go on
+        if (t == 0 && S.kind == 0 && !S.bfinal) {
+            const uint64_t pos = S.endbit;
+            bool ends = pos >= stop;
+            if (!ends) {
+                uint64_t lo = u + 1, hi = A.nunits;  // first start >= pos
+                while (lo < hi) {
+                    const uint64_t mid = (lo + hi) >> 1;
+                    if (A.starts[mid] < pos) lo = mid + 1;
+                    else hi = mid;
+                }
+                ends = lo < A.nunits && A.starts[lo] == pos;
+            }
+            if (!ends) S.kind = 2;
+        }
+        __syncthreads();
+        break;
+    }
+    const uint32_t kind = S.kind;
+    if (A.stats && t == 0) atomicAdd(&A.stats[weak ? 3 : kind == 3 ? 0 : kind], 1u);
+    if (kind == 0 || kind == 3) {
+        if (t == 0) {
+            FbUnit rec;
+            rec.start = start;
+            rec.end = kind == 0 ? S.endbit : start;
+            rec.size = kind == 0 ? S.bytes : 0;
+            rec.ntok = kind == 0 ? S.words : 0;
+            rec.flags = kind == 3 ? S.err : S.bfinal ? SEGF_FINAL : 0u;
+            A.units[u] = rec;
+        }
+    } else if (wave == 0) {
+        if (kind == 1) fb_serial(A, u, S.T, S.in, start, 0, 0, true);
+        else fb_serial(A, u, S.T, S.in, S.endbit, S.words, S.bytes, false);
     }
 }
 
@@ -570,13 +1054,28 @@ __global__ __launch_bounds__(64) void k_fb_replay(FbReplayArgs A) {
     uint64_t pos = 0;   // output entries so far (ring index = pos mod FB_RING)
     bool bad = false;   // a copy reaching before the stream start
     uint32_t t0 = 0;
+    // token words t0 + lane (wc) and t0 + 64 + lane (wn, loaded a group ahead: its latency
+    // passes while the current group replays), word t0 - 1 (wl)
+    uint32_t wc = lane < n ? tk[lane] : 0u;
+    uint32_t wn = 64 + lane < n ? tk[64 + lane] : 0u;
+    uint32_t wl = 0;
+    auto advance = [&](uint32_t adv) {  // 1 <= adv <= 64
+        const uint32_t idx = lane + adv;
+        const uint32_t a = (uint32_t)__shfl((int)wc, (int)(idx & 63), 64);
+        const uint32_t b = (uint32_t)__shfl((int)wn, (int)(idx & 63), 64);
+        wl = (uint32_t)__shfl((int)wc, (int)(adv - 1), 64);
+        wc = idx < 64 ? a : b;
+        const uint32_t nx = t0 + adv + 64 + lane;
+        wn = idx < 64 ? b : (nx < n ? tk[nx] : 0u);
+        t0 += adv;
+    };
     while (t0 < n) {
         const uint32_t ti = t0 + lane;
-        const uint32_t w = ti < n ? tk[ti] : 0u;
+        const uint32_t w = wc;
         // the word after a stored header is its offset (any 32-bit value, bit 31 included):
         // lane ti - 1 is that header
         const uint32_t wprev = (uint32_t)__shfl((int)w, (int)lane - 1, 64);
-        const uint32_t wp = lane == 0 ? (t0 > 0 ? tk[t0 - 1] : 0u) : wprev;
+        const uint32_t wp = lane == 0 ? wl : wprev;
         const bool isoff = (ti & 1) && !(wp >> 31) && ((wp >> 24) & 127) == 127 && ((ti - 1) & 1) == 0;
         const bool ism = (w >> 31) != 0 && !isoff;
         const uint32_t cnt = (w >> 24) & 127;
@@ -594,7 +1093,7 @@ __global__ __launch_bounds__(64) void k_fb_replay(FbReplayArgs A) {
         if (ntk == 0) {
             // a stored block larger than a group: copy it alone, in pieces of FB_GROUP_MAX
             const uint32_t len = (uint32_t)__builtin_amdgcn_readfirstlane((int)L);
-            const uint32_t so = tk[t0 + 1];
+            const uint32_t so = (uint32_t)__builtin_amdgcn_readlane((int)w, 1);
             const uint8_t* src = A.stream + byte0 + so;
             for (uint32_t p0 = 0; p0 < len; p0 += FB_GROUP_MAX) {
                 const uint32_t m = min(FB_GROUP_MAX, len - p0);
@@ -604,7 +1103,7 @@ __global__ __launch_bounds__(64) void k_fb_replay(FbReplayArgs A) {
                 wave_sync();
             }
             pos += len;
-            t0 += 2;
+            advance(2);
             continue;
         }
         const bool inq = lane < ntk;
@@ -653,7 +1152,10 @@ __global__ __launch_bounds__(64) void k_fb_replay(FbReplayArgs A) {
             if (wk >> 31) {
                 fb_ring_copy(ring, dst, (wk & 0x7FFFu) + 1, Lk);
             } else {
-                const uint32_t so = tk[t0 + k + 1];
+                // the offset word is token k + 1: in this group, or the first of the next
+                const uint32_t so0 = (uint32_t)__shfl((int)w, (k + 1) & 63, 64);
+                const uint32_t so1 = (uint32_t)__builtin_amdgcn_readlane((int)wn, 0);
+                const uint32_t so = k + 1 < 64 ? so0 : so1;
                 const uint8_t* src = A.stream + byte0 + so;
                 for (uint32_t i = lane; i < Lk; i += 64) ring[(dst + i) & (FB_RING - 1)] = src[i];
             }
@@ -663,7 +1165,7 @@ __global__ __launch_bounds__(64) void k_fb_replay(FbReplayArgs A) {
         for (uint32_t i = lane; i < T; i += 64) img[pos + i] = ring[(pos + i) & (FB_RING - 1)];
         wave_sync();
         pos += T;
-        t0 += ntk;
+        advance(ntk);
     }
     if (__ballot(bad) && lane == 0) atomicOr(A.err, 1u);
 }
@@ -747,13 +1249,69 @@ __global__ __launch_bounds__(FB_TNT) void k_fb_tails(const uint16_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------
-// k_fb_final: every entry before its unit's tail.  One workgroup per FB_FIN_SPAN entries; the
-// unit of the span's first entry is found by binary search over the chain offsets.
+// Parallel window hand-off (replaces k_fb_tails when the chain has < 65536 units).
+// Window k is the last FB_RING output positions before the end of unit k on the chain:
+// W[k * FB_RING + i] is output position uend_k - FB_RING + i, as a 32-bit entry that is either
+// a byte (bit 31 set) or the index of another window entry holding the same byte -- always in
+// window k - 1 or earlier, so the references form a forest rooted at bytes:
+//   k_fb_win_init   entries from the 16-bit image: a byte; a marker "b before unit k" -> entry
+//                   FB_RING - b of window k - 1; a position before unit k's start (short units)
+//                   -> the same position in window k - 1.
+//   k_fb_win_jump   pointer jumping, up to FB_HOPS hops per entry per round, in place (an
+//                   entry only ever moves further along its chain); a round that finds nothing
+//                   unresolved lets every later round return at once.  The chain depth is at
+//                   most the unit count, so ceil(log2(units)) + 1 rounds always suffice.
+//   k_fb_final      every output byte: an image byte, or its marker's window entry.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t FB_WLIT = 0x80000000u;
+constexpr int FB_HOPS = 8;
+constexpr uint32_t FB_WIN_BLK = 4096;  // window entries per k_fb_win_init workgroup
+__global__ __launch_bounds__(256) void k_fb_win_init(const uint16_t* __restrict__ img,
+                                                     const uint64_t* __restrict__ offs,
+                                                     const uint64_t* __restrict__ sizes,
+                                                     uint32_t* __restrict__ W) {
+    const uint64_t k = blockIdx.x;
+    const uint64_t uoff = offs[k], uend = uoff + sizes[k];
+    const uint64_t wk = k * FB_RING;
+    for (uint32_t i = blockIdx.y * FB_WIN_BLK + threadIdx.x; i < (blockIdx.y + 1) * FB_WIN_BLK; i += 256) {
+        uint32_t v = FB_WLIT;  // before the stream start: never referenced by a valid stream
+        if (uend + i >= FB_RING) {
+            const uint64_t x = uend + i - FB_RING;
+            if (x >= uoff) {
+                const uint32_t e = img[x];
+                if (e < 0x8000u) v = FB_WLIT | e;
+                else if (k > 0) v = (uint32_t)(wk - FB_RING + FB_RING - 1 - (e & 0x7FFFu));
+            } else {
+                v = (uint32_t)(wk - FB_RING + (x + FB_RING - uoff));
+            }
+        }
+        W[wk + i] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fb_win_jump(uint32_t* W, uint64_t nent, uint32_t* open, int round) {
+    if (round > 0 && __builtin_nontemporal_load(&open[round - 1]) == 0) return;
+    bool left = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nent; i += (uint64_t)gridDim.x * 256) {
+        uint32_t v = W[i];
+        if (v & FB_WLIT) continue;
+#pragma unroll 1
+        for (int h = 0; h < FB_HOPS && !(v & FB_WLIT); h++) v = W[v];
+        W[i] = v;
+        left |= !(v & FB_WLIT);
+    }
+    if (__ballot(left) && lane_id() == 0) atomicOr(&open[round], 1u);
+}
+
+// ---------------------------------------------------------------------------------------
+// k_fb_final: every entry (W != nullptr) or every entry before its unit's tail (after
+// k_fb_tails).  One workgroup per FB_FIN_SPAN entries; the unit of the span's first entry is
+// found by binary search over the chain offsets.
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t FB_FIN_SPAN = 16384;
 __global__ __launch_bounds__(256) void k_fb_final(const uint16_t* img, const uint64_t* offs,
                                                   const uint64_t* sizes, uint64_t nchain,
-                                                  uint64_t total, uint8_t* out) {
+                                                  uint64_t total, const uint32_t* W, uint8_t* out) {
     const uint64_t s0 = (uint64_t)blockIdx.x * FB_FIN_SPAN;
     if (s0 >= total) return;
     const uint64_t s1 = min(total, s0 + FB_FIN_SPAN);
@@ -771,11 +1329,15 @@ __global__ __launch_bounds__(256) void k_fb_final(const uint16_t* img, const uin
             uoff = offs[k];
             uend = uoff + sizes[k];
         }
-        const uint64_t s = uend - uoff;
-        if (x - uoff >= s - min(s, (uint64_t)FB_RING)) continue;  // tail: k_fb_tails wrote it
         const uint32_t v = img[x];
         const uint64_t b = (v & 0x7FFFu) + 1;  // a marker before the stream start was flagged
-        out[x] = v < 0x8000u ? (uint8_t)v : (b <= uoff ? out[uoff - b] : (uint8_t)0);
+        if (W) {
+            out[x] = v < 0x8000u ? (uint8_t)v : k > 0 ? (uint8_t)W[k * FB_RING - b] : (uint8_t)0;
+        } else {
+            const uint64_t s = uend - uoff;
+            if (x - uoff >= s - min(s, (uint64_t)FB_RING)) continue;  // tail: k_fb_tails wrote it
+            out[x] = v < 0x8000u ? (uint8_t)v : (b <= uoff ? out[uoff - b] : (uint8_t)0);
+        }
     }
 }
 
@@ -803,22 +1365,46 @@ hipError_t launch_fb_compact(const uint32_t* counts, const uint64_t* offs, const
 hipError_t launch_fb_decode(const uint32_t* in_words, uint64_t misalign, uint64_t n,
                             const uint64_t* starts, const uint64_t* stops, uint64_t nunits,
                             const uint64_t* tokoff, uint32_t* tok, FbUnit* units, uint32_t flags,
-                            hipStream_t st) {
-    hipLaunchKernelGGL(k_fb_decode, dim3((uint32_t)nunits), dim3(64), 0, st, in_words, misalign, n,
-                       starts, stops, nunits, tokoff, tok, units, flags);
+                            bool parallel, uint32_t* stats, hipStream_t st) {
+    const FbDecodeArgs A{in_words, misalign, n, starts, stops, nunits, tokoff, tok, units, flags, stats};
+    if (parallel)
+        hipLaunchKernelGGL(k_fb_pdecode, dim3((uint32_t)nunits), dim3(FBP_NT), 0, st, A);
+    else
+        hipLaunchKernelGGL(k_fb_decode, dim3((uint32_t)nunits), dim3(64), 0, st, A);
     return hipGetLastError();
+}
+
+uint64_t fb_window_entries(uint64_t nchain) { return nchain < 65536 ? nchain * FB_RING : 0; }
+uint32_t fb_window_rounds(uint64_t nchain) {
+    uint32_t r = 1;
+    while ((1ull << (r - 1)) < nchain) r++;
+    return r;
 }
 
 hipError_t launch_fb_resolve(const uint8_t* stream, const uint64_t* starts, const uint32_t* chain,
                              const uint64_t* offs, const uint64_t* sizes, uint64_t nchain,
                              const uint64_t* tokoff, const uint32_t* tok, const FbUnit* units,
                              uint16_t* img, uint64_t total, uint8_t* out, uint32_t* err,
-                             hipStream_t st) {
+                             uint32_t* win, uint32_t* open, hipStream_t st) {
     FbReplayArgs R{stream, starts, chain, offs, tokoff, tok, units, img, err};
     hipLaunchKernelGGL(k_fb_replay, dim3((uint32_t)nchain), dim3(64), 0, st, R);
-    hipLaunchKernelGGL(k_fb_tails, dim3(1), dim3(FB_TNT), 0, st, img, offs, sizes, nchain, out);
+    if (win) {
+        const uint64_t nent = fb_window_entries(nchain);
+        hipLaunchKernelGGL(k_fb_win_init, dim3((uint32_t)nchain, FB_RING / FB_WIN_BLK), dim3(256), 0, st,
+                           img, offs, sizes, win);
+        const uint32_t rounds = fb_window_rounds(nchain);
+        (void)hipMemsetAsync(open, 0, rounds * 4, st);
+        // one grid-striding wave of workgroups: a round with nothing left returns in microseconds
+        const uint32_t g = (uint32_t)std::min<uint64_t>((nent + 255) / 256, 1024);
+        for (uint32_t r = 0; r < rounds; r++)
+            hipLaunchKernelGGL(k_fb_win_jump, dim3(g), dim3(256), 0, st, win, nent, open, (int)r);
+    } else {
+        hipLaunchKernelGGL(k_fb_tails, dim3(1), dim3(FB_TNT), 0, st, img, offs, sizes, nchain, out);
+    }
     const uint64_t nb = (total + FB_FIN_SPAN - 1) / FB_FIN_SPAN;
-    if (nb) hipLaunchKernelGGL(k_fb_final, dim3((uint32_t)nb), dim3(256), 0, st, img, offs, sizes, nchain, total, out);
+    if (nb)
+        hipLaunchKernelGGL(k_fb_final, dim3((uint32_t)nb), dim3(256), 0, st, img, offs, sizes, nchain, total,
+                           (const uint32_t*)win, out);
     return hipGetLastError();
 }
 

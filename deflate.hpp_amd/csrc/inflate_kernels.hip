@@ -381,8 +381,6 @@ constexpr uint32_t PJ_MINBITS = PJ_MINBITS_;  // shortest range (bits) a lane de
 #ifndef PJ_WARM
 #define PJ_WARM 320u  // warm-up bits before a range's first pass (128: +25 % on text, 512: +1 %)
 #endif
-constexpr int PJ_LL = 12;  // lit/len lookup bits
-constexpr int PJ_LD = 10;  // distance lookup bits
 
 template <int SEG, int NT>
 struct PjSmem {
@@ -411,87 +409,6 @@ struct PjSmem {
     uint32_t total;
     uint64_t end_byte;
 };
-
-// 32 bits at bit p of the staged words (LSB = bit p)
-__device__ __forceinline__ uint32_t lds_peek32(const uint32_t* w, uint32_t p) {
-    const uint32_t i = p >> 5;
-    return __builtin_amdgcn_alignbit(w[i + 1], w[i], p & 31);
-}
-
-// primary lookup table over PB bits with 32-bit entries, filled by the whole workgroup
-template <int PB, bool DIST>
-__device__ void fill_lut32_wg(uint32_t* lut, const TreeMeta& m, const uint16_t* sorted, int tid, int nthr) {
-    uint32_t lo[16], hi[16], cn[16], of[16];
-#pragma unroll
-    for (int k = 1; k < 16; k++) {
-        lo[k] = m.lo[k];
-        hi[k] = m.hi[k];
-        cn[k] = m.cnt[k];
-        of[k] = m.offs[k];
-    }
-    for (int wv = tid; wv < (1 << PB); wv += nthr) {
-        const uint32_t v = bitrev(wv, PB);
-        uint32_t idx = 0, len = 0;
-#pragma unroll
-        for (int k = 1; k <= PB && k < 16; k++) {
-            const uint32_t x = v >> (PB - k);
-            if (!len && cn[k] && x <= hi[k]) {
-                const uint32_t cm = x + (((hi[k] - x) >> k) << k);
-                if (cm >= lo[k]) {
-                    idx = of[k] + cm - lo[k];
-                    len = k;
-                }
-            }
-        }
-        lut[wv] = len ? (DIST ? dist_entry(sorted[idx], len) : lit_entry(sorted[idx], len)) : 0u;
-    }
-}
-
-enum : uint32_t { TK_LIT = 0, TK_MATCH = 1, TK_EOB = 2, TK_BAD = 3 };
-
-// one token of decompressHuffmanBlock (inflate.hpp:226-275) at bit *p of the staged words:
-// a literal (*a = byte), a match (*a = length, *d = distance; 0 for symbols 286+ / 30+), the
-// end of block, or no code.  A literal reads one 32-bit window, a match two; the 32-bit table
-// entries carry class, code length, base and extra-bit count.
-__device__ __forceinline__ uint32_t pj_token(const uint32_t* w, uint32_t* p, const uint32_t* llut,
-                                             const uint32_t* dlut, const Tables& T, uint32_t* a,
-                                             uint32_t* d) {
-    uint32_t v = lds_peek32(w, *p);
-    uint32_t e = llut[v & ((1u << PJ_LL) - 1)];
-    if (!e) {
-        uint32_t sym, len;
-        if (!slow_decode(T.lm, T.lsorted, v & 0x7FFF, PJ_LL + 1, &sym, &len)) return TK_BAD;
-        e = lit_entry(sym, len);
-    }
-    const uint32_t cl = e & 15, ty = (e >> 4) & 3;
-    if (ty == 0) {
-        *p += cl;
-        *a = e >> 16;
-        return TK_LIT;
-    }
-    if (ty == 1) {
-        *p += cl;
-        return TK_EOB;
-    }
-    const uint32_t ex = (e >> 6) & 15;
-    *a = (e >> 16) + ((v >> cl) & ((1u << ex) - 1u));
-    *p += cl + ex;
-    v = lds_peek32(w, *p);
-    uint32_t de = dlut[v & ((1u << PJ_LD) - 1)];
-    if (!de) {
-        uint32_t ds, dl;
-        if (!slow_decode(T.dm, T.dsorted, v & 0x7FFF, PJ_LD + 1, &ds, &dl)) return TK_BAD;
-        de = dist_entry(ds, dl);
-    }
-    const uint32_t dl = de & 15, dx = (de >> 6) & 15;
-    *d = (de >> 16) + ((v >> dl) & ((1u << dx) - 1u));
-    *p += dl + dx;
-    return TK_MATCH;
-}
-
-__device__ __forceinline__ uint32_t tok_bytes(uint32_t k, uint32_t a, uint32_t d) {
-    return k == TK_LIT ? 1u : (k == TK_MATCH && a && d) ? a : 0u;
-}
 
 template <int SEG, int NT>
 __device__ __forceinline__ void pj_segment(const InflateArgs& A, PjSmem<SEG, NT>& S, const uint64_t j) {

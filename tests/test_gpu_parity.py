@@ -87,6 +87,53 @@ def test_inflate_foreign_stream_block_parallel_path(ctx, oracle, kind, lvl):
     assert ctx.decompress(small) == oracle.inflate(small) == d[: 1 << 19]
 
 
+def _zstream(d, lvl, mem, st, flush_every=0, mode=zlib.Z_SYNC_FLUSH):
+    z = zlib.compressobj(lvl, zlib.DEFLATED, -15, mem, st)
+    if not flush_every:
+        return z.compress(d) + z.flush()
+    return b"".join(z.compress(d[i:i + flush_every]) + z.flush(mode)
+                    for i in range(0, len(d), flush_every)) + z.flush()
+
+
+@pytest.mark.parametrize("kind,lvl,mem,st,fl", [
+    ("text", 1, 8, 0, 0), ("text", 9, 9, 0, 0), ("text", 4, 1, 0, 0), ("bmp", 1, 8, 0, 0),
+    ("mixed", 3, 2, 0, 0), ("repeat", 6, 8, 0, 0), ("text", 6, 8, zlib.Z_RLE, 0),
+    ("text", 6, 8, zlib.Z_HUFFMAN_ONLY, 0), ("mixed", 1, 8, 0, 100003), ("text", 5, 7, 0, 65536 + 17),
+    ("random", 1, 8, 0, 0), ("zeros", 1, 9, 0, 0), ("text", 6, 8, zlib.Z_FIXED, 0)])
+def test_inflate_path5_block_shapes(ctx, oracle, kind, lvl, mem, st, fl):
+    """Path 5's lane-parallel unit decode (k_fb_pdecode) over the block shapes zlib writes:
+    levels 1-9, memLevel 1-9 (block sizes from ~1 K to ~64 K symbols), RLE, Huffman-only and
+    fixed-code strategies, sync flushes (empty stored blocks between units), stored blocks of
+    random data.  Bit-exact with the oracle; the multi-MiB streams must stay on path 5 (or,
+    for one fixed-code block, on a serial decoder)."""
+    d = dmx.corpus(kind, 3 << 20, offset=4321)
+    s = _zstream(d, lvl, mem, st, fl)
+    out = ctx.decompress(s)
+    path = ctx.stats().path
+    assert out == d, (kind, lvl, mem, st, fl, path)
+    assert oracle.inflate(s) == d
+    if st != zlib.Z_FIXED and kind != "zeros":
+        assert path == 5, path
+
+
+def test_inflate_path5_truncated_and_corrupt(ctx, oracle):
+    """Error behaviour through path 5: a stream cut inside a block and one with a flipped bit
+    in the middle of a dynamic block give the oracle's result (bytes or error class)."""
+    d = dmx.corpus("text", 2 << 20, offset=5)
+    s = _zstream(d, 1, 8, 0)
+    for bad in (s[: len(s) * 2 // 3], s[:1000] + bytes([s[1000] ^ 0x10]) + s[1001:],
+                s[: len(s) // 2] + bytes([s[len(s) // 2] ^ 0x01]) + s[len(s) // 2 + 1:]):
+        try:
+            want = oracle.inflate(bad)
+        except CheckerError:
+            want = None
+        if want is None:
+            with pytest.raises(dmx.DmxError):
+                ctx.decompress(bad)
+        else:
+            assert ctx.decompress(bad) == want
+
+
 def test_inflate_c3_large_bmp_zlib1(ctx):
     """Config C3: the zlib level-1 raw stream of the full 25,165,962-B large.bmp
     stand-in (6.2 MB, hundreds of dynamic blocks with cross-block references), bit-exact with
