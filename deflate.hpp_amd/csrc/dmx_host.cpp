@@ -68,7 +68,7 @@ struct dmx_ctx {
     int ncu = 0;                         // compute units (mode 6 grid)
     // block-parallel path (path 5): scan counts / hits / offsets, hit list, unit starts, token
     // offsets and words, unit records, chain (unit index, offset, size), 16-bit image
-    DevBuf fbc, fbh, fbo, fbl, fbs, fbt, fbk, fbu, fbch, fbco, fbcs, fbimg, fbstop, fbwin, fbopen;
+    DevBuf fbc, fbh, fbo, fbl, fbs, fbt, fbk, fbu, fbch, fbco, fbcs, fbimg, fbstop, fbwin, fbopen, fbp32;
     DevBuf ck;  // checksum scratch (checksum.hip) + the 4-byte result at its start
     bool timing = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -376,10 +376,13 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         win = c->fbwin.as<uint32_t>();
         open = c->fbopen.as<uint32_t>();
     }
+    // the workgroup replay needs a 32-bit image of the output
+    uint32_t* p32 = nullptr;
+    if (!fb_serial_only() && c->fbp32.ensure(total * 4 + 16)) p32 = c->fbp32.as<uint32_t>();
     HIPCHK(launch_fb_resolve(d_in, c->fbs.as<uint64_t>(), c->fbch.as<uint32_t>(), c->fbco.as<uint64_t>(),
                              c->fbcs.as<uint64_t>(), nch, c->fbt.as<uint64_t>(), c->fbk.as<uint32_t>(),
                              c->fbu.as<FbUnit>(), c->fbimg.as<uint16_t>(), total, out, &ds->fb_err, win, open,
-                             st));
+                             p32, st));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     uint32_t ferr = 0;
     HIPCHK(hipMemcpyAsync(&ferr, &ds->fb_err, 4, hipMemcpyDeviceToHost, st));
@@ -820,7 +823,7 @@ void dmx_destroy(dmx_ctx* c) {
     for (DevBuf* b : {&c->in, &c->out, &c->slots, &c->sizes, &c->offs, &c->scal, &c->cands,
                       &c->tiles, &c->tileoffs, &c->recs, &c->status, &c->dbg, &c->ltok,
                       &c->ltokoff, &c->lntok, &c->lcaps, &c->lheavy, &c->rtmp, &c->rchain, &c->fbc, &c->fbh, &c->fbo, &c->fbl,
-                      &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg, &c->fbstop, &c->fbwin, &c->fbopen,
+                      &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg, &c->fbstop, &c->fbwin, &c->fbopen, &c->fbp32,
                       &c->ck})
         b->release();
     for (auto& e : c->ev)

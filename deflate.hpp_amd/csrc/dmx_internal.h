@@ -141,14 +141,15 @@ hipError_t launch_fb_decode(const uint32_t* in_words, uint64_t misalign, uint64_
 // replay + window hand-off + final resolve; *err (zeroed by the caller) becomes nonzero when a
 // copy reaches before the stream start.  win (fb_window_entries(nchain) words, 0 = not
 // available) and open (fb_window_rounds(nchain) words): the parallel hand-off; win == nullptr:
-// the serial one (k_fb_tails)
+// the serial one (k_fb_tails).  p32 (total words, or nullptr): the workgroup replay k_fb_units,
+// else the one-wave replay k_fb_replay
 uint64_t fb_window_entries(uint64_t nchain);
 uint32_t fb_window_rounds(uint64_t nchain);
 hipError_t launch_fb_resolve(const uint8_t* stream, const uint64_t* starts, const uint32_t* chain,
                              const uint64_t* offs, const uint64_t* sizes, uint64_t nchain,
                              const uint64_t* tokoff, const uint32_t* tok, const FbUnit* units,
                              uint16_t* img, uint64_t total, uint8_t* out, uint32_t* err,
-                             uint32_t* win, uint32_t* open, hipStream_t st);
+                             uint32_t* win, uint32_t* open, uint32_t* p32, hipStream_t st);
 // checksums (checksum.hip): scratch of checksum_scratch_bytes(n) bytes; results land in device
 // memory (*d_out).  CRC-32: the zero-start register; crc32_finish applies start value and xor.
 uint64_t checksum_scratch_bytes(uint64_t n);

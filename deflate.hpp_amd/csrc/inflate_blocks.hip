@@ -57,24 +57,32 @@ __device__ __forceinline__ uint32_t fb_bits(const uint32_t* w, uint32_t p) {  //
 }
 
 // Full check of a candidate whose precode is complete.  pl: 19 precode lengths (3 bits each,
-// by symbol).  p: bit position (in the staged image) of the first code-length symbol.
+// by symbol).  p: bit position (in the staged image) of the first code-length symbol.  lut: this
+// lane's 128-entry precode table in LDS (symbol | length << 5, 0 = no code), built here.
 // RFC 1951 rules as zlib's inflate enforces them; A-11/A-12 streams are not block starts any
 // real encoder writes, so rejecting them only costs parallelism.
 __device__ bool fb_check_lengths(const uint32_t* w, uint32_t p, uint64_t pl, uint32_t nlit,
-                                 uint32_t ndist, uint32_t plim) {
-    // canonical precode decoder "by counts": cnt[l] in 5-bit fields, symbols sorted by
-    // (length, value) in 5-bit fields of two words
-    uint64_t cnt = 0, sa = 0, sb = 0;
-    uint32_t ns = 0;
+                                 uint32_t ndist, uint32_t plim, uint8_t* lut) {
+    // canonical codes: counts per length (5-bit fields), first code per length (8-bit fields)
+    uint64_t cnt = 0;
+    for (uint32_t s = 0; s < 19; s++) {
+        const uint32_t l = (uint32_t)(pl >> (3 * s)) & 7;
+        cnt += l ? 1ull << (5 * l) : 0ull;
+    }
+    uint64_t nxt = 0;
+    uint32_t code = 0;
     for (uint32_t l = 1; l <= 7; l++) {
-        for (uint32_t s = 0; s < 19; s++) {
-            if (((pl >> (3 * s)) & 7) == l) {
-                if (ns < 12) sa |= (uint64_t)s << (5 * ns);
-                else sb |= (uint64_t)s << (5 * (ns - 12));
-                ns++;
-                cnt += 1ull << (5 * l);
-            }
-        }
+        code = (code + (uint32_t)((cnt >> (5 * (l - 1))) & 31)) << 1;  // (no length-0 count)
+        nxt |= (uint64_t)code << (8 * l);
+    }
+    for (uint32_t v = 0; v < 128; v += 4) *reinterpret_cast<uint32_t*>(lut + v) = 0;
+    for (uint32_t s = 0; s < 19; s++) {
+        const uint32_t l = (uint32_t)(pl >> (3 * s)) & 7;
+        if (!l) continue;
+        const uint32_t c = (uint32_t)(nxt >> (8 * l)) & 0xFF;
+        nxt += 1ull << (8 * l);
+        const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);
+        for (uint32_t v = r; v < 128; v += 1u << l) lut[v] = (uint8_t)(s | (l << 5));
     }
     const uint32_t total = nlit + ndist;
     uint32_t i = 0, prev = 0;
@@ -83,22 +91,9 @@ __device__ bool fb_check_lengths(const uint32_t* w, uint32_t p, uint64_t pl, uin
     while (i < total) {
         if (p > plim) return false;  // longer than any header a real encoder writes
         const uint32_t v = fb_bits(w, p);
-        // decode one precode symbol MSB-first from the bit-reversed stream order
-        uint32_t code = 0, first = 0, index = 0, sym = 0xFF, len = 0;
-        for (uint32_t l = 1; l <= 7; l++) {
-            code |= (v >> (l - 1)) & 1u;
-            const uint32_t c = (uint32_t)(cnt >> (5 * l)) & 31;
-            if (code - first < c) {
-                const uint32_t k = index + code - first;
-                sym = (uint32_t)((k < 12 ? sa >> (5 * k) : sb >> (5 * (k - 12))) & 31);
-                len = l;
-                break;
-            }
-            index += c;
-            first = (first + c) << 1;
-            code <<= 1;
-        }
-        if (sym == 0xFF) return false;
+        const uint32_t e = lut[v & 127];
+        if (!e) return false;
+        const uint32_t sym = e & 31, len = e >> 5;
         p += len;
         uint32_t val = sym, run = 1;
         if (sym == 16) {
@@ -140,23 +135,29 @@ __device__ bool fb_check_lengths(const uint32_t* w, uint32_t p, uint64_t pl, uin
 //      length is nonzero (~0.5 % pass);
 //   2. those, queued again, one per lane: fb_check_lengths.
 // Hits come out in offset order; the chunk keeps its first FB_HITS.
-__device__ __forceinline__ bool fb_precode(uint32_t h, const uint32_t* stg, uint32_t q, uint64_t* pl_out) {
+// stage 1: HCLEN + 4 precode lengths (3 bits each, in the kPerm order) form a complete code
+// and the last one sent is nonzero (zlib / libdeflate / libdmx send HCLEN up to the last nonzero
+// length, >= 4)
+__device__ __forceinline__ bool fb_precode_ok(uint32_t h, const uint32_t* stg, uint32_t q) {
     const uint32_t hclen = ((h >> 13) & 15) + 4;
     const uint32_t x0 = fb_bits(stg, q + 17), x1 = fb_bits(stg, q + 49);
-    const uint64_t x = (uint64_t)x0 | ((uint64_t)x1 << 32);
-    uint64_t pl = 0;
-    uint32_t kr = 0, lastl = 0;
+    uint32_t kr = 0;
+#pragma unroll
     for (uint32_t i = 0; i < 19; i++) {
-        if (i < hclen) {
-            const uint32_t l = (uint32_t)(x >> (3 * i)) & 7;
-            pl |= (uint64_t)l << (3 * kPerm[i]);
-            kr += l ? 128u >> l : 0u;
-            lastl = l;
-        }
+        const uint32_t l = i < 10 ? (x0 >> (3 * i)) & 7 : i == 10 ? ((x0 >> 30) | (x1 << 2)) & 7 : (x1 >> (3 * i - 32)) & 7;
+        kr += (i < hclen && l) ? 128u >> l : 0u;
     }
-    *pl_out = pl;
-    // zlib / libdeflate / libdmx send HCLEN up to the last nonzero length (>= 4)
-    return kr == 128 && (lastl != 0 || hclen == 4);
+    const uint32_t bl = 3 * (hclen - 1);
+    const uint32_t last = (uint32_t)((((uint64_t)x1 << 32) | x0) >> bl) & 7;
+    return kr == 128 && (last != 0 || hclen == 4);
+}
+// the precode lengths by symbol (3 bits each)
+__device__ __forceinline__ uint64_t fb_precode_lengths(uint32_t h, const uint32_t* stg, uint32_t q) {
+    const uint32_t hclen = ((h >> 13) & 15) + 4;
+    const uint64_t x = (uint64_t)fb_bits(stg, q + 17) | ((uint64_t)fb_bits(stg, q + 49) << 32);
+    uint64_t pl = 0;
+    for (uint32_t i = 0; i < hclen; i++) pl |= ((x >> (3 * i)) & 7) << (3 * kPerm[i]);
+    return pl;
 }
 
 __global__ __launch_bounds__(64) void k_fb_scan(const uint32_t* in_words, uint64_t misalign,
@@ -164,6 +165,7 @@ __global__ __launch_bounds__(64) void k_fb_scan(const uint32_t* in_words, uint64
     __shared__ uint32_t stg[FB_STAGE_WORDS + 2];
     __shared__ uint32_t q1[FB_STEP + 64];  // offsets r (bit 31: a stored-block hit)
     __shared__ uint32_t q2[128];
+    __shared__ __attribute__((aligned(4))) uint8_t luts[64 * 128];  // stage 2's precode tables
     const uint32_t lane = threadIdx.x;
     const uint64_t c = blockIdx.x;
     // stage words of the aligned image: bit 0 of word 0 = stream bit b0 - sh
@@ -200,10 +202,9 @@ __global__ __launch_bounds__(64) void k_fb_scan(const uint32_t* in_words, uint64
             } else {
                 const uint32_t q = sh + r;
                 const uint32_t h = fb_bits(stg, q);
-                uint64_t pl;
-                (void)fb_precode(h, stg, q, &pl);
-                hit = fb_check_lengths(stg, q + 17 + 3 * (((h >> 13) & 15) + 4), pl, ((h >> 3) & 31) + 257,
-                                       ((h >> 8) & 31) + 1, (FB_STAGE_WORDS - 1) * 32);
+                hit = fb_check_lengths(stg, q + 17 + 3 * (((h >> 13) & 15) + 4), fb_precode_lengths(h, stg, q),
+                                       ((h >> 3) & 31) + 257, ((h >> 8) & 31) + 1, (FB_STAGE_WORDS - 1) * 32,
+                                       luts + 128 * lane);
             }
         }
         const uint64_t hm = __ballot(hit);
@@ -228,8 +229,7 @@ __global__ __launch_bounds__(64) void k_fb_scan(const uint32_t* in_words, uint64
                 pass = true;
             } else {
                 const uint32_t q = sh + e;
-                uint64_t pl;
-                pass = fb_precode(fb_bits(stg, q), stg, q, &pl);
+                pass = fb_precode_ok(fb_bits(stg, q), stg, q);
             }
         }
         const uint64_t pm = __ballot(pass);
@@ -1171,6 +1171,113 @@ __global__ __launch_bounds__(64) void k_fb_replay(FbReplayArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------
+// k_fb_units: the replay as pointer jumping, one 1024-lane workgroup per unit on the chain
+// (replaces k_fb_replay's one wavefront, whose copies inside a 64-token group run one after
+// another).  In a 32-bit image P of the unit's output (unit-relative positions, in HBM/L2):
+//   1. the token words, 1024 at a time: block scan of their lengths gives each token's output
+//      offset; a literal writes final bytes, a match writes for each byte the position it
+//      copies from (periodic copies point into the first period), or -- for a position before
+//      the unit -- the final marker 0x8000 | (b - 1); stored blocks are copied by the whole
+//      workgroup from the stream;
+//   2. pointer jumping P[x] = P[P[x]] (up to four hops per entry per round, in place) until
+//      every entry is final (sources are always earlier positions);
+//   3. the low 16 bits -- a byte or a marker, k_fb_replay's image format -- to the image.
+// ---------------------------------------------------------------------------------------
+constexpr int FBR_NT = 1024;
+constexpr uint32_t FBR_FINAL = 0x80000000u;
+__global__ __launch_bounds__(FBR_NT) void k_fb_units(FbReplayArgs A, uint32_t* __restrict__ P) {
+    __shared__ uint32_t part[FBR_NT / 64];
+    __shared__ uint32_t slist[FBR_NT / 2][3];  // stored blocks of the chunk: offset, length, source
+    __shared__ uint32_t nst;
+    constexpr int NW = FBR_NT / 64;
+    const uint32_t t = threadIdx.x, wave = t >> 6;
+    const uint64_t ci = blockIdx.x;
+    const uint32_t u = A.chain[ci];
+    const FbUnit rec = A.units[u];
+    const uint64_t off = A.offs[ci];
+    const uint32_t* tk = A.tok + A.tokoff[u];
+    const uint32_t n = rec.ntok;
+    const uint8_t* sbase = A.stream + (A.starts[u] >> 3);  // stored offsets are relative to this byte
+    uint32_t* Pu = P + off;
+    bool bad = false;
+    uint32_t obase = 0;  // unit-relative output offset of the chunk
+    if (t == 0) nst = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += FBR_NT) {
+        const uint32_t ti = c0 + t;
+        const uint32_t w = ti < n ? tk[ti] : 0u;
+        const uint32_t wp = ti >= 1 && ti - 1 < n ? tk[ti - 1] : 0u;
+        // the word after a stored header (at an even index) is its offset: any 32-bit value
+        const bool isoff = (ti & 1) && !(wp >> 31) && ((wp >> 24) & 127) == 127;
+        const bool ism = (w >> 31) != 0 && !isoff;
+        const uint32_t cnt = (w >> 24) & 127;
+        const bool isst = !ism && !isoff && cnt == 127 && !(ti & 1);
+        const bool islit = !ism && !isst && !isoff && cnt >= 1 && cnt <= 3;
+        uint32_t L = ism ? (w >> 15) & 0xFFFFu : isst ? (w & 0xFFFFFFu) : islit ? cnt : 0u;
+        if (ti >= n) L = 0;
+        // block-wide exclusive scan of the lengths
+        const uint32_t inc = wave_incl_scan(L);
+        if ((t & 63) == 63) part[wave] = inc;
+        __syncthreads();
+        uint32_t before = 0, T = 0;
+#pragma unroll
+        for (int k = 0; k < NW; k++) {
+            const uint32_t v = part[k];
+            before += k < (int)wave ? v : 0u;
+            T += v;
+        }
+        const uint32_t go = obase + before + inc - L;
+        if (islit && L) {
+            Pu[go] = FBR_FINAL | (w & 0xFF);
+            if (cnt > 1) Pu[go + 1] = FBR_FINAL | ((w >> 8) & 0xFF);
+            if (cnt > 2) Pu[go + 2] = FBR_FINAL | ((w >> 16) & 0xFF);
+        } else if (ism && L) {
+            const uint32_t d = (w & 0x7FFFu) + 1;
+            if ((uint64_t)d > off + go) bad = true;  // a copy from before the stream start
+            uint32_t rr = 0;
+            for (uint32_t i = 0; i < L; i++) {
+                const uint32_t src = go + rr - d;  // as signed: the source position
+                Pu[go + i] = (int32_t)src >= 0 ? src : (FBR_FINAL | 0x8000u | (uint32_t)(-(int32_t)src - 1));
+                if (++rr == d) rr = 0;
+            }
+        } else if (isst && L) {
+            const uint32_t k = atomicAdd(&nst, 1u);
+            slist[k][0] = go;
+            slist[k][1] = L;
+            slist[k][2] = ti + 1 < n ? tk[ti + 1] : 0u;
+        }
+        __syncthreads();
+        const uint32_t ns = nst;
+        for (uint32_t k = 0; k < ns; k++) {
+            const uint32_t o = slist[k][0], len = slist[k][1];
+            const uint8_t* src = sbase + slist[k][2];
+            for (uint32_t j = t; j < len; j += FBR_NT) Pu[o + j] = FBR_FINAL | src[j];
+        }
+        __syncthreads();
+        if (t == 0) nst = 0;
+        obase += T;
+    }
+    __syncthreads();
+    const uint32_t total = obase;
+    bool open = true;
+    for (int round = 0; round < 32 && open; round++) {
+        bool pend = false;
+        for (uint32_t x = t; x < total; x += FBR_NT) {
+            uint32_t v = Pu[x];
+            if (v & FBR_FINAL) continue;
+#pragma unroll 1
+            for (int h = 0; h < 4 && !(v & FBR_FINAL); h++) v = Pu[v];
+            Pu[x] = v;
+            pend |= !(v & FBR_FINAL);
+        }
+        open = __syncthreads_or(pend) != 0;
+    }
+    if (open) bad = true;  // cannot happen: chains strictly go back
+    uint16_t* img = A.img + off;
+    for (uint32_t x = t; x < total; x += FBR_NT) img[x] = (uint16_t)Pu[x];
+    if (__syncthreads_or(bad) && t == 0) atomicOr(A.err, 1u);
+}
+
+// ---------------------------------------------------------------------------------------
 // k_fb_tails: the serial window hand-off.  One workgroup; for every unit on the chain, in
 // order, the markers of its last min(size, 32 KiB) entries are resolved against the last
 // 32 KiB of output before it (kept in LDS), the bytes go to the output, and the window moves.
@@ -1385,9 +1492,12 @@ hipError_t launch_fb_resolve(const uint8_t* stream, const uint64_t* starts, cons
                              const uint64_t* offs, const uint64_t* sizes, uint64_t nchain,
                              const uint64_t* tokoff, const uint32_t* tok, const FbUnit* units,
                              uint16_t* img, uint64_t total, uint8_t* out, uint32_t* err,
-                             uint32_t* win, uint32_t* open, hipStream_t st) {
+                             uint32_t* win, uint32_t* open, uint32_t* p32, hipStream_t st) {
     FbReplayArgs R{stream, starts, chain, offs, tokoff, tok, units, img, err};
-    hipLaunchKernelGGL(k_fb_replay, dim3((uint32_t)nchain), dim3(64), 0, st, R);
+    if (p32)
+        hipLaunchKernelGGL(k_fb_units, dim3((uint32_t)nchain), dim3(FBR_NT), 0, st, R, p32);
+    else
+        hipLaunchKernelGGL(k_fb_replay, dim3((uint32_t)nchain), dim3(64), 0, st, R);
     if (win) {
         const uint64_t nent = fb_window_entries(nchain);
         hipLaunchKernelGGL(k_fb_win_init, dim3((uint32_t)nchain, FB_RING / FB_WIN_BLK), dim3(256), 0, st,
