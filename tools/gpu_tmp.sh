@@ -1,10 +1,15 @@
+# scratch A/B script (developer aid; rewritten as needed)
 set -e
-mkdir -p gpurun_out && cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "deflate_roundtrip or compiled_reference" > gpurun_out/fm.log 2>&1 || { tail -30 gpurun_out/fm.log; exit 1; }
-tail -1 gpurun_out/fm.log
-rm -f gpurun_out/ab.txt
-for lib in ab/libdmx_l258.so deflate.hpp_amd/lib/libdmx.so ab/libdmx_l64.so ab/libdmx_l16.so; do
-  echo "== $lib" >> gpurun_out/ab.txt
-  DMX_LIB=$lib timeout -k 10 120 python tools/kernel_times.py 256 text,repeat,bmp,mixed 3 >> gpurun_out/ab.txt 2>&1
+mkdir -p gpurun_out && cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+rm -f gpurun_out/ph.txt; DMX_MIB=1024 DMX_KINDS=text timeout -k 10 200 python tools/phases.py gpurun_out/ph.txt 2>&1 | grep -v "^W\|^E" | grep -v "^deflate"
+for v in 2048 0; do
+  rm -rf gpurun_out/tmp_$v
+  DMX_RWG_MIN=$v timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/tmp_$v --output-format csv -- python3 tools/kernel_times.py 1024 text 2 > /dev/null 2>&1
+  python3 - "$v" <<'PY'
+import csv, glob, sys
+f = glob.glob(f"gpurun_out/tmp_{sys.argv[1]}/**/*kernel_stats.csv", recursive=True)[0]
+for r in csv.DictReader(open(f)):
+    if "inflate" in r['Name']:
+        print(f"RWG={sys.argv[1]:5s} {r['Name'][:48]:48s} {r['Calls']:>4s} {float(r['AverageNs'])/1e3:10.1f} us")
+PY
 done
-grep -v amdgpu.ids gpurun_out/ab.txt

@@ -19,7 +19,7 @@ for kind in os.environ.get("DMX_KINDS", "repeat,text,zeros").split(","):
     d_o = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     with open(out, "a") as f:
         f.write(f"# corpus {kind}\n")
-    for lvl in (2,):
+    for lvl in (int(os.environ.get("DMX_LEVEL", "2")),):
         clen = ctx.deflate_device(d_in.data_ptr(), n, lvl, d_c.data_ptr(), cap)
         kd = ctx.stats().ms_main_kernel
         olen = ctx.inflate_device(d_c.data_ptr(), clen, d_o.data_ptr(), n + 64)
