@@ -74,6 +74,13 @@ constexpr uint32_t DF_L3_ROUND = DMX_L3_ROUND;  // level 3: positions per link-b
 #endif
 constexpr bool DF_L3_LINK_ROUNDS = DMX_L3_LINK_ROUNDS != 0;
 // Level 3: positions per match round (the level-2 rounds take 2 * DF_NT = 2048)
+#ifndef DMX_L3_U
+#define DMX_L3_U 3
+#endif
+// level 3's chain search: 1 = the tail test as one unaligned 4-byte LDS read, 2 = also the match
+// lengths by unaligned 8-byte reads, 3 = those but the first link's length by aligned words
+// (0 = aligned words and alignbyte throughout)
+constexpr int DF_L3_U = DMX_L3_U;
 #ifndef DMX_L3_RP
 #define DMX_L3_RP 512
 #endif
@@ -349,6 +356,34 @@ __device__ __forceinline__ uint32_t matchlen(const uint32_t* w, uint32_t p, uint
         }
         if (x) {
             L += off + ((uint32_t)__builtin_ctz(x) >> 3);
+            break;
+        }
+        L += 16;
+    }
+    return min(L, maxl);
+}
+
+// gfx950 LDS takes unaligned 4- and 8-byte reads as one instruction each
+typedef uint32_t df_u32u __attribute__((aligned(1)));
+typedef uint64_t df_u64u __attribute__((aligned(1)));
+__device__ __forceinline__ uint32_t lds_rd32u(const uint32_t* w, uint32_t p) {
+    return *reinterpret_cast<const df_u32u*>(reinterpret_cast<const uint8_t*>(w) + p);
+}
+__device__ __forceinline__ uint64_t lds_rd64u(const uint32_t* w, uint32_t p) {
+    return *reinterpret_cast<const df_u64u*>(reinterpret_cast<const uint8_t*>(w) + p);
+}
+// matchlen with two unaligned 8-byte reads per side per 16 bytes (4 LDS reads instead of 10)
+__device__ __forceinline__ uint32_t matchlen_u(const uint32_t* w, uint32_t p, uint32_t q, uint32_t maxl) {
+    uint32_t L = 0;
+    while (L < maxl) {
+        const uint64_t x0 = lds_rd64u(w, p + L) ^ lds_rd64u(w, q + L);
+        const uint64_t x1 = lds_rd64u(w, p + L + 8) ^ lds_rd64u(w, q + L + 8);
+        if (x0) {
+            L += (uint32_t)__builtin_ctzll(x0) >> 3;
+            break;
+        }
+        if (x1) {
+            L += 8 + ((uint32_t)__builtin_ctzll(x1) >> 3);
             break;
         }
         L += 16;
@@ -1120,21 +1155,30 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                     // longer if the 4 bytes ending at offset bl match as well (zlib's scan_end
                     // test, widened): one word compare per link, the full length only for the
                     // links that pass.
+                    auto ml = [&](uint32_t a, uint32_t b, uint32_t m) {
+                        return DF_L3_U >= 2 ? matchlen_u(S.data32, a, b, m) : matchlen(S.data32, a, b, m);
+                    };
+                    auto rd = [&](uint32_t a) {
+                        return DF_L3_U >= 1 ? lds_rd32u(S.data32, a) : ld32u(S.data32, a);
+                    };
                     uint32_t q = p - d0;
-                    uint32_t bl = matchlen(S.data32, p, q, min(maxl, DF_L3_LONG));
+                    // (the first link with aligned words: neighbouring lanes read neighbouring
+                    // bytes here, which unaligned 8-byte reads serve slower -- repeat +46 %)
+                    uint32_t bl = DF_L3_U >= 3 ? matchlen(S.data32, p, q, min(maxl, DF_L3_LONG))
+                                               : ml(p, q, min(maxl, DF_L3_LONG));
                     if (bl >= 3) bd = d0;
                     else bl = 2;  // (a fingerprint collision: no match yet)
-                    uint32_t tail = bl >= 3 ? ld32u(S.data32, p + bl - 3) : 0u;
+                    uint32_t tail = bl >= 3 ? rd(p + bl - 3) : 0u;
                     for (int hop = 1; hop < DF_L3_DEPTH && bl < maxl && bl < DF_L3_LONG; hop++) {
                         const uint32_t dq = S.cand[q];
                         if (!dq) break;
                         q -= dq;
-                        if (bl >= 3 && ld32u(S.data32, q + bl - 3) != tail) continue;
-                        const uint32_t L = matchlen(S.data32, p, q, maxl);
+                        if (bl >= 3 && rd(q + bl - 3) != tail) continue;
+                        const uint32_t L = ml(p, q, maxl);
                         if (L > bl) {
                             bl = L;
                             bd = p - q;
-                            tail = ld32u(S.data32, p + bl - 3);
+                            tail = rd(p + bl - 3);
                         }
                     }
                 }
