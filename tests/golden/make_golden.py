@@ -151,15 +151,27 @@ def main():
     # 8. multi-block zlib streams of 1 MiB slices (cross-block back-references: the streams a
     #    marker-based decoder cannot split) and a Z_FULL_FLUSH stream (00 00 FF FF every 64 KiB
     #    with 15-bit codes)
+    #    Not committed: zgen.py rebuilds each from its spec and checks the recorded SHA-256.
+    from zgen import zgen_stream
+
+    def add_z(name, spec, how):
+        s = zgen_stream(spec)
+        d = dmx.corpus(spec["kind"], spec["n"], offset=spec["offset"])
+        ent = {"name": name, "zgen": spec, "stream_sha256": sha(s), "stream_len": len(s), "how": how}
+        try:
+            out = ref.decompress(s)
+            ent.update(ref_ok=True, out_sha256=sha(out), out_len=len(out), equals_original=out == d)
+        except CheckerError:
+            ent.update(ref_ok=False, ref_error="Reading bits beyond the alloted buffer size!")
+        man["vectors"].append(ent)
+
     for kind, lvl in (("text", 1), ("text", 6), ("bmp", 1), ("mixed", 1), ("repeat", 6), ("zeros", 1)):
-        d = dmx.corpus(kind, 1 << 20, offset=(1 << 20) * 5)
-        add(f"zmulti_{kind}1M_l{lvl}", raw(d, lvl, 0), f"zlib raw level {lvl} of 1 MiB '{kind}' at offset 5 MiB",
-            original=d)
-    d = dmx.corpus("text", 1 << 20, offset=(1 << 20) * 7)
-    z = zlib.compressobj(6, zlib.DEFLATED, -15, 9, 0)
-    fs = b"".join(z.compress(d[i:i + 65536]) + z.flush(zlib.Z_FULL_FLUSH) for i in range(0, len(d), 65536)) + z.flush()
-    add("zfullflush_text1M_l6", fs, "zlib raw level 6, Z_FULL_FLUSH every 64 KiB, 1 MiB 'text' at offset 7 MiB",
-        original=d)
+        add_z(f"zmulti_{kind}1M_l{lvl}", {"kind": kind, "n": 1 << 20, "offset": (1 << 20) * 5, "level": lvl,
+                                          "mem": 9, "strategy": 0},
+              f"zlib raw level {lvl} of 1 MiB '{kind}' at offset 5 MiB")
+    add_z("zfullflush_text1M_l6", {"kind": "text", "n": 1 << 20, "offset": (1 << 20) * 7, "level": 6, "mem": 9,
+                                   "strategy": 0, "flush_every": 65536, "flush": "full"},
+          "zlib raw level 6, Z_FULL_FLUSH every 64 KiB, 1 MiB 'text' at offset 7 MiB")
     # 9. config C3: the zlib level-1 raw stream of the full large.bmp stand-in.
     #    Too large to commit (6.2 MB): tests regenerate it with zlib and check its SHA-256 first.
     bmp = dmx.corpus("bmp", 25165962)

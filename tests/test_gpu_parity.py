@@ -3,6 +3,7 @@ the golden vectors made by the real reference, and zlib."""
 import hashlib
 import json
 import os
+import sys
 import random
 import subprocess
 import zlib
@@ -15,8 +16,10 @@ from oracle_bind import CheckerError, Reference
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, GOLD)
+from zgen import stream_of  # noqa: E402
 MAN = json.load(open(os.path.join(GOLD, "manifest.json")))
-VECS = [v for v in MAN["vectors"] if "stream" in v]
+VECS = [v for v in MAN["vectors"] if "stream" in v or "zgen" in v]
 
 
 def sha(b):
@@ -33,7 +36,7 @@ def zraw(d, lvl=6, st=0):
 # ---------------------------------------------------------------------------------------
 @pytest.mark.parametrize("v", VECS, ids=[v["name"] for v in VECS])
 def test_inflate_golden_vector(ctx, v):
-    s = open(os.path.join(GOLD, v["stream"]), "rb").read()
+    s = stream_of(v, GOLD)
     if v.get("reference_reads_past_buffer") or not v["ref_ok"]:
         with pytest.raises(dmx.DmxError):
             ctx.decompress(s)

@@ -3,6 +3,7 @@ vectors produced by the real reference (tests/golden/make_golden.py) and against
 import hashlib
 import json
 import os
+import sys
 import random
 import zlib
 
@@ -11,8 +12,10 @@ import pytest
 from oracle_bind import CheckerError, Oracle, Reference
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+sys.path.insert(0, GOLD)
+from zgen import stream_of  # noqa: E402
 MAN = json.load(open(os.path.join(GOLD, "manifest.json")))
-VECS = [v for v in MAN["vectors"] if "stream" in v]
+VECS = [v for v in MAN["vectors"] if "stream" in v or "zgen" in v]
 
 
 def sha(b):
@@ -21,7 +24,7 @@ def sha(b):
 
 @pytest.mark.parametrize("v", VECS, ids=[v["name"] for v in VECS])
 def test_oracle_matches_reference_vector(oracle, v):
-    s = open(os.path.join(GOLD, v["stream"]), "rb").read()
+    s = stream_of(v, GOLD)
     if v.get("reference_reads_past_buffer"):
         # the reference's result depends on the byte after the buffer (A-9); ours errors
         with pytest.raises(CheckerError):
