@@ -85,6 +85,11 @@ constexpr int DF_L3_U = DMX_L3_U;
 #define DMX_L3_RP 512
 #endif
 constexpr uint32_t DF_L3_RP = DMX_L3_RP;
+// level 2: run-continuation test of the match rounds (see run_rounds)
+#ifndef DMX_DF_SKIP
+#define DMX_DF_SKIP 0
+#endif
+constexpr bool DF_SKIP = DMX_DF_SKIP != 0;
 
 // ---------------------------------------------------------------------------------------
 // block primitives
@@ -972,6 +977,10 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         if (t < 288) S.litfreq[t] = 0;
         if (t < 32) { S.distfreq[t] = 0; S.prefreq[t] = 0; }
         if (t < NMAP) S.tokmap[t] = 0;
+        if (t == 0) {  // the match rounds' failed-test tag and candidate count
+            S.sh[42] = 0;
+            S.sh[44] = 0;
+        }
         if (level >= 2)
             for (int i = t; i < 2 * HT; i += DF_NT) S.U[i] = 0;
     }
@@ -1064,16 +1073,74 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                     constexpr uint32_t FPB = 17 - TAGB;  // fingerprint bits in the first entry
                     const bool act = RP >= 2 * DF_NT || t < (int)(RP / 2);
                     const uint32_t tt = RP >= 2 * DF_NT ? (uint32_t)t : (uint32_t)t & (RP / 2 - 1);
+                    // Run continuation (level 2): after a round in which at least 7/8 of the
+                    // positions found a candidate, the next round first tests whether all of its
+                    // positions repeat at one distance d (the candidate of the previous round's
+                    // last position): the key at p equals the key at p - d, verified on the bytes.
+                    // If so the round takes d as every candidate and skips the hash table (its
+                    // positions are never entered, so later rounds see older, farther occurrences
+                    // of those keys: still verified candidates), and the next round is tested with
+                    // the same d.  Long runs of one period (zeros, a repeated record, an image
+                    // row) cost one compare per position instead of two atomics and a lookup --
+                    // the parallel form of zlib not inserting the positions inside a long match
+                    // (deflate_fast's max_insert_length).  A failed test waits 1, 2, 4 .. 16 normal
+                    // rounds before the next.  LDS: sh[42] = tag (round + 1) of a failed test,
+                    // sh[44 + slot] = positions with a candidate in the current normal round.
+                    constexpr bool SKIP = DF_SKIP && RP == 2 * DF_NT;
+                    uint32_t skip_d = 0, slot = 0, wait = 0, backoff = 1;  // uniform (readfirstlane)
+                    bool pend = false;  // the previous round was a normal one (its count is read)
                     auto round = [&](uint32_t r0, uint32_t rr, RoundState& cur, const RoundState& prev, auto full) {
                         constexpr bool FULL = decltype(full)::value;
                         const uint32_t p0 = r0 + 2 * tt, p1 = p0 + 1;
                         const uint32_t i0 = p0 >> 2, sh = p0 & 3;  // sh = 0 or 2
                         const uint32_t wa = S.data32[i0], wb = S.data32[i0 + 1];
-                        const uint32_t prod0 = __builtin_amdgcn_alignbyte(wb, wa, sh) * 0x1E35A7BDu;
-                        const uint32_t prod1 = __builtin_amdgcn_alignbyte(wb, wa, sh + 1) * 0x1E35A7BDu;
+                        const uint32_t k0 = __builtin_amdgcn_alignbyte(wb, wa, sh);
+                        const uint32_t k1 = __builtin_amdgcn_alignbyte(wb, wa, sh + 1);
+                        const uint32_t prod0 = k0 * 0x1E35A7BDu;
+                        const uint32_t prod1 = k1 * 0x1E35A7BDu;
                         const bool ok0 = act && (FULL || p0 + 4 <= nb), ok1 = act && (FULL || p1 + 4 <= nb);
                         const uint32_t h0 = ok0 ? prod0 >> (32 - HB) : NOH, h1 = ok1 ? prod1 >> (32 - HB) : NOH;
                         const uint32_t fa0 = (prod0 >> (32 - HB - 16)) & 0xFFFFu, fa1 = (prod1 >> (32 - HB - 16)) & 0xFFFFu;
+                        // latest occurrence, for the previous round's positions: its p0 needs no update
+                        // when its p0 + 1 has the hash, p0 + 1 none when p0 + 2 (the next lane's) has it
+                        const uint32_t hn = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)(prev.ok0 ? prev.h0 : NOH), 0x101, 0xF, 0xF, false);
+                        if (prev.ok0 && prev.h0 != (prev.ok1 ? prev.h1 : NOH))
+                            atomicMax(&S.U[2 * prev.h0], ((prev.p0 + 1) << 16) | prev.f0);
+                        if (prev.ok1 && prev.h1 != hn) atomicMax(&S.U[2 * prev.h1], ((prev.p0 + 2) << 16) | prev.f1);
+                        if (SKIP && pend) {  // (these reads overlap the data words' latency)
+                            const uint32_t cov = __builtin_amdgcn_readfirstlane(S.sh[44 + (slot ^ 1)]);
+                            const uint32_t dl = __builtin_amdgcn_readfirstlane(S.cand[r0 - 1]);
+                            wait -= wait ? 1u : 0u;
+                            skip_d = (!wait && cov >= RP - RP / 8) ? dl : 0u;
+                            pend = false;
+#ifdef DMX_DF_SKIPDBG
+                            if (seg == 10 && t == 0) printf("seg %u round %u cov %u dl %u wait %u skip_d %u\n", (unsigned)seg, rr, cov, dl, wait, skip_d);
+#endif
+                        }
+                        if (SKIP && skip_d) {
+                            // p0 - skip_d >= 1: skip_d is a candidate of an earlier position
+                            // (aligned words: unaligned 8-byte LDS reads at neighbouring lanes' byte
+                            // offsets are served slowly)
+                            const uint32_t ia = (p0 - skip_d) >> 2, sa = 8 * ((p0 - skip_d) & 3);
+                            const uint32_t x0 = S.data32[ia], x1 = S.data32[ia + 1], x2 = S.data32[ia + 2];
+                            const uint64_t lo = ((uint64_t)x1 << 32) | x0;
+                            const uint64_t s = sa ? (lo >> sa) | ((uint64_t)x2 << (64 - sa)) : lo;
+                            const bool bad = (ok0 && (uint32_t)s != k0) || (ok1 && (uint32_t)(s >> 8) != k1);
+                            if (__ballot(bad) && (t & 63) == 0) S.sh[42] = rr + 1;
+                            __syncthreads();
+#ifdef DMX_DF_SKIPDBG
+                            if (seg == 10 && t == 0) printf("seg %u round %u test %s\n", (unsigned)seg, rr, S.sh[42] != rr + 1 ? "pass" : "fail");
+#endif
+                            if (__builtin_amdgcn_readfirstlane(S.sh[42]) != rr + 1) {
+                                if (act && (FULL || p0 < nb))
+                                    cand32[p0 >> 1] = (ok0 ? skip_d : 0u) | ((ok1 ? skip_d : 0u) << 16);
+                                cur = RoundState{NOH, NOH, p0, 0, 0, false, false};
+                                backoff = 1;
+                                return;
+                            }
+                            wait = backoff;
+                            backoff = min(2 * backoff, 16u);
+                        }
                         // first occurrence in this round: p1 needs no update when p0 has its hash, p0
                         // none when p0 - 1 (the previous lane's p1, by DPP within rows of 16) has it
                         const uint32_t hl = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)h1, 0x111, 0xF, 0xF, false);
@@ -1082,12 +1149,6 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                             atomicMax(&S.U[2 * h0 + 1], rtag | ((0x7FFFu - p0) << FPB) | (fa0 >> (16 - FPB)));
                         if (ok1 && h1 != h0)
                             atomicMax(&S.U[2 * h1 + 1], rtag | ((0x7FFFu - p1) << FPB) | (fa1 >> (16 - FPB)));
-                        // latest occurrence, for the previous round's positions: its p0 needs no update
-                        // when its p0 + 1 has the hash, p0 + 1 none when p0 + 2 (the next lane's) has it
-                        const uint32_t hn = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)(prev.ok0 ? prev.h0 : NOH), 0x101, 0xF, 0xF, false);
-                        if (prev.ok0 && prev.h0 != (prev.ok1 ? prev.h1 : NOH))
-                            atomicMax(&S.U[2 * prev.h0], ((prev.p0 + 1) << 16) | prev.f0);
-                        if (prev.ok1 && prev.h1 != hn) atomicMax(&S.U[2 * prev.h1], ((prev.p0 + 2) << 16) | prev.f1);
                         __syncthreads();
                         uint2 e0 = tab[ok0 ? h0 : 0u], e1 = tab[ok1 ? h1 : 0u];
                         // both halves now: otherwise the compiler sinks the head half of e0 into the
@@ -1102,8 +1163,17 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                             const uint32_t c = fr ? p - q : (lt ? p + 1u - (hd >> 16) : 0u);
                             return ok ? c : 0u;
                         };
-                        if (act && (FULL || p0 < nb)) cand32[p0 >> 1] = pick(e0, p0, fa0, ok0) | (pick(e1, p1, fa1, ok1) << 16);
+                        const uint32_t c0 = pick(e0, p0, fa0, ok0), c1 = pick(e1, p1, fa1, ok1);
+                        if (act && (FULL || p0 < nb)) cand32[p0 >> 1] = c0 | (c1 << 16);
                         cur = RoundState{h0, h1, p0, fa0, fa1, ok0, ok1};
+                        if (SKIP) {  // positions with a candidate (per-wave counts)
+                            const uint32_t nc = (uint32_t)__popcll(__ballot(c0 != 0u)) + (uint32_t)__popcll(__ballot(c1 != 0u));
+                            if ((t & 63) == 0) atomicAdd(&S.sh[44 + slot], nc);
+                            if (t == 0) S.sh[44 + (slot ^ 1)] = 0;  // the next normal round's count
+                            slot ^= 1;
+                            pend = FULL;
+                            skip_d = 0;
+                        }
                         __syncthreads();
                     };
                     using Full = std::integral_constant<bool, true>;
@@ -1301,12 +1371,47 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                             }
                         }
                     }
-                    if (best == c) {  // one probe at c / k, k the largest divisor <= 8 (a probe
-                                      // per k would serialize across lanes that differ in k)
+                    if (!DF_SKIP && best == c) {  // one probe at c / k, k the largest divisor <= 8 (a
+                                                  // probe per k would serialize across lanes that differ in k)
                         uint32_t k = 1;
 #pragma unroll
                         for (uint32_t q = 2; q <= 8; q++) k = (c % q == 0) ? q : k;
                         if (k > 1 && matchlen4(S.data32, p, p - c / k, ml, sub) >= L) best = c / k;
+                    }
+                    if (DF_SKIP && best == c) {
+                        // divisors c / k of the candidate, k <= 16 (the run-continuation rounds give
+                        // every position of a run the same, possibly far, multiple of the period): lane sub takes the (sub + 1)-th
+                        // largest k dividing c; one 16-byte compare round for the four, then full
+                        // lengths for those that passed, smallest distance first
+                        uint32_t k = 0, seen = 0;
+#pragma unroll
+                        for (uint32_t q = 16; q >= 2; q--) {
+                            const bool dv = c % q == 0;
+                            k = (dv && seen == sub) ? q : k;
+                            seen += dv ? 1u : 0u;
+                        }
+                        const uint32_t dk = k ? c / k : 0u;
+                        bool pass = false;
+                        if (dk > 4) {  // (1..4 were tested above)
+                            const uint32_t ip = p >> 2, sp = p & 3, iq = (p - dk) >> 2, sq = (p - dk) & 3;
+                            uint32_t x = 0;
+#pragma unroll
+                            for (int j = 0; j < 4; j++)
+                                x |= __builtin_amdgcn_alignbyte(S.data32[ip + j + 1], S.data32[ip + j], sp) ^
+                                     __builtin_amdgcn_alignbyte(S.data32[iq + j + 1], S.data32[iq + j], sq);
+                            pass = x == 0;
+                        }
+                        const int qb = lane_id() & ~3;
+                        uint32_t pm = (uint32_t)(__ballot(pass) >> qb) & 0xFu;
+                        while (pm) {
+                            const int f = __builtin_ctz(pm);
+                            pm &= pm - 1;
+                            const uint32_t d1 = (uint32_t)__shfl((int)dk, qb + f, 64);
+                            if (matchlen4(S.data32, p, p - d1, ml, sub) >= L) {
+                                best = d1;
+                                break;
+                            }
+                        }
                     }
                     if (lead) S.cand[p] = (uint16_t)best;
                 }

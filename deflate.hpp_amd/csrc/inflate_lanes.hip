@@ -69,6 +69,21 @@ static_assert(LN_HDR_QUADS * 16 <= LN_LENS, "header quads overlap the code lengt
 // so one wave of 32 segments beats two of 16 (1 GiB text inflate 12.3 -> 10.9 ms); the
 // table builds take the other half of the wave's lanes.
 constexpr uint32_t LN_LANES = DMX_LN_LANES;
+// token step: a literal followed by a literal decodes both (the step's second table lookup is the
+// distance code after a length, else the next lit/len symbol)
+#ifndef DMX_LN_PAIR
+#define DMX_LN_PAIR 1
+#endif
+// precode tables: one per lane, all segments at once (1), or built by the whole wave one segment
+// after the other (0, ln_coop_table)
+#ifndef DMX_LN_PRETAB
+#define DMX_LN_PRETAB 1
+#endif
+// resolve: the segment's last token, a periodic copy, written straight to HBM (1) or through the
+// window (0; measured faster: repeat inflate 0.629 vs 0.655 ms, zeros 0.468 vs 0.495 ms)
+#ifndef DMX_LN_DIRECT
+#define DMX_LN_DIRECT 0
+#endif
 
 __constant__ const uint8_t kLnPerm[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5,
                                           11, 4,  12, 3, 13, 2, 14, 1, 15};
@@ -237,6 +252,66 @@ __device__ __forceinline__ bool ln_lane_table(uint16_t* T, const Pk9& cnt, uint3
     return true;
 }
 
+// The precode table of one segment per lane: T[0, 128) as u8 entries sym | len << 5 for the
+// 19 precode lengths pl (3 bits each, by symbol), by the same canonical seeds and level doubling
+// as ln_lane_table (per-length counts and next codes packed in registers; from level 3 on the
+// doubling moves 8 entries per 8-byte word, the entries to copy picked by a per-byte compare of
+// their length fields).  0xFF marks an entry not yet written.  False unless the code is complete.
+__device__ __forceinline__ bool ln_lane_pretab(uint8_t* T, uint64_t pl) {
+    const uint32_t lane = lane_id();
+    uint64_t cnt = 0;  // per-length counts, 5 bits each, length L at 5 (L - 1)
+#pragma unroll
+    for (uint32_t s = 0; s < 19; s++) {
+        const uint32_t L = (uint32_t)(pl >> (3 * s)) & 7u;
+        cnt += L ? 1ull << (5 * (L - 1)) : 0ull;
+    }
+    uint32_t kraft = 0, code = 0, prev = 0;
+    uint64_t nc = 0;  // next code per length, 7 bits each
+#pragma unroll
+    for (uint32_t l = 1; l <= 7; l++) {
+        const uint32_t c = (uint32_t)(cnt >> (5 * (l - 1))) & 31u;
+        kraft += c << (7 - l);
+        code = (code + prev) << 1;
+        nc |= (uint64_t)code << (7 * (l - 1));
+        prev = c;
+    }
+    if (kraft != 128u) return false;
+    uint64_t* const T64 = reinterpret_cast<uint64_t*>(T);
+#pragma unroll
+    for (uint32_t w = 0; w < 16; w++) T64[(w + lane) & 15] = ~0ull;
+#pragma unroll
+    for (uint32_t s = 0; s < 19; s++) {
+        const uint32_t L = (uint32_t)(pl >> (3 * s)) & 7u;
+        if (L) {
+            const uint32_t c = (uint32_t)(nc >> (7 * (L - 1))) & 127u;
+            T[__builtin_bitreverse32(c) >> (32 - L)] = (uint8_t)(s | (L << 5));
+        }
+        nc += L ? 1ull << (7 * (L - 1)) : 0ull;
+    }
+    auto put = [&](uint32_t q, uint32_t e, uint32_t b) {
+        if ((e >> 5) <= b) T[q] = (uint8_t)e;
+    };
+    put(2, T[0], 1);
+    put(3, T[1], 1);
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) put(4 + i, T[i], 2);
+    constexpr uint64_t ONES = 0x0101010101010101ull;
+#pragma unroll
+    for (uint32_t b = 3; b < 7; b++) {
+        const uint32_t nw = 1u << (b - 3);  // words of level b
+#pragma unroll
+        for (uint32_t i = 0; i < nw; i++) {
+            const uint32_t q = (i + lane) & (nw - 1);
+            const uint64_t src = T64[q], dst = T64[q + nw];
+            const uint64_t lens = (src >> 5) & (7 * ONES);
+            const uint64_t gt = ((lens + (7 - b) * ONES) >> 3) & ONES;  // length > b
+            const uint64_t m = (gt ^ ONES) * 0xFFu;                      // bytes to copy
+            T64[q + nw] = (src & m) | (dst & ~m);
+        }
+    }
+    return true;
+}
+
 __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[LN_LANES * (LN_REGION + LN_PRE_BYTES)];
     const uint32_t lane = threadIdx.x;
@@ -354,6 +429,11 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
     const uint32_t dyn_mask = (uint32_t)__ballot(huff && btype == 2);
     // ---- precode tables of the dynamic segments, built by the wave (7-bit, u8 entries) -------
     uint32_t bad_mask = 0;
+#if DMX_LN_PRETAB
+    // one table per lane, all segments at once
+    if (huff && btype == 2 && !ln_lane_pretab(PRE, pl)) flags |= SEGF_EXOTIC;
+    wave_sync();
+#else
     for (uint32_t m = dyn_mask; m; m &= m - 1) {
         const uint32_t s = (uint32_t)__builtin_ctz(m);
         const uint64_t pls = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(pl >> 32), s) << 32) |
@@ -369,6 +449,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             [&](uint32_t x, uint32_t sym, uint32_t len) { tab[x] = (uint8_t)(sym | (len << 5)); });
         if (!ok) bad_mask |= 1u << s;
     }
+#endif
     if (seg_lane && ((bad_mask >> lane) & 1u)) flags |= SEGF_EXOTIC;
     if (dbg) dbg[1] = __builtin_amdgcn_s_memtime();
 
@@ -548,12 +629,26 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             const uint32_t L = (e & 255) + 3 + ((uint32_t)(win >> cl) & ((1u << ex) - 1u));
             const uint32_t n1 = cl + ex;
             const uint64_t dwin = win >> n1;
+#if DMX_LN_PAIR
+            // the second lookup from the same window: the distance code after a length, else the
+            // next lit/len symbol -- a literal after a literal is consumed in the same step
+            // (literal pairs at the cost of one step)
+            const uint32_t de = lut16(isl ? LN_DIST + 2 * ((uint32_t)dwin & 63u) : 2 * ((uint32_t)dwin & 511u));
+#else
             const uint32_t de = lut16(LN_DIST + 2 * ((uint32_t)dwin & 63u));
+#endif
             const uint32_t dcl = (de >> 8) & 7, ds = de & 31;
             const uint32_t dx = dist_extra(ds);
             const uint32_t d = dist_base(ds) + ((uint32_t)(dwin >> dcl) & ((1u << dx) - 1u));
             const uint32_t sym = e & 511;
+#if DMX_LN_PAIR
+            const uint32_t sym2 = de & 511, cl2 = (de >> 11) & 15;
+            const bool lit2 = !isl & (sym < 256) & ((de & 0x8000u) == 0u) & (sym2 < 256) &
+                              (outpos + 2 <= LN_OUT_CAP);
+            const uint32_t c = n1 + (isl ? dcl + dx : (lit2 ? cl2 : 0u));  // 1 .. 33 bits
+#else
             const uint32_t c = n1 + (isl ? dcl + dx : 0u);  // 1 .. 33 bits
+#endif
             const uint64_t ext = window_at(bp + 64, nq0, nq1);
             win = (win >> c) | ((ext << 1) << (63 - c));
             bp += c;
@@ -574,6 +669,30 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             const bool mt = isl & !far & ok;
             const bool lt = lit & ok;
             const bool prod = lt | mt;
+#if DMX_LN_PAIR
+            // nl literal bytes lb (1 or 2); a pending run of 2 takes the first of a pair and a
+            // new run starts with the second (lsplit)
+            const bool lt2 = lt & lit2;
+            const uint32_t nl = lt2 ? 2u : 1u;
+            const uint32_t lb = lt2 ? sym | (sym2 << 8) : sym;
+            const bool lcont = lt & (pk == 1u) & (pd + nl <= 3u);
+            const bool lsplit = lt2 & (pk == 1u) & (pd == 2u);
+            const bool mcont = mt & (pk == 2u) & (pd == d) & (pa + L <= 0xFFFFu);
+            const bool cont = lcont | mcont;
+            const bool emit = prod & !cont & (pk != 0u);
+            const uint32_t ew = lsplit ? (3u << 24) | pa | (sym << 16)
+                              : pk == 1u ? (pd << 24) | pa : 0x80000000u | (pa << 15) | (pd - 1u);
+            const uint32_t a_cont = lcont ? (pa | (lb << (8 * pd))) : (pa + L);
+            const uint32_t a_new = lsplit ? sym2 : lt ? lb : L;
+            const uint32_t d_cont = lcont ? pd + nl : pd;
+            const uint32_t d_new = lsplit ? 1u : lt ? nl : d;
+            const uint32_t npa = cont ? a_cont : a_new;
+            const uint32_t npd = cont ? d_cont : d_new;
+            pa = prod ? npa : pa;
+            pd = prod ? npd : pd;
+            pk = prod ? (lt ? 1u : 2u) : pk;
+            outpos += prod ? (lt ? nl : L) : 0u;
+#else
             const bool lcont = lt & (pk == 1u) & (pd < 3u);
             const bool mcont = mt & (pk == 2u) & (pd == d) & (pa + L <= 0xFFFFu);
             const bool cont = lcont | mcont;
@@ -589,6 +708,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             pd = prod ? npd : pd;
             pk = prod ? (lt ? 1u : 2u) : pk;
             outpos += prod ? (lt ? 1u : L) : 0u;
+#endif
             // queue of 4 token words (shift register), one 16-byte store per 4 words
             q0 = emit ? q1 : q0;
             q1 = emit ? q2 : q1;
@@ -767,19 +887,20 @@ __device__ __forceinline__ void ln_copy_plain(uint8_t* win, uint32_t o, uint32_t
 // (P >= Q + 16): every source quad lies in that prefix, so the rest of the match is one pass of
 // independent quad copies.  Lane phases advance by 1024 mod Q per wave-step (one division per
 // lane, at the start).
-__device__ __forceinline__ void ln_fill_mod(uint8_t* win, uint32_t o, uint32_t P, uint32_t L, uint32_t Q) {
+__device__ __forceinline__ uint32_t ln_fill_mod(uint8_t* win, uint32_t o, uint32_t P, uint32_t L, uint32_t Q,
+                                                uint8_t* out) {
     const uint32_t lane = lane_id();
     const uint32_t beg = o + P, end = o + L;
     const uint32_t a0 = min((beg + 15) & ~15u, end);
     const uint32_t a1 = max(a0, end & ~15u);
     if (lane < a0 - beg) win[beg + lane] = win[o + (P + lane) % Q];
-    else if (lane >= 16 && lane - 16 < end - a1) win[a1 + lane - 16] = win[o + (a1 - o + lane - 16) % Q];
+    else if (lane >= 16 && lane - 16 < end - a1) out[a1 + lane - 16] = win[o + (a1 - o + lane - 16) % Q];
     const uint32_t nq = (a1 - a0) >> 4;
-    if (nq <= lane) return;
+    if (nq <= lane) return a0;
     const uint32_t R = 1024u % Q;
     auto adv = [&](uint32_t r) { r += R; return r >= Q ? r - Q : r; };
     uint32_t r = (a0 - o + 16 * lane) % Q;  // phase of quad k = lane
-    uint4* const D = reinterpret_cast<uint4*>(win + a0);
+    uint4* const D = reinterpret_cast<uint4*>(out + a0);
     uint32_t k = lane;
     for (; k + 192 < nq; k += 256) {
         const uint32_t r1 = adv(r), r2 = adv(r1), r3 = adv(r2);
@@ -795,6 +916,7 @@ __device__ __forceinline__ void ln_fill_mod(uint8_t* win, uint32_t o, uint32_t P
         D[k] = ln_quad_at(win, o + r);
         r = adv(r);
     }
+    return a0;
 }
 
 // 8 bytes of the window at byte a (a < LN_OUT_CAP); near the window's end the read is moved
@@ -823,10 +945,14 @@ __device__ __forceinline__ void ln_store_tail(uint8_t* q, uint64_t x, uint32_t r
 // multiple of d that fits one byte per lane) is built directly; the prefix is doubled (a plain
 // copy of itself, P stays a multiple of d) until it holds a multiple Q >= 16 of d plus 16 bytes
 // and the rest is more than 3 prefixes long, then ln_fill_mod writes the rest in one pass.
-__device__ __forceinline__ void ln_copy_wave(uint8_t* win, uint32_t o, uint32_t L, uint32_t d) {
+// `out`: where that pass writes the bytes from its first 16-byte boundary on -- the window, or
+// for the segment's last token (nothing reads those bytes back) the segment's output in HBM.
+// Returns the window byte from which the output went to `out` (L + o when all of it is in the
+// window).
+__device__ __forceinline__ uint32_t ln_copy_wave(uint8_t* win, uint32_t o, uint32_t L, uint32_t d, uint8_t* out) {
     if (d >= L) {
         ln_copy_plain(win, o, o - d, L);
-        return;
+        return o + L;
     }
     uint32_t P;
     if (d >= 64) {
@@ -849,8 +975,9 @@ __device__ __forceinline__ void ln_copy_wave(uint8_t* win, uint32_t o, uint32_t 
     }
     if (P < L) {
         wave_sync();
-        ln_fill_mod(win, o, P, L, P - c16);
+        return ln_fill_mod(win, o, P, L, P - c16, out);
     }
+    return o + L;
 }
 
 // One segment of k_inflate_resolve: `sf` = its record's {out_size, flags}, n token words at tk.
@@ -891,6 +1018,9 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
     uint64_t* const dbg = (A.dbg && lane == 0) ? A.dbg + j * kPhaseSlots : nullptr;
     if (dbg) dbg[5] = __builtin_amdgcn_s_memtime();
     uint32_t pos = 0, n_cx = 0;
+    // the window holds the output below lim; the rest went straight to dst (see ln_copy_wave)
+    uint32_t lim = nb;
+    const bool direct = nb == size && (((uintptr_t)dst) & 15) == 0;
     uint64_t c_simple = 0, c_cx = 0, tstep0 = dbg ? __builtin_amdgcn_s_memtime() : 0;  // DMX_PHASES
     // One step = 64 token words, loaded one step ahead: the memory latency of the next step's
     // load passes while this step's copies run (unconditional, index clamped, so the wait before
@@ -950,7 +1080,9 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
             const uint32_t ok = (uint32_t)__builtin_amdgcn_readlane((int)off, k);
             const uint32_t Lk = (uint32_t)__builtin_amdgcn_readlane((int)L, k);
             const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)d, k);
-            ln_copy_wave(win, ok, Lk, dk);
+            const bool last = DMX_LN_DIRECT && direct && t0 + (uint32_t)k + 1 == n && ok + Lk == nb;
+            const uint32_t e = ln_copy_wave(win, ok, Lk, dk, last ? dst : win);
+            if (last) lim = e;
             wave_sync();
             n_cx++;
         }
@@ -973,7 +1105,7 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
         dbg[14] = c_cx;
     }
     if ((((uintptr_t)dst) & 15) == 0) {
-        const uint32_t nv = nb / 16;
+        const uint32_t nv = lim / 16;  // (lim < nb: a 16-byte boundary)
         const uint4* s4 = reinterpret_cast<const uint4*>(win);
         uint4* d4 = reinterpret_cast<uint4*>(dst);
         uint32_t i = lane;
@@ -985,7 +1117,7 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
             d4[i + 192] = v3;
         }
         for (; i < nv; i += 64) d4[i] = s4[i];
-        for (uint32_t i = nv * 16 + lane; i < nb; i += 64) dst[i] = win[i];
+        for (uint32_t i = nv * 16 + lane; i < lim; i += 64) dst[i] = win[i];
     } else {
         for (uint32_t i = lane; i < nb; i += 64) dst[i] = win[i];
     }
