@@ -85,9 +85,11 @@ constexpr int DF_L3_U = DMX_L3_U;
 #define DMX_L3_RP 512
 #endif
 constexpr uint32_t DF_L3_RP = DMX_L3_RP;
-// level 2: run-continuation test of the match rounds (see run_rounds)
+// level 2: run-continuation test of the match rounds (see run_rounds).  Measured on 1 GiB (ms):
+// repeat 4.18 -> 3.40, zeros 3.88 -> 3.26, bmp 4.05 -> 3.48, mixed 6.67 -> 6.60; the bookkeeping
+// costs text 8.89 -> 9.14 and random 5.48 -> 5.71 (no runs there)
 #ifndef DMX_DF_SKIP
-#define DMX_DF_SKIP 0
+#define DMX_DF_SKIP 1
 #endif
 constexpr bool DF_SKIP = DMX_DF_SKIP != 0;
 
@@ -977,10 +979,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         if (t < 288) S.litfreq[t] = 0;
         if (t < 32) { S.distfreq[t] = 0; S.prefreq[t] = 0; }
         if (t < NMAP) S.tokmap[t] = 0;
-        if (t == 0) {  // the match rounds' failed-test tag and candidate count
-            S.sh[42] = 0;
-            S.sh[44] = 0;
-        }
+        if (t == 0) S.sh[46] = 0;  // the match rounds' mismatch tag (run continuation)
         if (level >= 2)
             for (int i = t; i < 2 * HT; i += DF_NT) S.U[i] = 0;
     }
@@ -1065,6 +1064,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                     uint32_t h0, h1, p0, f0, f1;
                     bool ok0, ok1;
                 };
+                bool skipped = false;  // a round skipped by the run continuation (uniform)
                 auto run_rounds = [&](auto rpc) {
                     constexpr uint32_t RP = decltype(rpc)::value;
                     constexpr uint32_t NR = SEG / RP;
@@ -1073,25 +1073,41 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                     constexpr uint32_t FPB = 17 - TAGB;  // fingerprint bits in the first entry
                     const bool act = RP >= 2 * DF_NT || t < (int)(RP / 2);
                     const uint32_t tt = RP >= 2 * DF_NT ? (uint32_t)t : (uint32_t)t & (RP / 2 - 1);
-                    // Run continuation (level 2): after a round in which at least 7/8 of the
-                    // positions found a candidate, the next round first tests whether all of its
-                    // positions repeat at one distance d (the candidate of the previous round's
-                    // last position): the key at p equals the key at p - d, verified on the bytes.
-                    // If so the round takes d as every candidate and skips the hash table (its
-                    // positions are never entered, so later rounds see older, farther occurrences
-                    // of those keys: still verified candidates), and the next round is tested with
-                    // the same d.  Long runs of one period (zeros, a repeated record, an image
-                    // row) cost one compare per position instead of two atomics and a lookup --
-                    // the parallel form of zlib not inserting the positions inside a long match
-                    // (deflate_fast's max_insert_length).  A failed test waits 1, 2, 4 .. 16 normal
-                    // rounds before the next.  LDS: sh[42] = tag (round + 1) of a failed test,
-                    // sh[44 + slot] = positions with a candidate in the current normal round.
+                    // Run continuation (level 2): after a round whose last 128 positions all
+                    // found a candidate, the next round tests the rest of the segment at one
+                    // distance d (the candidate of that round's last position): the bytes at q
+                    // and q - d, 32 per thread, the first mismatch by an LDS atomic.  Every round
+                    // whose positions all lie before it (their 4-byte keys verified at d) takes d
+                    // as every candidate and skips the hash table: no atomics, no lookup, no
+                    // barrier (its positions are never entered, so later rounds see older,
+                    // farther occurrences of those keys: still verified candidates).  Long runs of
+                    // one period (zeros, a repeated record, an image row) cost one compare per
+                    // byte instead of two atomics and a lookup per position -- the parallel form of
+                    // zlib not inserting the positions inside a long match (deflate_fast's
+                    // max_insert_length).  A run that ends inside the tested round waits 1, 2, 4
+                    // .. 16 normal rounds before the next test.  LDS: sh[44] = that candidate (0:
+                    // no test), written by the round's last thread; sh[46] = (round + 1) << 16 |
+                    // 0xFFFF - first mismatch (atomicMax: no reset between rounds).
                     constexpr bool SKIP = DF_SKIP && RP == 2 * DF_NT;
-                    uint32_t skip_d = 0, slot = 0, wait = 0, backoff = 1;  // uniform (readfirstlane)
-                    bool pend = false;  // the previous round was a normal one (its count is read)
+                    uint32_t skip_d = 0, skip_end = 0, wait = 0, backoff = 1;  // uniform
+                    skipped = false;
+                    bool pend = false;  // the previous round was a normal one (sh[44] is read)
                     auto round = [&](uint32_t r0, uint32_t rr, RoundState& cur, const RoundState& prev, auto full) {
                         constexpr bool FULL = decltype(full)::value;
                         const uint32_t p0 = r0 + 2 * tt, p1 = p0 + 1;
+                        if (SKIP && skip_d) {
+                            if (r0 + RP <= skip_end || skip_end >= nb) {  // inside the verified run
+                                if (FULL || p0 < nb)
+                                    cand32[p0 >> 1] = (FULL || p0 + 4 <= nb ? skip_d : 0u) |
+                                                      ((FULL || p1 + 4 <= nb ? skip_d : 0u) << 16);
+                                cur = RoundState{NOH, NOH, p0, 0, 0, false, false};
+                                skipped = true;
+                                return;
+                            }
+                            skip_d = 0;
+                        }
+                        uint32_t dlr = 0;  // (issued first: its latency overlaps the data words')
+                        if (SKIP && pend) dlr = S.sh[44];
                         const uint32_t i0 = p0 >> 2, sh = p0 & 3;  // sh = 0 or 2
                         const uint32_t wa = S.data32[i0], wb = S.data32[i0 + 1];
                         const uint32_t k0 = __builtin_amdgcn_alignbyte(wb, wa, sh);
@@ -1101,55 +1117,73 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                         const bool ok0 = act && (FULL || p0 + 4 <= nb), ok1 = act && (FULL || p1 + 4 <= nb);
                         const uint32_t h0 = ok0 ? prod0 >> (32 - HB) : NOH, h1 = ok1 ? prod1 >> (32 - HB) : NOH;
                         const uint32_t fa0 = (prod0 >> (32 - HB - 16)) & 0xFFFFu, fa1 = (prod1 >> (32 - HB - 16)) & 0xFFFFu;
-                        // latest occurrence, for the previous round's positions: its p0 needs no update
-                        // when its p0 + 1 has the hash, p0 + 1 none when p0 + 2 (the next lane's) has it
-                        const uint32_t hn = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)(prev.ok0 ? prev.h0 : NOH), 0x101, 0xF, 0xF, false);
-                        if (prev.ok0 && prev.h0 != (prev.ok1 ? prev.h1 : NOH))
-                            atomicMax(&S.U[2 * prev.h0], ((prev.p0 + 1) << 16) | prev.f0);
-                        if (prev.ok1 && prev.h1 != hn) atomicMax(&S.U[2 * prev.h1], ((prev.p0 + 2) << 16) | prev.f1);
-                        if (SKIP && pend) {  // (these reads overlap the data words' latency)
-                            const uint32_t cov = __builtin_amdgcn_readfirstlane(S.sh[44 + (slot ^ 1)]);
-                            const uint32_t dl = __builtin_amdgcn_readfirstlane(S.cand[r0 - 1]);
-                            wait -= wait ? 1u : 0u;
-                            skip_d = (!wait && cov >= RP - RP / 8) ? dl : 0u;
-                            pend = false;
-#ifdef DMX_DF_SKIPDBG
-                            if (seg == 10 && t == 0) printf("seg %u round %u cov %u dl %u wait %u skip_d %u\n", (unsigned)seg, rr, cov, dl, wait, skip_d);
-#endif
-                        }
-                        if (SKIP && skip_d) {
-                            // p0 - skip_d >= 1: skip_d is a candidate of an earlier position
-                            // (aligned words: unaligned 8-byte LDS reads at neighbouring lanes' byte
-                            // offsets are served slowly)
-                            const uint32_t ia = (p0 - skip_d) >> 2, sa = 8 * ((p0 - skip_d) & 3);
-                            const uint32_t x0 = S.data32[ia], x1 = S.data32[ia + 1], x2 = S.data32[ia + 2];
-                            const uint64_t lo = ((uint64_t)x1 << 32) | x0;
-                            const uint64_t s = sa ? (lo >> sa) | ((uint64_t)x2 << (64 - sa)) : lo;
-                            const bool bad = (ok0 && (uint32_t)s != k0) || (ok1 && (uint32_t)(s >> 8) != k1);
-                            if (__ballot(bad) && (t & 63) == 0) S.sh[42] = rr + 1;
-                            __syncthreads();
-#ifdef DMX_DF_SKIPDBG
-                            if (seg == 10 && t == 0) printf("seg %u round %u test %s\n", (unsigned)seg, rr, S.sh[42] != rr + 1 ? "pass" : "fail");
-#endif
-                            if (__builtin_amdgcn_readfirstlane(S.sh[42]) != rr + 1) {
-                                if (act && (FULL || p0 < nb))
-                                    cand32[p0 >> 1] = (ok0 ? skip_d : 0u) | ((ok1 ? skip_d : 0u) << 16);
-                                cur = RoundState{NOH, NOH, p0, 0, 0, false, false};
-                                backoff = 1;
-                                return;
-                            }
-                            wait = backoff;
-                            backoff = min(2 * backoff, 16u);
-                        }
                         // first occurrence in this round: p1 needs no update when p0 has its hash, p0
                         // none when p0 - 1 (the previous lane's p1, by DPP within rows of 16) has it
+                        // (issued before the head updates, which do not wait for the data words: the
+                        // wait for the words then finds no atomic in flight)
                         const uint32_t hl = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)h1, 0x111, 0xF, 0xF, false);
                         const uint32_t rtag = rr << (32 - TAGB);
                         if (ok0 && h0 != hl)
                             atomicMax(&S.U[2 * h0 + 1], rtag | ((0x7FFFu - p0) << FPB) | (fa0 >> (16 - FPB)));
                         if (ok1 && h1 != h0)
                             atomicMax(&S.U[2 * h1 + 1], rtag | ((0x7FFFu - p1) << FPB) | (fa1 >> (16 - FPB)));
+                        // latest occurrence, for the previous round's positions: its p0 needs no update
+                        // when its p0 + 1 has the hash, p0 + 1 none when p0 + 2 (the next lane's) has it
+                        const uint32_t hn = (uint32_t)__builtin_amdgcn_update_dpp((int)NOH, (int)(prev.ok0 ? prev.h0 : NOH), 0x101, 0xF, 0xF, false);
+                        if (prev.ok0 && prev.h0 != (prev.ok1 ? prev.h1 : NOH))
+                            atomicMax(&S.U[2 * prev.h0], ((prev.p0 + 1) << 16) | prev.f0);
+                        if (prev.ok1 && prev.h1 != hn) atomicMax(&S.U[2 * prev.h1], ((prev.p0 + 2) << 16) | prev.f1);
+                        bool tested = false;
+                        if (SKIP && pend) {
+                            pend = false;
+                            const uint32_t dl = __builtin_amdgcn_readfirstlane(dlr);
+                            wait -= wait ? 1u : 0u;
+#ifdef DMX_DF_SKIPDBG
+                            if (seg == 10 && t == 0) printf("seg %u round %u dl %u wait %u\n", (unsigned)seg, rr, dl, wait);
+#endif
+                            if (!wait && dl) {
+                                // bytes [b, b + 32) against [b - dl, ...): 8 aligned words, 9 shifted
+                                tested = true;
+                                skip_d = dl;
+                                const uint32_t bq = r0 + 32 * (uint32_t)t;
+                                if (bq < nb) {
+                                    const uint32_t ia = (bq - dl) >> 2, sa = (bq - dl) & 3;
+                                    uint32_t x[9], y[8];
+#pragma unroll
+                                    for (int k = 0; k < 9; k++) x[k] = S.data32[ia + k];
+#pragma unroll
+                                    for (int k = 0; k < 8; k++) y[k] = S.data32[(bq >> 2) + k];
+                                    uint32_t mm = 0xFFFFFFFFu;
+#pragma unroll
+                                    for (int k = 7; k >= 0; k--) {
+                                        const uint32_t df = y[k] ^ __builtin_amdgcn_alignbyte(x[k + 1], x[k], sa);
+                                        mm = df ? bq + 4 * k + ((uint32_t)__builtin_ctz(df) >> 3) : mm;
+                                    }
+                                    if (mm != 0xFFFFFFFFu) atomicMax(&S.sh[46], ((rr + 1) << 16) | (0xFFFFu - mm));
+                                }
+                            }
+                        }
                         __syncthreads();
+                        if (SKIP && tested) {
+                            // positions p < m - 3 have their key verified at skip_d (m: first mismatch)
+                            const uint32_t mt = __builtin_amdgcn_readfirstlane(S.sh[46]);
+                            const uint32_t m = (mt >> 16) == rr + 1 ? 0xFFFFu - (mt & 0xFFFFu) : 0xFFFFFFFFu;
+                            skip_end = m >= nb ? nb : (m >= 3 ? m - 3 : 0u);
+#ifdef DMX_DF_SKIPDBG
+                            if (seg == 10 && t == 0) printf("seg %u round %u tested m %u skip_end %u\n", (unsigned)seg, rr, m, skip_end);
+#endif
+                            if (r0 + RP <= skip_end || skip_end >= nb) {  // this round is inside the run
+                                if (act && (FULL || p0 < nb))
+                                    cand32[p0 >> 1] = (ok0 ? skip_d : 0u) | ((ok1 ? skip_d : 0u) << 16);
+                                cur = RoundState{NOH, NOH, p0, 0, 0, false, false};
+                                backoff = 1;
+                                skipped = true;
+                                return;
+                            }
+                            skip_d = 0;
+                            wait = backoff;
+                            backoff = min(2 * backoff, 16u);
+                        }
                         uint2 e0 = tab[ok0 ? h0 : 0u], e1 = tab[ok1 ? h1 : 0u];
                         // both halves now: otherwise the compiler sinks the head half of e0 into the
                         // not-first-in-round branch, a second LDS round trip after the first
@@ -1166,13 +1200,12 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                         const uint32_t c0 = pick(e0, p0, fa0, ok0), c1 = pick(e1, p1, fa1, ok1);
                         if (act && (FULL || p0 < nb)) cand32[p0 >> 1] = c0 | (c1 << 16);
                         cur = RoundState{h0, h1, p0, fa0, fa1, ok0, ok1};
-                        if (SKIP) {  // positions with a candidate (per-wave counts)
-                            const uint32_t nc = (uint32_t)__popcll(__ballot(c0 != 0u)) + (uint32_t)__popcll(__ballot(c1 != 0u));
-                            if ((t & 63) == 0) atomicAdd(&S.sh[44 + slot], nc);
-                            if (t == 0) S.sh[44 + (slot ^ 1)] = 0;  // the next normal round's count
-                            slot ^= 1;
+                        if (SKIP) {  // the last wave: all its positions have a candidate?
+                            if (t >= DF_NT - 64) {
+                                const bool all = __ballot(c0 == 0u || c1 == 0u) == 0ull;
+                                if (t == DF_NT - 1) S.sh[44] = all ? c1 : 0u;
+                            }
                             pend = FULL;
-                            skip_d = 0;
                         }
                         __syncthreads();
                     };
@@ -1195,6 +1228,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                     run_rounds(std::integral_constant<uint32_t, DF_L3_RP>{});
                 else
                     run_rounds(std::integral_constant<uint32_t, 2 * DF_NT>{});
+                if (DF_SKIP && skipped) __syncthreads();  // skipped rounds end without a barrier
             }
             DMX_PHASE(A.dbg, seg, 14);
         }
