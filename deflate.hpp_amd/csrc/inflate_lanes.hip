@@ -489,23 +489,24 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
         uint32_t nxt = H[br.wi - hw0];  // the word at br.wi, read one step ahead
         // one precode symbol per step, outcome by selects (short-circuit && would branch)
         while (!flags && i < total) {
-            {   // >= 14 bits buffered: a precode code (<= 7 bits) and its repeat bits (<= 7)
+            {   // >= 14 bits buffered: a precode code (<= 7 bits) and its repeat bits (<= 7).
+                // Bytes past the stream end are not masked: a header that reads them ends past
+                // it, and the segment is then flagged (endbit > 8 E below) and decoded exactly.
                 const bool need = br.nb < 14;
-                const uint32_t wb = br.wi * 4;
-                const uint32_t rem = min(max(br.E, wb) - wb, 4u);  // stream bytes left in the word
-                const uint32_t w = nxt & (uint32_t)((1ull << (8 * rem)) - 1ull);
-                br.bb |= need ? (uint64_t)w << br.nb : 0ull;
+                br.bb |= need ? (uint64_t)nxt << br.nb : 0ull;
                 br.nb += need ? 32u : 0u;
                 br.wi += need ? 1u : 0u;
                 nxt = H[min(br.wi - hw0, 4 * LN_HDR_QUADS - 1)];
             }
             const uint32_t e = PRE[(uint32_t)(br.bb & 127)];
             const uint32_t len = e >> 5, sym = e & 31;
-            const uint32_t ex = sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u;
+            const bool lit = sym < 16;
+            // repeat codes 16 / 17 / 18: extra bits 2 / 3 / 7, base count 3 / 3 / 11 (nibbles)
+            const uint32_t rk = 4 * (sym - 16);
+            const uint32_t ex = lit ? 0u : (0x732u >> rk) & 15u;
             const uint32_t xv = (uint32_t)(br.bb >> len) & ((1u << ex) - 1u);
             br.consume(len + ex);
-            const bool lit = sym < 16;
-            const uint32_t run = lit ? 1u : (sym == 18 ? 11u : 3u) + xv;
+            const uint32_t run = lit ? 1u : ((0xB33u >> rk) & 15u) + xv;
             const uint32_t val = lit ? sym : (sym == 16 ? prev : 0u);
             const bool inl = i < hlit;
             const bool bad = ((sym == 16) & (!prevok | (i == hlit))) |  // A-12 / sequence-start repeat
