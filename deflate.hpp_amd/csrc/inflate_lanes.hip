@@ -193,7 +193,7 @@ __device__ __forceinline__ void pk_add(Pk9& p, uint32_t L) {  // L in 0..9 (0: n
 // come from its seed).  Entries not yet written hold `mark` (a length above B).  Index rotation
 // by lane keeps the lanes' accesses (regions 1152 B apart) off a common bank.  B >= 6.  Returns false
 // unless the code is complete.
-template <int B, class Word, class Ent>
+template <int B, int NL, class Word, class Ent>
 __device__ __forceinline__ bool ln_lane_table(uint16_t* T, const Pk9& cnt, uint32_t nsym, Word word, Ent ent,
                                               uint32_t lsh, uint32_t lmask, uint32_t mark) {
     const uint32_t lane = lane_id();
@@ -213,7 +213,20 @@ __device__ __forceinline__ bool ln_lane_table(uint16_t* T, const Pk9& cnt, uint3
     const uint64_t m4 = (uint64_t)(mark | (mark << 16)) * 0x0000000100000001ull;
 #pragma unroll 4
     for (uint32_t w = 0; w < NW / 2; w++) T64w[(w + lane) & (NW / 2 - 1)] = m4;
-    for (uint32_t k = 0; 8 * k < nsym; k++) {
+    // symbols below NL (a multiple of 8, < nsym): entry (L << lsh) | sym, no bound test
+    for (uint32_t k = 0; 8 * k < (uint32_t)NL; k++) {
+        const uint32_t x = word(k);
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++) {
+            const uint32_t sym = 8 * k + i, L = (x >> (4 * i)) & 15u;
+            if (L != 0u) {
+                const uint32_t c = pk_get(nc, L);
+                T[__builtin_bitreverse32(c) >> (32 - L)] = (uint16_t)((L << lsh) | sym);
+            }
+            pk_add(nc, L);
+        }
+    }
+    for (uint32_t k = NL / 8; 8 * k < nsym; k++) {
         const uint32_t x = word(k);
 #pragma unroll
         for (uint32_t i = 0; i < 8; i++) {
@@ -558,10 +571,10 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
         const uint32_t dw0 = PD[4], dw1 = PD[5], dw2 = PD[6], dw3 = PD[7];
         uint16_t* const lt = reinterpret_cast<uint16_t*>(R);
         uint16_t* const dt = reinterpret_cast<uint16_t*>(R + LN_DIST);
-        bool ok = ln_lane_table<9>(
+        bool ok = ln_lane_table<9, 256>(
             lt, cl, 288u, [&](uint32_t k) { return k < 32 ? PK[(k + lane) & 31] : PD[k - 32]; },
             [](uint32_t sym, uint32_t len) { return ln_lit_entry(sym, len); }, 11, 15, 0x7800u);
-        ok = ok && ln_lane_table<6>(
+        ok = ok && ln_lane_table<6, 0>(
             dt, cd, 32u, [&](uint32_t k) { return k == 0 ? dw0 : k == 1 ? dw1 : k == 2 ? dw2 : dw3; },
             [](uint32_t sym, uint32_t len) { return 0x8000u | (len << 8) | sym; }, 8, 7, 0x8700u);
         if (!ok) flags |= SEGF_EXOTIC;

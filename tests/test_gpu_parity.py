@@ -225,6 +225,45 @@ def test_deflate_roundtrip_oracle_zlib_gpu(oracle, seg, level):
     c.close()
 
 
+def _run_segments(seed):
+    """32 KiB segments built to exercise the match rounds' run continuation (deflate_kernels.hip,
+    run_rounds): a period p, a run start, a run end (mid-round, on a round edge, near the segment
+    end, or none), and what surrounds the run (random bytes, or a second period)."""
+    rnd = random.Random(seed)
+    segs = []
+    for period in (1, 2, 3, 7, 64, 251, 1000, 2047, 2048, 2049, 5000):
+        for start, end in ((0, 32768), (0, 9000), (100, 6144), (4096, 32760), (2048, 30000),
+                           (777, 20481), (0, 4099)):
+            pat = bytes(rnd.getrandbits(8) for _ in range(period))
+            seg = bytearray(rnd.getrandbits(8) for _ in range(32768))
+            if rnd.random() < 0.5:  # a different period around the run
+                alt = bytes(rnd.getrandbits(8) for _ in range(rnd.choice((5, 97, 300))))
+                seg = bytearray((alt * (32768 // len(alt) + 1))[:32768])
+            run = (pat * ((end - start) // period + 2))[:end - start]
+            seg[start:end] = run
+            segs.append(bytes(seg))
+    return segs
+
+
+def test_deflate_run_continuation_segments(ctx, oracle):
+    """Level 2's run continuation on runs of many periods that start and end at awkward offsets
+    (inside a round, on a round edge, in the last bytes of a segment), alone and concatenated
+    with other segments; every stream decodes to the input with the oracle, zlib and our inflate,
+    and a long periodic run costs a few bytes per 258."""
+    segs = _run_segments(7)
+    for k in range(0, len(segs), 11):
+        d = b"".join(segs[k:k + 11])
+        s = ctx.compress(d, 2)
+        assert oracle.inflate(s) == d, k
+        assert zlib.decompressobj(-15).decompress(s) == d, k
+        assert ctx.decompress(s) == d, k
+    d = segs[0]  # period 1 over the whole segment
+    assert len(ctx.compress(d * 64, 2)) < 64 * 200
+    d = bytes(random.Random(3).getrandbits(8) for _ in range(251)) * 4096  # the repeat corpus shape
+    s = ctx.compress(d, 2)
+    assert ctx.decompress(s) == d and len(d) / len(s) > 60
+
+
 @pytest.mark.skipif(not Reference.available(), reason="oracle/_ref not shipped")
 def test_deflate_decodes_with_compiled_reference(ctx):
     ref = Reference()
