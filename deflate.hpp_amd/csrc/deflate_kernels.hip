@@ -177,7 +177,10 @@ __device__ __forceinline__ void fit_classes(uint32_t (&cnt)[17], int maxbits) {
 // initial length round(log2(F/f)) clamped to [1, maxbits] (0 for f == 0)
 __device__ __forceinline__ uint32_t init_len(uint32_t f, uint32_t F, int maxbits) {
     if (!f) return 0;
-    const uint32_t L0 = 31 - __clz(F / f);
+    // floor(log2(F / f)) without a division: F / f lies in [2^(e-1), 2^(e+1)) for e = the
+    // difference of the leading-bit positions, and is >= 2^e exactly when f << e <= F
+    const uint32_t e = (uint32_t)(__clz(f) - __clz(F));
+    const uint32_t L0 = e - (((uint64_t)f << e) > F ? 1u : 0u);
     const uint64_t a = (uint64_t)f << (L0 + 1);
     const uint32_t L = L0 + ((a * a <= 2ull * F * F) ? 1u : 0u);
     return max(1u, min((uint32_t)maxbits, L));
@@ -611,7 +614,13 @@ __device__ void block_build_codes(DfSmem<SEG>& S, uint64_t* dbg, uint64_t seg) {
                 // rank in the order (initial length, symbol): symbols of shorter classes, the
                 // class members on earlier waves of the alphabet, then those below on this wave
                 uint32_t q = within0 + S.hb_kpre[a][k0];
-                for (int v = a ? 5 : 0; v < w; v++) q += S.hb_wcnt0[v][k0];
+                // (the earlier waves' counts as independent reads: one LDS latency, not w; the
+                // distance alphabet lies in wave 5 alone)
+#pragma unroll
+                for (int v = 0; v < 4; v++) {
+                    const uint32_t x = S.hb_wcnt0[v][k0];
+                    q += (!a && v < w) ? x : 0u;
+                }
 #pragma unroll
                 for (int l = 1; l <= 15; l++) L += q >= S.hb_start[a][l] ? 1u : 0u;
             }
@@ -648,7 +657,11 @@ __device__ void block_build_codes(DfSmem<SEG>& S, uint64_t* dbg, uint64_t seg) {
         uint32_t code = 0;
         if (L) {
             uint32_t c = S.hb_next[a][L] + within;
-            for (int v = 0; v < w && !a; v++) c += S.hb_wcnt[v][L];
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+                const uint32_t x = S.hb_wcnt[v][L];
+                c += (!a && v < w) ? x : 0u;
+            }
             code = (L << 16) | bitrev(c, L);
         }
         (a ? S.distcode : S.litcode)[s] = code;
