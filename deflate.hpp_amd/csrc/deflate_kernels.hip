@@ -1155,25 +1155,23 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                             if (seg == 10 && t == 0) printf("seg %u round %u dl %u wait %u\n", (unsigned)seg, rr, dl, wait);
 #endif
                             if (!wait && dl) {
-                                // bytes [b, b + 32) against [b - dl, ...): 8 aligned words, 9 shifted
+                                // words r0 / 4 + t + 1024 j (neighbouring lanes, neighbouring words:
+                                // no bank conflicts) against the words dl bytes before them
                                 tested = true;
                                 skip_d = dl;
-                                const uint32_t bq = r0 + 32 * (uint32_t)t;
-                                if (bq < nb) {
-                                    const uint32_t ia = (bq - dl) >> 2, sa = (bq - dl) & 3;
-                                    uint32_t x[9], y[8];
+                                const uint32_t sa = (r0 - dl) & 3;  // (r0 is a multiple of 4)
+                                uint32_t mm = 0xFFFFFFFFu;
 #pragma unroll
-                                    for (int k = 0; k < 9; k++) x[k] = S.data32[ia + k];
-#pragma unroll
-                                    for (int k = 0; k < 8; k++) y[k] = S.data32[(bq >> 2) + k];
-                                    uint32_t mm = 0xFFFFFFFFu;
-#pragma unroll
-                                    for (int k = 7; k >= 0; k--) {
-                                        const uint32_t df = y[k] ^ __builtin_amdgcn_alignbyte(x[k + 1], x[k], sa);
-                                        mm = df ? bq + 4 * k + ((uint32_t)__builtin_ctz(df) >> 3) : mm;
+                                for (int j = 7; j >= 0; j--) {
+                                    const uint32_t bq = r0 + 4 * ((uint32_t)t + DF_NT * j);
+                                    if (bq < nb) {
+                                        const uint32_t ia = (bq - dl) >> 2;
+                                        const uint32_t df = S.data32[bq >> 2] ^
+                                                            __builtin_amdgcn_alignbyte(S.data32[ia + 1], S.data32[ia], sa);
+                                        mm = df ? bq + ((uint32_t)__builtin_ctz(df) >> 3) : mm;
                                     }
-                                    if (mm != 0xFFFFFFFFu) atomicMax(&S.sh[46], ((rr + 1) << 16) | (0xFFFFu - mm));
                                 }
+                                if (mm != 0xFFFFFFFFu) atomicMax(&S.sh[46], ((rr + 1) << 16) | (0xFFFFu - mm));
                             }
                         }
                         __syncthreads();
