@@ -1086,8 +1086,8 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                     constexpr uint32_t FPB = 17 - TAGB;  // fingerprint bits in the first entry
                     const bool act = RP >= 2 * DF_NT || t < (int)(RP / 2);
                     const uint32_t tt = RP >= 2 * DF_NT ? (uint32_t)t : (uint32_t)t & (RP / 2 - 1);
-                    // Run continuation (level 2): after a round whose last 128 positions all
-                    // found a candidate, the next round tests the rest of the segment at one
+                    // Run continuation (level 2): after a round in which at least 120 of the last
+                    // 128 positions found a candidate, the next round tests the rest of the segment at one
                     // distance d (the candidate of that round's last position): the bytes at q
                     // and q - d, 32 per thread, the first mismatch by an LDS atomic.  Every round
                     // whose positions all lie before it (their 4-byte keys verified at d) takes d
@@ -1211,10 +1211,11 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                         const uint32_t c0 = pick(e0, p0, fa0, ok0), c1 = pick(e1, p1, fa1, ok1);
                         if (act && (FULL || p0 < nb)) cand32[p0 >> 1] = c0 | (c1 << 16);
                         cur = RoundState{h0, h1, p0, fa0, fa1, ok0, ok1};
-                        if (SKIP) {  // the last wave: all its positions have a candidate?
+                        if (SKIP) {  // the last wave: (nearly) all its positions have a candidate?
                             if (t >= DF_NT - 64) {
-                                const bool all = __ballot(c0 == 0u || c1 == 0u) == 0ull;
-                                if (t == DF_NT - 1) S.sh[44] = all ? c1 : 0u;
+                                // (>= 120 of its 128: collided hash buckets leave a few without)
+                                const uint32_t nc = (uint32_t)__popcll(__ballot(c0 != 0u)) + (uint32_t)__popcll(__ballot(c1 != 0u));
+                                if (t == DF_NT - 1) S.sh[44] = nc >= 120 ? c1 : 0u;
                             }
                             pend = FULL;
                         }
