@@ -1088,8 +1088,9 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                     const uint32_t tt = RP >= 2 * DF_NT ? (uint32_t)t : (uint32_t)t & (RP / 2 - 1);
                     // Run continuation (level 2): after a round in which at least 120 of the last
                     // 128 positions found a candidate, the next round tests the rest of the segment at one
-                    // distance d (the candidate of that round's last position): the bytes at q
-                    // and q - d, 32 per thread, the first mismatch by an LDS atomic.  Every round
+                    // distance d (the candidate of that round's last position): the words at q and
+                    // q - d, neighbouring lanes on neighbouring words (no bank conflicts), the first
+                    // mismatch by an LDS atomic.  Every round
                     // whose positions all lie before it (their 4-byte keys verified at d) takes d
                     // as every candidate and skips the hash table: no atomics, no lookup, no
                     // barrier (its positions are never entered, so later rounds see older,
