@@ -12,8 +12,8 @@ torch.distributed (RCCL over xGMI on MI355X nodes, gloo for the CPU tests):
   2. rank 0 receives every shard at its prefix offset (batched P2P), others send.
 
 deflate_gather() pipelines this: the shard is compressed in sub-shards, and each sub-shard's
-bytes go to rank 0 (into a staging slot) while the next one compresses; rank 0 packs the slots
-into the stream at the end.
+bytes go to rank 0 (into a staging slot) while the next one compresses; rank 0 compresses its
+own shard straight into the output and packs the other ranks' slots behind it at the end.
 """
 import torch
 import torch.distributed as dist
@@ -49,13 +49,16 @@ def gather_stream(local, clen, out=None):
     """Gather the compressed shards (local[:clen] on every rank) into out on rank 0.
 
     Returns the total stream length on every rank; on rank 0 out[:total] holds the stream.
-    Raises ValueError on EVERY rank when rank 0's out is missing or too small.
+    Raises ValueError on EVERY rank when rank 0's out is too small; out=None only asks for the
+    total (nothing is copied, the shards stay where they are).
     """
     rank, world = dist.get_rank(), dist.get_world_size()
     cap = out.numel() if (rank == 0 and out is not None) else -1
-    st = _all_gather_ints([clen, cap], local.device)
+    st = _all_gather_ints([clen, cap, 1 if out is None else 0], local.device)
     sizes = [s[0] for s in st]
     total = sum(sizes)
+    if st[0][2]:  # no output buffer on rank 0: the total only
+        return total
     if total and st[0][1] < total:
         raise ValueError("rank 0 needs an output buffer of at least the total stream size")
     if world == 1:
@@ -77,10 +80,14 @@ def deflate_gather(ctx, d_in, n, level, out=None, sub=4, align=32768):
     rank 0, the transfers pipelined behind the compression.
 
     The shard is cut into `sub` sub-shards (multiples of `align`), each compressed NOT_FINAL
-    (the last rank's last one final) into a staging slot; after sub-shard k, every rank sends
-    its length and then its bytes to rank 0 (asynchronous P2P) and goes on compressing k + 1.
-    Rank 0 posts the payload receives as soon as the lengths of step k are in, into per-rank
-    staging slots, and packs the pieces into out[:total] at the end (rank order, then k).
+    except the last rank's last NON-EMPTY one, which carries BFINAL (a last rank with no bytes
+    emits the empty final block 03 00, so the gathered stream always ends in BFINAL).  After
+    sub-shard k every rank r >= 1 sends its length and then its bytes to rank 0 (asynchronous
+    P2P) and goes on compressing k + 1.  Rank 0 compresses its own shard straight into `out`
+    (its bytes open the stream), posts the length receives of step k before compressing k + 1
+    and reads them only after it (one step of lag: rank 0's compression never waits for the
+    other ranks), then posts the payload receives into a per-rank staging buffer of the shard
+    bound; at the end it packs ranks 1.. behind its own bytes (rank order, then k).
     ctx: dmx.Context on this rank's GPU.  Returns (total stream bytes, this rank's bytes) on
     every rank; raises ValueError on every rank when rank 0's out is too small.
     """
@@ -90,8 +97,12 @@ def deflate_gather(ctx, d_in, n, level, out=None, sub=4, align=32768):
     last = rank == world - 1
     cuts = [min(n, -(-(n * k // sub) // align) * align) for k in range(sub + 1)]
     cuts[-1] = n
+    nonempty = [k for k in range(sub) if cuts[k + 1] > cuts[k]]
+    fin_k = (nonempty[-1] if nonempty else -1) if last else None
     slot = dmx.deflate_bound(max([1] + [b - a for a, b in zip(cuts, cuts[1:])])) + 64
-    stage = torch.empty(sub * slot, dtype=torch.uint8, device=dev)
+    cap0 = out.numel() if (rank == 0 and out is not None) else -1
+    direct = rank == 0 and cap0 >= sub * slot  # rank 0 compresses into out (room for any result)
+    stage = None if direct else torch.empty(sub * slot, dtype=torch.uint8, device=dev)
     lens = [0] * sub
     rlens = [[0] * sub for _ in range(world)]
     rstage = [None] * world
@@ -99,26 +110,45 @@ def deflate_gather(ctx, d_in, n, level, out=None, sub=4, align=32768):
         for r in range(1, world):
             rstage[r] = torch.empty(sub * slot, dtype=torch.uint8, device=dev)
     pend, keep = [], []
+    lag = None  # rank 0: (k, length tensors) whose payload receives are still to be posted
+
+    def post_payloads(k, got):  # the payload receives of step k (its lengths have arrived)
+        ops = []
+        for r in range(1, world):
+            Lr = int(got[r].item())
+            rlens[r][k] = Lr
+            if Lr:
+                ops.append(dist.P2POp(dist.irecv, rstage[r][k * slot: k * slot + Lr], r))
+        return ops
+
+    o0 = 0
     for k in range(sub):
         a, b = cuts[k], cuts[k + 1]
         L = 0
-        if b > a:
-            L = ctx.deflate_device(d_in.data_ptr() + a, b - a, level, stage.data_ptr() + k * slot, slot,
-                                   not_final=not (last and k == sub - 1))
+        if b > a or k == fin_k or (fin_k == -1 and k == sub - 1):
+            final = k == fin_k or (fin_k == -1 and k == sub - 1)
+            if direct:
+                dst, cap = out.data_ptr() + o0, slot
+            else:
+                dst, cap = stage.data_ptr() + k * slot, slot
+            L = ctx.deflate_device(d_in.data_ptr() + a, b - a, level, dst, cap, not_final=not final)
         lens[k] = L
+        if direct:
+            o0 += L
         if world == 1:
             continue
         if rank == 0:
+            # receives are posted in the order each rank sends (length k, payload k, length
+            # k + 1, ...): P2P matching per peer is in posting order (RCCL, gloo)
             got = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-            _p2p([dist.P2POp(dist.irecv, got[r], r) for r in range(1, world)])
             ops = []
-            for r in range(1, world):
-                Lr = int(got[r].item())
-                rlens[r][k] = Lr
-                if Lr:
-                    ops.append(dist.P2POp(dist.irecv, rstage[r][k * slot: k * slot + Lr], r))
-            if ops:
-                pend += dist.batch_isend_irecv(ops)
+            if lag is not None:
+                for q in lag[2]:
+                    q.wait()
+                ops = post_payloads(lag[0], lag[1])
+            ops += [dist.P2POp(dist.irecv, got[r], r) for r in range(1, world)]
+            reqs = dist.batch_isend_irecv(ops)
+            lag = (k, got, reqs)
         else:
             lt = torch.tensor([L], dtype=torch.int64, device=dev)
             keep.append(lt)
@@ -126,19 +156,24 @@ def deflate_gather(ctx, d_in, n, level, out=None, sub=4, align=32768):
             if L:
                 ops.append(dist.P2POp(dist.isend, stage[k * slot: k * slot + L], 0))
             pend += dist.batch_isend_irecv(ops)
+    if lag is not None:
+        for q in lag[2]:
+            q.wait()
+        ops = post_payloads(lag[0], lag[1])
+        if ops:
+            pend += dist.batch_isend_irecv(ops)
     for q in pend:
         q.wait()
     mine = sum(lens)
-    cap = out.numel() if (rank == 0 and out is not None) else -1
-    st = _all_gather_ints([mine, cap], dev) if world > 1 else [[mine, cap]]
+    st = _all_gather_ints([mine, cap0], dev) if world > 1 else [[mine, cap0]]
     total = sum(x[0] for x in st)
     if total and st[0][1] < total:
         raise ValueError("rank 0 needs an output buffer of at least the total stream size")
     if rank == 0:
         rlens[0] = lens
         rstage[0] = stage
-        o = 0
-        for r in range(world):
+        o = o0 if direct else 0
+        for r in range(1 if direct else 0, world):
             for k in range(sub):
                 L = rlens[r][k]
                 if L:

@@ -288,13 +288,13 @@ class _HostDeflate:
         return len(s)
 
 
-def _deflate_gather_worker(rank, world, port, total, sub, q):
+def _deflate_gather_worker(rank, world, port, total, sub, cuts, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import dmx
     data = dmx.corpus("mixed", total)
-    b, e = shard.shard_range(total, rank, world, SEG)
+    b, e = (cuts[rank], cuts[rank + 1]) if cuts else shard.shard_range(total, rank, world, SEG)
     d_in = torch.frombuffer(bytearray(data[b:e] or b"\0"), dtype=torch.uint8)
     out = torch.empty(2 * total + 4096, dtype=torch.uint8) if rank == 0 else None
     n, mine = shard.deflate_gather(_HostDeflate(), d_in, e - b, 0, out=out, sub=sub)
@@ -308,11 +308,24 @@ def test_deflate_gather_pipelined(oracle, world, sub):
     single valid stream as the one-shot gather: the oracle decodes it to the corpus."""
     import dmx
     total = 11 * SEG + 777
-    res = _run(_deflate_gather_worker, world, total, sub, all_ranks=True)
+    res = _run(_deflate_gather_worker, world, total, sub, None, all_ranks=True)
     stream = res[0]
     assert oracle.inflate(stream) == dmx.corpus("mixed", total)
     assert len(stream) == sum(v if r else 0 for r, v in res.items()) + \
         len(stream) - sum(v for r, v in res.items() if r)
+
+
+@pytest.mark.parametrize("last_bytes", [0, 100, 2 * SEG, 3 * SEG])
+def test_deflate_gather_short_last_shard(oracle, last_bytes):
+    """the last rank's last NON-EMPTY sub-shard carries BFINAL.  A last shard of 0
+    bytes (empty final block), of 100 bytes (sub-shards 1..3 empty) and of 2 or 3 segments with
+    sub = 4 (trailing sub-shards empty) must all gather into a stream that ends in BFINAL."""
+    import dmx
+    first = 3 * SEG + 555
+    total = first + last_bytes
+    res = _run(_deflate_gather_worker, 2, total, 4, [0, first, total], all_ranks=True)
+    stream = res[0]
+    assert oracle.inflate(stream) == dmx.corpus("mixed", total)
 
 
 def test_split_points():
