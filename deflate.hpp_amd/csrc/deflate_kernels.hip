@@ -272,75 +272,6 @@ __device__ void wave_assign_codes(const uint8_t* lens, int nsym, uint32_t* codes
     }
 }
 
-// LSB-first bit writer that ORs 32-bit words into an LDS image (image pre-zeroed).
-struct BitOr {
-    uint32_t* out;
-    uint64_t acc;
-    uint32_t nacc, wi;
-    __device__ void init(uint32_t* o, uint32_t bitpos) {
-        out = o;
-        wi = bitpos >> 5;
-        nacc = bitpos & 31;
-        acc = 0;
-    }
-    __device__ void put(uint32_t bits, uint32_t n) {  // n <= 32
-        acc |= (uint64_t)bits << nacc;
-        nacc += n;
-        if (nacc >= 32) {
-            atomicOr(&out[wi], (uint32_t)acc);
-            wi++;
-            acc >>= 32;
-            nacc -= 32;
-        }
-    }
-    __device__ void flush() {
-        if (nacc) atomicOr(&out[wi], (uint32_t)acc);
-    }
-};
-
-// The same for a thread that owns the bit range it writes: only the first and the last word
-// can be shared with a neighbouring range (atomicOr); the words between are plain stores.
-struct BitSt {
-    uint32_t* out;
-    uint64_t acc;
-    uint32_t nacc, wi;
-    bool shared;  // the current word is the range's first
-    __device__ void init(uint32_t* o, uint32_t bitpos) {
-        out = o;
-        wi = bitpos >> 5;
-        nacc = bitpos & 31;
-        acc = 0;
-        shared = true;
-    }
-    __device__ void put(uint32_t bits, uint32_t n) {  // n <= 32
-        acc |= (uint64_t)bits << nacc;
-        nacc += n;
-        if (nacc >= 32) {
-            if (shared) atomicOr(&out[wi], (uint32_t)acc);
-            else out[wi] = (uint32_t)acc;
-            shared = false;
-            wi++;
-            acc >>= 32;
-            nacc -= 32;
-        }
-    }
-    __device__ void put64(uint64_t bits, uint32_t n) {  // n <= 33 (nacc <= 31 on entry)
-        acc |= bits << nacc;
-        nacc += n;
-        while (nacc >= 32) {
-            if (shared) atomicOr(&out[wi], (uint32_t)acc);
-            else out[wi] = (uint32_t)acc;
-            shared = false;
-            wi++;
-            acc >>= 32;
-            nacc -= 32;
-        }
-    }
-    __device__ void flush() {
-        if (nacc) atomicOr(&out[wi], (uint32_t)acc);
-    }
-};
-
 // common prefix of the bytes at p and q, up to maxl; 16 bytes per step (five independent word
 // reads per side, one LDS latency per step).  The segment buffer is zero-padded past its end.
 __device__ __forceinline__ uint32_t matchlen(const uint32_t* w, uint32_t p, uint32_t q,
@@ -489,189 +420,22 @@ struct DfSmem {
     static constexpr int NWALK = (SEG + DF_CHUNK - 1) / DF_CHUNK;
     static constexpr int HB = df_hash_bits(SEG);
     static constexpr int HT = 1 << HB;  // entries per hash table
-    static constexpr int UW0 = 2 * HT;
-    static constexpr int UW1 = SEG / 4 + 64;
-    static constexpr int UW = UW0 > UW1 ? UW0 : UW1;
+    static constexpr int UW = 2 * HT;
     uint32_t data32[SEG / 4 + 32];  // + 128 B: matchlen4 reads up to 84 B past a match end
     alignas(16) uint16_t cand[SEG + 8];
-    // while matching: HT pairs {head, first} (one ds_read_b64 per lookup); the output bit image
-    // afterwards
+    // the match rounds' HT pairs {head, first} (one ds_read_b64 per lookup)
     alignas(16) uint32_t U[UW];
     uint32_t mmap[SEG / 32];    // "a verified match of >= 3 starts here" (match rounds)
     uint32_t tokmap[SEG / 32];  // token-start bitmap (parse walk; chunks share boundary words)
     uint16_t lasttok[NWALK + 1];  // last token start of each parse chunk
-    alignas(16) uint32_t litfreq[288];  // 16-B aligned: the rank count reads 4 at a time
-    alignas(16) uint32_t distfreq[32];
-    uint32_t prefreq[32];
-    uint32_t litcode[288];  // (len << 16) | bit-reversed code
-    uint32_t distcode[32];
-    uint32_t precode[32];
-    uint8_t litlen[288];
-    uint8_t distlen[32];
-    uint8_t prelen[32];
     uint32_t scan[4 * DF_NT / 64];
-    uint64_t runmask[6];
     uint32_t sh[48];
-    // block_build_codes: per-wave and per-alphabet sizes of the initial half-classes, class
-    // start ranks, next canonical code, per-wave length counts, F / used
-    uint32_t hb_wcnt0[6][32];
-    uint32_t hb_kcnt[2][32];
-    uint32_t hb_kpre[2][32];
-    uint32_t hb_start[2][16];
-    uint32_t hb_next[2][16];
-    uint32_t hb_wcnt[6][16];
-    uint32_t hb_sum[4];
-    uint32_t hb_used[2];
 };
-
-// Block-parallel code lengths and canonical codes of the lit/len code (286 symbols, threads
-// 0..285) and the distance code (30 symbols, threads 320..349), built side by side.  Initial
-// lengths round(log2(F/f)) clamped to [1, maxbits] (init_len), fit_classes on the class sizes,
-// then lengths by rank in the order (initial length, frequency half of the class, symbol): each
-// final class is a rank range, so a Kraft repair lengthens the last symbols of a class and a
-// slack fill shortens the first.  Inside a half-class the frequencies differ by less than
-// sqrt(2), so this order stays close to a frequency sort and needs none: ranks come from
-// per-wave ballots and counts (the 512-key bitonic sort it replaced was 7% of a high-ratio
-// segment's time).
-// Canonical codes (RFC 1951 3.2.2; reference FlatHuffmanTree::construct common.hpp:104-145)
-// from the final class sizes and per-wave ballots.  Also sums the token cost under the dynamic
-// and the fixed code (sh[32], sh[33]) and finds HLIT / HDIST (sh[34], sh[35]).  Stands in for
-// generateCodeLengths (common.hpp:322-404) and the cost compare of deflate.hpp:739-746.
-template <int SEG>
-__device__ void block_build_codes(DfSmem<SEG>& S, uint64_t* dbg, uint64_t seg) {
-    static_assert(DF_NT == 1024, "thread layout of block_build_codes");
-    const int t = df_tid(), lane = t & 63, w = t >> 6;
-    const int a = t >= 320 ? 1 : 0;  // alphabet of the symbol thread: 0 lit/len, 1 distance
-    const uint32_t s = a ? t - 320 : t;
-    const bool sym = a ? (s < 30) : (s < 286);
-    const uint32_t* const freq = a ? S.distfreq : S.litfreq;
-    const uint32_t f = sym ? freq[s] : 0;
-    const int maxbits = a ? DF_DIST_MAXBITS : DF_LIT_MAXBITS;
-    const uint64_t ltmask = (1ull << lane) - 1ull;
-    if (t < 64) S.hb_kcnt[t >> 5][t & 31] = 0;
-    if (t < 4) { S.hb_sum[t] = 0; S.sh[32 + t] = 0; }
-    if (t < 2) S.hb_used[t] = 0;
-    __syncthreads();
-    if (t < 384) {  // F, used count and highest used symbol, one atomic per wave
-        const uint32_t Fw = wave_sum(f);
-        const uint64_t nzm = __ballot(f != 0);
-        if (lane == 0 && nzm) {
-            atomicAdd(&S.hb_sum[2 * a], Fw);
-            atomicAdd(&S.hb_sum[2 * a + 1], (uint32_t)__popcll(nzm));
-            atomicMax(&S.hb_used[a], (uint32_t)((w - 5 * a) * 64 + 64 - __clzll(nzm)));
-        }
-    }
-    __syncthreads();
-    DMX_PHASE(dbg, seg, 12);
-    const uint32_t nz = S.hb_sum[2 * a + 1];
-    // class sizes of the initial lengths (lane k adds the wave's count of class k), per-wave
-    // class counts, and each symbol's rank among the wave's symbols of its class
-    // Symbols are ordered by half-classes k = 2 L0 + (f <= F / 2^L0): inside a class of initial
-    // length L0 the more frequent half comes first, then symbol order.
-    const uint32_t Fa = S.hb_sum[2 * a];
-    const uint32_t L0 = (t < 384 && sym) ? init_len(f, Fa, maxbits) : 0u;
-    const uint32_t k0 = L0 ? 2 * L0 + (((uint64_t)f << L0) <= Fa ? 1u : 0u) : 0u;
-    uint32_t within0 = 0;
-    if (t < 384) {
-        uint32_t mine = 0;
-#pragma unroll
-        for (int k = 2; k <= 2 * DF_LIT_MAXBITS + 1; k++) {
-            const uint64_t b = __ballot(k0 == (uint32_t)k);
-            mine = lane == k ? (uint32_t)__popcll(b) : mine;
-            within0 = k0 == (uint32_t)k ? (uint32_t)__popcll(b & ltmask) : within0;
-        }
-        if (mine) atomicAdd(&S.hb_kcnt[a][lane], mine);
-        if (lane < 32) S.hb_wcnt0[w][lane] = mine;
-    }
-    __syncthreads();
-    if (t == 0 || t == 320) {  // Kraft repair / slack fill on the class sizes, class starts,
-                               // next codes (two waves, in parallel)
-        uint32_t cnt[17];
-        cnt[0] = cnt[16] = 0;
-#pragma unroll
-        for (int L = 1; L <= 15; L++)
-            cnt[L] = nz > 1 ? S.hb_kcnt[a][2 * L] + S.hb_kcnt[a][2 * L + 1] : (L == 1 ? 2u : 0u);
-        if (nz > 1) fit_classes(cnt, maxbits);
-        uint32_t st = 0, code = 0;
-#pragma unroll
-        for (int L = 1; L <= 15; L++) {
-            S.hb_start[a][L] = st;
-            st += cnt[L];
-            code = (code + cnt[L - 1]) << 1;
-            S.hb_next[a][L] = code;
-        }
-    }
-    if (w == 2 || w == 3) {  // meanwhile: half-class start ranks (exclusive scans), one wave each
-        const uint32_t ka = w - 2, v = lane < 32 ? S.hb_kcnt[ka][lane] : 0u;
-        if (lane < 32) S.hb_kpre[ka][lane] = wave_incl_scan(v) - v;
-    }
-    __syncthreads();
-    DMX_PHASE(dbg, seg, 13);
-    uint32_t L = 0;
-    if (sym) {
-        if (nz > 1) {
-            if (f) {
-                // rank in the order (initial length, symbol): symbols of shorter classes, the
-                // class members on earlier waves of the alphabet, then those below on this wave
-                uint32_t q = within0 + S.hb_kpre[a][k0];
-                // (the earlier waves' counts as independent reads: one LDS latency, not w; the
-                // distance alphabet lies in wave 5 alone)
-#pragma unroll
-                for (int v = 0; v < 4; v++) {
-                    const uint32_t x = S.hb_wcnt0[v][k0];
-                    q += (!a && v < w) ? x : 0u;
-                }
-#pragma unroll
-                for (int l = 1; l <= 15; l++) L += q >= S.hb_start[a][l] ? 1u : 0u;
-            }
-        } else {  // zero or one used symbol: two codes of length 1 (a complete code, as zlib)
-            const uint32_t u = S.hb_used[a];
-            L = (s == (u ? u - 1 : 0u) || s == (u <= 1 ? 1u : 0u)) ? 1u : 0u;
-        }
-        (a ? S.distlen : S.litlen)[s] = (uint8_t)L;
-    }
-    uint32_t within = 0;
-    if (t < 384) {  // rank of the symbol among the wave's symbols of the same length
-        uint32_t mine = 0;
-#pragma unroll
-        for (int k = 1; k <= 15; k++) {
-            const uint64_t b = __ballot(L == (uint32_t)k);
-            within = L == (uint32_t)k ? (uint32_t)__popcll(b & ltmask) : within;
-            mine = lane == k ? (uint32_t)__popcll(b) : mine;
-        }
-        if (lane < 16) S.hb_wcnt[w][lane] = mine;
-        // token cost under the dynamic / fixed code, HLIT / HDIST
-        const uint32_t ex = a ? dist_extra(s) : (s > 256 ? len_extra(s) : 0);
-        const uint32_t dyn = sym ? f * (L + ex) : 0;
-        const uint32_t fix = sym ? f * ((a ? 5u : fixed_lit_len(s)) + ex) : 0;
-        const uint32_t dw = wave_sum(dyn), fw = wave_sum(fix);
-        const uint64_t used = __ballot(L != 0);
-        if (lane == 0) {
-            if (dw) atomicAdd(&S.sh[32], dw);
-            if (fw) atomicAdd(&S.sh[33], fw);
-            if (used) atomicMax(&S.sh[34 + a], (uint32_t)((w - 5 * a) * 64 + 64 - __clzll(used)));
-        }
-    }
-    __syncthreads();
-    if (sym) {
-        uint32_t code = 0;
-        if (L) {
-            uint32_t c = S.hb_next[a][L] + within;
-#pragma unroll
-            for (int v = 0; v < 4; v++) {
-                const uint32_t x = S.hb_wcnt[v][L];
-                c += (!a && v < w) ? x : 0u;
-            }
-            code = (L << 16) | bitrev(c, L);
-        }
-        (a ? S.distcode : S.litcode)[s] = code;
-    }
-}
 
 // Persistent workgroups: the next segment of this workgroup (seg + gridDim.x) is loaded straight
 // into the LDS byte image (global_load_lds, no registers) once the current segment's bytes are
-// dead -- after the token bits are counted, the emission reads only the candidate array -- so
-// its memory latency passes during the emission and the copy-out.  The loop's closing
+// dead -- after its token words are written -- so its memory latency passes during the stores
+// and the loop's bookkeeping.  The loop's closing
 // __syncthreads waits for it (an LDS-DMA load counts on vmcnt).
 template <int SEG>
 __device__ __forceinline__ bool df_prefetch_next(const DeflateArgs& A, uint64_t seg, DfSmem<SEG>& S) {
@@ -691,44 +455,6 @@ __device__ __forceinline__ bool df_prefetch_next(const DeflateArgs& A, uint64_t 
     return go;
 }
 
-// stored block: [BFINAL|00][LEN][NLEN][data] (+ empty stored block unless final)
-template <int SEG>
-__device__ void emit_stored(DfSmem<SEG>& S, uint32_t nb, bool is_final, uint8_t* slot,
-                            uint32_t* size_out) {
-    const int t = df_tid();
-    __syncthreads();
-    const uint32_t total = 5 + nb + (is_final ? 0 : 5);
-    const uint32_t nw = (total + 3) / 4;
-    // word k holds output bytes 4k..4k+3 = data bytes 4k-5 .. 4k-2
-    for (uint32_t k = t; k < nw; k += DF_NT) {
-        uint32_t v;
-        if (k == 0) {
-            v = (is_final ? 1u : 0u) | ((nb & 0xFF) << 8) | (((nb >> 8) & 0xFF) << 16) |
-                ((~nb & 0xFF) << 24);
-        } else if (k == 1) {
-            v = ((~nb >> 8) & 0xFF) | ((uint32_t)data_byte(S.data32, 0) << 8) |
-                ((uint32_t)data_byte(S.data32, 1) << 16) | ((uint32_t)data_byte(S.data32, 2) << 24);
-        } else {
-            v = ld32u(S.data32, 4 * k - 5);
-        }
-        uint32_t w = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const uint32_t pos = 4 * k + b;
-            uint32_t byte = (v >> (8 * b)) & 0xFF;
-            if (pos >= 5 + nb) byte = (!is_final && pos >= 5 + nb + 3) ? 0xFF : 0;
-            w |= byte << (8 * b);
-        }
-        S.U[k] = w;
-    }
-    __syncthreads();
-    const uint32_t nv = (total + 15) / 16;
-    const uint4* s4 = reinterpret_cast<const uint4*>(S.U);
-    uint4* d4 = reinterpret_cast<uint4*>(slot);
-    for (uint32_t i = t; i < nv; i += DF_NT) d4[i] = s4[i];
-    if (t == 0) *size_out = total;
-}
-
 // Token ranges: after the parse, thread t owns tokens [t K, (t + 1) K) of the segment in
 // position order (K = ceil(tokens / DF_NT)), found from per-word token counts of the token-start
 // bitmap.  Every thread then walks the same number of tokens (a wave iterates K times, not the
@@ -744,221 +470,6 @@ __device__ __forceinline__ uint32_t next_tok(const uint32_t* tokmap, uint32_t& w
     return p;
 }
 
-// Encodes the token starting at p (a literal if cand[p] == 0, else a match with distance
-// cand[p] and length cand[p + 1]) under the block's codes and returns its bit count.  The bit
-// pattern replaces the token's candidate entries, for the emission pass:
-//   literal  cand[p]     = 0x8000 | bits << 9 | code           (code <= 9 bits)
-//   match    cand[p]     = pattern bits 0..14                   (bit 15 clear: d < 32768)
-//            cand[p + 1] = pattern bits 15..30
-//            cand[p + 2] = pattern bits 31..32 | bits << 2      (bits <= 9+5+6+13 = 33)
-// cand[p + 2] lies inside the match (L >= 3): no other token reads it.
-template <int SEG>
-__device__ __forceinline__ uint32_t encode_token(DfSmem<SEG>& S, uint32_t p) {
-    const uint32_t d = S.cand[p];
-    if (d) {
-        const uint32_t L = S.cand[p + 1];
-        const uint32_t ls = len_sym(L), ds = dist_sym(d);
-        const uint32_t lc = S.litcode[ls], dc = S.distcode[ds];
-        uint64_t pat = lc & 0xFFFF;
-        uint32_t n = lc >> 16;
-        pat |= (uint64_t)(L - len_base(ls)) << n;
-        n += len_extra(ls);
-        pat |= (uint64_t)(dc & 0xFFFF) << n;
-        n += dc >> 16;
-        pat |= (uint64_t)(d - dist_base(ds)) << n;
-        n += dist_extra(ds);
-        S.cand[p] = (uint16_t)(pat & 0x7FFF);
-        S.cand[p + 1] = (uint16_t)(pat >> 15);
-        S.cand[p + 2] = (uint16_t)(((pat >> 31) & 3) | (n << 2));
-        return n;
-    }
-    const uint32_t lc = S.litcode[data_byte(S.data32, p)];
-    S.cand[p] = (uint16_t)(0x8000u | ((lc >> 16) << 9) | (lc & 0x1FF));
-    return lc >> 16;
-}
-
-// Huffman (dynamic or fixed) block for the tokenized segment; returns false when a stored
-// block would be smaller (the caller then emits it), true after writing the slot.
-template <int SEG>
-__device__ bool emit_huffman(const DeflateArgs& A, bool& staged, DfSmem<SEG>& S, const TokRange tr,
-                             uint32_t nb, bool is_final, uint8_t* slot, uint32_t* size_out, uint64_t* dbg,
-                             uint64_t seg) {
-    const int t = df_tid();
-
-    // ---- code lengths, canonical codes, token cost, HLIT / HDIST (whole block) -----------
-    block_build_codes<SEG>(S, dbg, seg);
-    __syncthreads();
-    DMX_PHASE(dbg, seg, 4);
-    const uint32_t dyn_tok = S.sh[32], fix_tok = S.sh[33];
-    const uint32_t nlit = max(257u, S.sh[34]), ndist = max(1u, S.sh[35]);
-    const uint32_t nall = nlit + ndist;
-
-    // ---- dynamic header: RLE runs over (litlen[0..nlit), distlen[0..ndist)) -------------
-    // run starts as a bitmap (one ballot per wave), each run start finds the next start
-    RunPlan plan = {0, 0, 0, 0, 0, 0, 0};
-    uint32_t runv = 0;
-    bool isrun = false;
-    {
-        const uint32_t i = t;
-        bool start = false;
-        uint32_t v = 0;
-        if (i < nall) {
-            v = i < nlit ? S.litlen[i] : S.distlen[i - nlit];
-            start = (i == 0 || i == nlit);
-            if (!start) {
-                const uint32_t pv = (i - 1) < nlit ? S.litlen[i - 1] : S.distlen[i - 1 - nlit];
-                start = pv != v;
-            }
-        }
-        const uint64_t bm = __ballot(start);
-        if (t < 6 * 64 && (t & 63) == 0) S.runmask[t >> 6] = bm;
-        __syncthreads();
-        if (start) {
-            uint32_t wq = (i + 1) >> 6;
-            uint64_t m = wq < 6 ? S.runmask[wq] & (~0ull << ((i + 1) & 63)) : 0;
-            while (!m && ++wq < 6) m = S.runmask[wq];
-            const uint32_t j = min(m ? wq * 64 + (uint32_t)__builtin_ctzll(m) : nall, nall);
-            isrun = true;
-            runv = v;
-            plan = plan_run(v, j - i);
-            if (plan.n18) atomicAdd(&S.prefreq[18], plan.n18);
-            if (plan.n17) atomicAdd(&S.prefreq[17], plan.n17);
-            if (plan.n16) atomicAdd(&S.prefreq[16], plan.n16);
-            if (plan.nlit) atomicAdd(&S.prefreq[v], plan.nlit);
-        }
-    }
-    __syncthreads();
-    if (t < 64) {
-        wave_build_lengths64(S.prefreq, 19, 7, S.prelen);
-        wave_assign_codes(S.prelen, 19, S.precode);
-    }
-    __syncthreads();
-    DMX_PHASE(dbg, seg, 6);
-    // HCLEN: one past the last nonzero precode length in RFC order, by one ballot per wave
-    const int ln = t & 63;
-    const uint32_t pv = ln < 19 ? S.prelen[kPerm[ln]] : 0u;
-    const uint64_t nzp = __ballot(pv != 0u);
-    const uint32_t hclen = max(4u, nzp ? 64u - (uint32_t)__clzll(nzp) : 0u);
-    const uint32_t runbits = isrun ? plan.n18 * (S.prelen[18] + 7) + plan.n17 * (S.prelen[17] + 3) +
-                                         plan.n16 * (S.prelen[16] + 2) + plan.nlit * S.prelen[runv]
-                                   : 0;
-    uint32_t rtot;
-    const uint32_t roff = block_excl_scan(runbits, S.scan, &rtot);
-    const uint32_t hdr_bits = 14 + 3 * hclen + rtot;  // after the 3-bit block header
-    DMX_PHASE(dbg, seg, 7);
-
-    // ---- choose the block type (reference deflate.hpp:739-746 picks the smallest too) ----
-    const uint64_t dyn_bits = 3ull + hdr_bits + dyn_tok;
-    const uint64_t fix_bits = 3ull + fix_tok;
-    const bool use_dyn = dyn_bits <= fix_bits;
-    const uint64_t bits = use_dyn ? dyn_bits : fix_bits;
-    const uint64_t hbytes = is_final ? (bits + 7) / 8 : (bits + 3 + 7) / 8 + 4;
-    const uint64_t stored_bytes = 5ull + nb + (is_final ? 0 : 5);
-    if (hbytes >= stored_bytes) return false;
-
-    if (!use_dyn) {
-        if (t < 286) S.litcode[t] = (fixed_lit_len(t) << 16) | fixed_lit_code(t);
-        if (t < 30) S.distcode[t] = (5u << 16) | bitrev(t, 5);
-        __syncthreads();
-    }
-
-    // ---- bits of the thread's token range, block scan -------------------------------------
-    uint32_t mybits = 0;
-    {
-        uint32_t w = tr.w, m = tr.m;
-        for (uint32_t i = 0; i < tr.n; i++) mybits += encode_token(S, next_tok(S.tokmap, w, m));
-    }
-    uint32_t tok_total;
-    const uint32_t myoff = block_excl_scan(mybits, S.scan, &tok_total);
-    const uint32_t hdr_end = 3 + (use_dyn ? hdr_bits : 0);
-    DMX_PHASE(dbg, seg, 8);
-    staged = df_prefetch_next<SEG>(A, seg, S);  // the segment's bytes are dead from here
-
-    // ---- emission into the zeroed LDS image ---------------------------------------------
-    if (t == 0) {
-        BitOr bw;
-        bw.init(S.U, 0);
-        bw.put((is_final ? 1u : 0u) | ((use_dyn ? 2u : 1u) << 1), 3);
-        if (use_dyn) {
-            bw.put(nlit - 257, 5);
-            bw.put(ndist - 1, 5);
-            bw.put(hclen - 4, 4);
-        }
-        bw.flush();
-    }
-    if (use_dyn && t < (int)hclen) {  // the precode lengths in RFC order, 3 bits each, in parallel
-        BitOr bw;
-        bw.init(S.U, 17 + 3 * t);
-        bw.put(pv, 3);
-        bw.flush();
-    }
-    if (use_dyn && isrun) {
-        BitOr bw;
-        bw.init(S.U, 3 + 14 + 3 * hclen + roff);
-        const uint32_t v = runv;
-        if (v == 0) {
-            const uint32_t c18 = S.precode[18] & 0xFFFF, l18 = S.precode[18] >> 16;
-            for (uint32_t q = 0; q < plan.n18; q++) {
-                const uint32_t rep = (q + 1 == plan.n18) ? plan.last18 : 138;
-                bw.put(c18, l18);
-                bw.put(rep - 11, 7);
-            }
-            if (plan.n17) {
-                bw.put(S.precode[17] & 0xFFFF, S.precode[17] >> 16);
-                bw.put(plan.r17 - 3, 3);
-            }
-            for (uint32_t q = 0; q < plan.nlit; q++) bw.put(S.precode[0] & 0xFFFF, S.precode[0] >> 16);
-        } else {
-            const uint32_t cv = S.precode[v] & 0xFFFF, lv = S.precode[v] >> 16;
-            bw.put(cv, lv);
-            const uint32_t c16 = S.precode[16] & 0xFFFF, l16 = S.precode[16] >> 16;
-            for (uint32_t q = 0; q < plan.n16; q++) {
-                const uint32_t rep = (q + 1 == plan.n16) ? plan.last16 : 6;
-                bw.put(c16, l16);
-                bw.put(rep - 3, 2);
-            }
-            for (uint32_t q = 1; q < plan.nlit; q++) bw.put(cv, lv);
-        }
-        bw.flush();
-    }
-    DMX_PHASE(dbg, seg, 5);
-    if (tr.n) {
-        BitSt bw;
-        bw.init(S.U, hdr_end + myoff);
-        uint32_t w = tr.w, m = tr.m;
-        for (uint32_t i = 0; i < tr.n; i++) {
-            const uint32_t p = next_tok(S.tokmap, w, m);
-            const uint32_t v0 = S.cand[p], v1 = S.cand[p + 1], v2 = S.cand[p + 2];
-            if (v0 & 0x8000) bw.put(v0 & 0x1FF, (v0 >> 9) & 15);
-            else bw.put64((uint64_t)v0 | ((uint64_t)v1 << 15) | ((uint64_t)(v2 & 3) << 31), v2 >> 2);
-        }
-        bw.flush();
-    }
-    // end of block, then (non-final) the byte-aligning empty stored block 000|pad|0000|FFFF
-    const uint32_t eob_at = hdr_end + tok_total;
-    const uint32_t eob = S.litcode[256];
-    const uint32_t end_bits = eob_at + (eob >> 16);
-    const uint32_t total = is_final ? (end_bits + 7) / 8 : (end_bits + 3 + 7) / 8 + 4;
-    if (t == 0) {
-        BitOr bw;
-        bw.init(S.U, eob_at);
-        bw.put(eob & 0xFFFF, eob >> 16);
-        bw.flush();
-        if (!is_final) {
-            atomicOr(&S.U[(total - 2) >> 2], 0xFFu << (((total - 2) & 3) * 8));
-            atomicOr(&S.U[(total - 1) >> 2], 0xFFu << (((total - 1) & 3) * 8));
-        }
-    }
-    __syncthreads();
-    DMX_PHASE(dbg, seg, 9);
-    const uint32_t nv = (total + 15) / 16;
-    const uint4* s4 = reinterpret_cast<const uint4*>(S.U);
-    uint4* d4 = reinterpret_cast<uint4*>(slot);
-    for (uint32_t i = t; i < nv; i += DF_NT) d4[i] = s4[i];
-    if (t == 0) *size_out = total;
-    return true;
-}
-
 template <int SEG>
 __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG>& S, uint64_t seg,
                                                 bool& staged) {
@@ -968,9 +479,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
     const int t = df_tid();
     const uint64_t base = seg * (uint64_t)SEG;
     const uint32_t nb = (uint32_t)min((uint64_t)SEG, A.n - base);
-    const bool is_final = (seg + 1 == A.nseg) && A.final_last;
     const int level = A.level;
-    uint8_t* const slot = A.slots + seg * (uint64_t)A.slot_bytes;
     uint8_t* const dbytes = reinterpret_cast<uint8_t*>(S.data32);
     DMX_PHASE(A.dbg, seg, 0);
 
@@ -989,8 +498,6 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         }
         // zero padding after the data (match compares read up to 8 bytes past)
         for (uint32_t i = nb + t; i < ((nb + 3) & ~3u) + 32; i += DF_NT) dbytes[i] = 0;
-        if (t < 288) S.litfreq[t] = 0;
-        if (t < 32) { S.distfreq[t] = 0; S.prefreq[t] = 0; }
         if (t < NMAP) S.tokmap[t] = 0;
         if (t == 0) S.sh[46] = 0;  // the match rounds' mismatch tag (run continuation)
         if (level >= 2)
@@ -1469,13 +976,6 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
             if (tok && lead) atomicOr(&S.tokmap[w], tok);
             if (lead) S.lasttok[t >> 2] = (uint16_t)lastp;
         }
-        if (level < 2) {  // Huffman only: every position is a literal token
-            for (uint32_t i = t; i < nb; i += DF_NT) S.cand[i] = 0;
-            if (t < NMAP) {
-                const uint32_t b0 = t * 32;
-                S.tokmap[t] = b0 >= nb ? 0u : (nb - b0 >= 32 ? 0xFFFFFFFFu : ((1u << (nb - b0)) - 1u));
-            }
-        }
         __syncthreads();
         DMX_PHASE(A.dbg, seg, 3);
 
@@ -1577,30 +1077,44 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
             tr.m = m & (0xFFFFFFFFu << b);
         }
         DMX_PHASE(A.dbg, seg, 15);
-        // ---- histogram over the thread's tokens; the output image is zeroed meanwhile ------
+        // ---- token words for k_deflate_emit, in position order: literal runs of up to three
+        //      bytes per word, one word per match (count, block scan of the counts, write) -----
         {
-            uint32_t w = tr.w, m = tr.m;
-            for (uint32_t i = 0; i < tr.n; i++) {
-                const uint32_t p = next_tok(S.tokmap, w, m);
-                const uint32_t d = S.cand[p];
-                if (d) {
-                    atomicAdd(&S.litfreq[len_sym(S.cand[p + 1])], 1u);
-                    atomicAdd(&S.distfreq[dist_sym(d)], 1u);
-                } else {
-                    atomicAdd(&S.litfreq[data_byte(S.data32, p)], 1u);
+            auto walk = [&](auto emit) {
+                uint32_t w = tr.w, m = tr.m, lit = 0, nl = 0;
+                for (uint32_t i = 0; i < tr.n; i++) {
+                    const uint32_t p = next_tok(S.tokmap, w, m);
+                    const uint32_t d = S.cand[p];
+                    if (d) {
+                        if (nl) emit(lit | (nl << 24));
+                        nl = 0;
+                        lit = 0;
+                        emit(0x80000000u | ((uint32_t)(S.cand[p + 1] - 3) << 16) | (d - 1));
+                    } else {
+                        lit |= (uint32_t)data_byte(S.data32, p) << (8 * nl);
+                        if (++nl == 3) {
+                            emit(lit | (3u << 24));
+                            nl = 0;
+                            lit = 0;
+                        }
+                    }
                 }
-            }
+                if (nl) emit(lit | (nl << 24));
+            };
+            uint32_t nw = 0;
+            walk([&](uint32_t) { nw++; });
+            uint32_t wtot;
+            const uint32_t woff = block_excl_scan(nw, S.scan, &wtot);
+            uint32_t* const dst = A.tok + seg * (uint64_t)A.tok_stride + woff;
+            uint32_t j = 0;
+            walk([&](uint32_t v) { dst[j++] = v; });
+            if (t == 0) A.ntok[seg] = wtot;
         }
-        for (int i = t; i < DfSmem<SEG>::UW; i += DF_NT) S.U[i] = 0;
-        if (t == 0) atomicAdd(&S.litfreq[256], 1u);  // end-of-block
-        __syncthreads();
         DMX_PHASE(A.dbg, seg, 11);
-        if (emit_huffman<SEG>(A, staged, S, tr, nb, is_final, slot, &A.sizes[seg], A.dbg, seg)) {
-            DMX_PHASE(A.dbg, seg, 10);
-            return;
-        }
+        __syncthreads();  // every read of the segment's bytes is done
+        staged = df_prefetch_next<SEG>(A, seg, S);
+        DMX_PHASE(A.dbg, seg, 10);
     }
-    emit_stored<SEG>(S, nb, is_final, slot, &A.sizes[seg]);
 }
 
 // The 32 KiB kernel is limited to one workgroup per CU by its LDS (~146 KiB), so the compiler may
@@ -1624,6 +1138,524 @@ __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
 __global__ __launch_bounds__(DF_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_deflate_segments16(DeflateArgs A) {
     __shared__ DfSmem<16384> S;
     deflate_segments<16384>(A, S);
+}
+
+// ---------------------------------------------------------------------------------------
+// k_deflate_emit: the entropy stage, ONE WAVEFRONT PER SEGMENT.  k_deflate_segments leaves
+// each level-2/3 segment's tokens in HBM as 32-bit words in position order:
+//     match        1 | L - 3 (8) << 16 | d - 1 (15)
+//     literal run  0 | count (2) << 24 | up to three bytes (24), first byte lowest
+// (level 1: the input's own words, four literals each; level 0: none).  A wave takes one
+// segment: histogram (LDS atomics into its own table), length-limited lit/len and distance
+// codes (em_build_codes), the RLE of the two code-length sequences and the precode, the block
+// type by exact size (dynamic / fixed / stored, as the reference's compare deflate.hpp:739-746),
+// then the bit packing: blocks of 256 token words, four consecutive words per lane, one wave
+// scan of their bit counts, the patterns ORed into an LDS staging window that goes to the
+// segment's HBM slot in whole words.  Every step is wave-synchronous (no workgroup barrier):
+// the serial parts of a segment (the code build, the header) overlap other segments' work in
+// the other waves of the CU instead of idling fifteen waves of a 1024-thread workgroup.
+// ---------------------------------------------------------------------------------------
+constexpr int EM_NW = 4;          // waves (segments) per 256-thread workgroup
+constexpr int EM_FLUSH = 256;     // staged whole words that trigger a flush to HBM
+constexpr int EM_STG = 576;       // staging words: EM_FLUSH + one block (256 x 36 bits) + slack
+constexpr int EM_LIT = 288, EM_SYM = 320;  // lit/len symbols at [0, 288), distance at [288, 320)
+
+struct EmWave {
+    uint32_t freq[EM_SYM];
+    uint32_t code[EM_SYM];   // (len << 16) | bit-reversed code
+    uint8_t len[EM_SYM];
+    uint16_t rk[EM_SYM];     // per symbol slot: half-class | rank in it, then rank in its length;
+                             // per header position: run length (run starts), then run bit offset
+    uint32_t prefreq[20];
+    uint32_t precode[20];
+    uint8_t prelen[24];
+    uint32_t hcnt[6][20];    // per chunk of 64 symbols: members of half-class k (k < 20)
+    uint32_t lcnt[6][16];    // per chunk: members of code length l
+    uint32_t kpre[2][20];    // per alphabet: members of the half-classes below k
+    uint32_t start[2][16];   // per alphabet: first rank of code length l
+    uint32_t next[2][16];    // per alphabet: first canonical code of length l
+    uint32_t stg[EM_STG];
+};
+
+struct EmCodes {
+    uint32_t dyn_tok, fix_tok;  // token bits under the dynamic / the fixed code (EOB included)
+    uint32_t nlit, ndist;       // HLIT + 257, HDIST + 1
+};
+
+// symbol slot c of a lane: lit/len symbol 64 c + lane (c < 5) or distance symbol lane (c = 5)
+__device__ __forceinline__ uint32_t em_slot(int c, int lane) { return c < 5 ? 64 * c + lane : EM_LIT + lane; }
+__device__ __forceinline__ bool em_valid(int c, int lane) { return c < 5 ? 64 * c + lane < 286 : lane < 30; }
+
+// One-wave form of the block-parallel code build the 1024-thread kernel used (same lengths,
+// same codes): initial lengths round(log2 F/f) clamped to the limit, order (initial length,
+// frequency half of the class, symbol) by ballots per 64-symbol chunk, Kraft repair / slack fill
+// on the class sizes (fit_classes), lengths by rank ranges, canonical codes (RFC 1951 3.2.2;
+// reference FlatHuffmanTree::construct common.hpp:104-145).  Per-symbol state lives in LDS
+// (W.rk), not in registers.  Stands in for generateCodeLengths (common.hpp:322-404); the costs
+// feed the size compare of deflate.hpp:739-746.
+__device__ EmCodes em_build_codes(EmWave& W) {
+    const int lane = lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t Fl = 0, nzl = 0, hil = 0;
+    for (int c = 0; c < 5; c++) {
+        const uint32_t f = em_valid(c, lane) ? W.freq[em_slot(c, lane)] : 0u;
+        Fl += f;
+        const uint64_t b = __ballot(f != 0);
+        nzl += (uint32_t)__popcll(b);
+        if (b) hil = 64 * c + 64 - (uint32_t)__clzll(b);
+    }
+    Fl = wave_sum(Fl);
+    const uint32_t f5 = lane < 30 ? W.freq[EM_LIT + lane] : 0u;
+    const uint32_t Fd = wave_sum(f5);
+    const uint64_t bd = __ballot(f5 != 0);
+    const uint32_t nzd = (uint32_t)__popcll(bd), hid = bd ? 64 - (uint32_t)__clzll(bd) : 0u;
+    // half-classes, their per-chunk counts (lane k holds the count of half-class k), ranks
+    for (int c = 0; c < 6; c++) {
+        const uint32_t f = em_valid(c, lane) ? W.freq[em_slot(c, lane)] : 0u;
+        const uint32_t F = c < 5 ? Fl : Fd;
+        const uint32_t L0 = init_len(f, F, c < 5 ? DF_LIT_MAXBITS : DF_DIST_MAXBITS);
+        const uint32_t k0 = L0 ? 2 * L0 + (((uint64_t)f << L0) <= F ? 1u : 0u) : 0u;
+        uint32_t mine = 0, w0 = 0;
+#pragma unroll
+        for (int k = 2; k <= 2 * DF_LIT_MAXBITS + 1; k++) {
+            const uint64_t b = __ballot(k0 == (uint32_t)k);
+            mine = lane == k ? (uint32_t)__popcll(b) : mine;
+            w0 = k0 == (uint32_t)k ? (uint32_t)__popcll(b & lt) : w0;
+        }
+        if (lane < 20) W.hcnt[c][lane] = mine;
+        W.rk[64 * c + lane] = (uint16_t)(k0 | (w0 << 5));
+    }
+    wave_sync();
+    // class sizes per alphabet (lanes 0..19: lit/len, 32..51: distance), start ranks of the
+    // half-classes (exclusive scan over k), then fit_classes and the class starts / next codes
+    {
+        const int a = lane >= 32 ? 1 : 0, k = lane & 31;
+        uint32_t v = 0;
+        if (k < 20) {
+            if (a) v = W.hcnt[5][k];
+            else v = W.hcnt[0][k] + W.hcnt[1][k] + W.hcnt[2][k] + W.hcnt[3][k] + W.hcnt[4][k];
+        }
+        uint32_t inc = v;  // inclusive scan inside each half (rows of 32 lanes)
+#pragma unroll
+        for (int d = 1; d < 32; d <<= 1) {
+            const uint32_t u = __shfl_up(inc, d, 64);
+            if (k >= d) inc += u;
+        }
+        if (k < 20) W.kpre[a][k] = inc - v;
+        uint32_t cnt[17];
+        cnt[0] = cnt[16] = 0;
+        const uint32_t nz = a ? nzd : nzl;
+#pragma unroll
+        for (int L = 1; L <= 15; L++) {
+            const uint32_t x = (2 * L + 1 < 20) ? (uint32_t)__shfl(v, (a << 5) + 2 * L, 64) +
+                                                      (uint32_t)__shfl(v, (a << 5) + 2 * L + 1, 64)
+                                                : 0u;
+            cnt[L] = nz > 1 ? x : (L == 1 ? 2u : 0u);
+        }
+        if (nz > 1) fit_classes(cnt, a ? DF_DIST_MAXBITS : DF_LIT_MAXBITS);
+        if (k == 0) {
+            uint32_t st = 0, code = 0;
+#pragma unroll
+            for (int L = 1; L <= 15; L++) {
+                W.start[a][L] = st;
+                st += cnt[L];
+                code = (code + cnt[L - 1]) << 1;
+                W.next[a][L] = code;
+            }
+        }
+    }
+    wave_sync();
+    // code lengths by rank; per-chunk ranks within each length
+    for (int c = 0; c < 6; c++) {
+        const int a = c == 5 ? 1 : 0;
+        const bool sym = em_valid(c, lane);
+        const uint32_t nz = a ? nzd : nzl;
+        uint32_t L = 0;
+        if (sym) {
+            const uint32_t s = c < 5 ? 64 * c + lane : (uint32_t)lane;
+            if (nz > 1) {
+                if (W.freq[em_slot(c, lane)]) {
+                    const uint32_t r = W.rk[64 * c + lane], k0 = r & 31;
+                    uint32_t q = (r >> 5) + W.kpre[a][k0];
+                    for (int c2 = 0; c2 < c && !a; c2++) q += W.hcnt[c2][k0];
+#pragma unroll
+                    for (int l = 1; l <= 15; l++) L += q >= W.start[a][l] ? 1u : 0u;
+                }
+            } else {  // zero or one used symbol: two codes of length 1 (a complete code)
+                const uint32_t u = a ? hid : hil;
+                L = (s == (u ? u - 1 : 0u) || s == (u <= 1 ? 1u : 0u)) ? 1u : 0u;
+            }
+            W.len[em_slot(c, lane)] = (uint8_t)L;
+        }
+        uint32_t mine = 0, wl = 0;
+#pragma unroll
+        for (int k = 1; k <= DF_LIT_MAXBITS; k++) {
+            const uint64_t b = __ballot(L == (uint32_t)k);
+            wl = L == (uint32_t)k ? (uint32_t)__popcll(b & lt) : wl;
+            mine = lane == k ? (uint32_t)__popcll(b) : mine;
+        }
+        if (lane < 16) W.lcnt[c][lane] = mine;
+        W.rk[64 * c + lane] = (uint16_t)wl;
+    }
+    wave_sync();
+    uint32_t dyn = 0, fix = 0, hl = 0, hd = 0;
+    for (int c = 0; c < 6; c++) {
+        const int a = c == 5 ? 1 : 0;
+        const bool sym = em_valid(c, lane);
+        const uint32_t L = sym ? W.len[em_slot(c, lane)] : 0u;
+        if (sym) {
+            const uint32_t s = c < 5 ? 64 * c + lane : (uint32_t)lane;
+            uint32_t code = 0;
+            if (L) {
+                uint32_t cc = W.next[a][L] + W.rk[64 * c + lane];
+                for (int c2 = 0; c2 < c && !a; c2++) cc += W.lcnt[c2][L];
+                code = (L << 16) | bitrev(cc, L);
+            }
+            W.code[em_slot(c, lane)] = code;
+            const uint32_t f = W.freq[em_slot(c, lane)];
+            const uint32_t ex = a ? dist_extra(s) : (s > 256 ? len_extra(s) : 0u);
+            dyn += f * (L + ex);
+            fix += f * ((a ? 5u : fixed_lit_len(s)) + ex);
+        }
+        const uint64_t used = __ballot(L != 0);
+        if (used) {
+            const uint32_t h = 64 - (uint32_t)__clzll(used);
+            if (a) hd = h;
+            else hl = 64 * c + h;
+        }
+    }
+    wave_sync();
+    EmCodes r;
+    r.dyn_tok = wave_sum(dyn);
+    r.fix_tok = wave_sum(fix);
+    r.nlit = max(257u, hl);
+    r.ndist = max(1u, hd);
+    return r;
+}
+
+// OR a pattern of n <= 36 bits into the staging window at bit pos
+__device__ __forceinline__ void em_put(uint32_t* stg, uint32_t pos, uint64_t pat, uint32_t n) {
+    if (!n) return;
+    const uint32_t wi = pos >> 5, sh = pos & 31;
+    const uint64_t lo = pat << sh;
+    atomicOr(&stg[wi], (uint32_t)lo);
+    if (sh + n > 32) atomicOr(&stg[wi + 1], (uint32_t)(lo >> 32));
+    if (sh + n > 64) atomicOr(&stg[wi + 2], (uint32_t)(pat >> (64 - sh)));
+}
+
+// bit pattern of one token word under the codes in W.code (n <= 36)
+template <bool RAW>
+__device__ __forceinline__ uint64_t em_pattern(const EmWave& W, uint32_t v, uint32_t cnt, uint32_t& n) {
+    uint64_t pat = 0;
+    n = 0;
+    if (!RAW && (v >> 31)) {
+        const uint32_t L = ((v >> 16) & 0xFFu) + 3, d = (v & 0x7FFFu) + 1;
+        const uint32_t ls = len_sym(L), ds = dist_sym(d);
+        const uint32_t lc = W.code[ls], dc = W.code[EM_LIT + ds];
+        pat = lc & 0xFFFFu;
+        n = lc >> 16;
+        pat |= (uint64_t)(L - len_base(ls)) << n;
+        n += len_extra(ls);
+        pat |= (uint64_t)(dc & 0xFFFFu) << n;
+        n += dc >> 16;
+        pat |= (uint64_t)(d - dist_base(ds)) << n;
+        n += dist_extra(ds);
+        return pat;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < (RAW ? 4u : 3u); i++) {
+        if (i < cnt) {
+            const uint32_t c = W.code[(v >> (8 * i)) & 0xFFu];
+            pat |= (uint64_t)(c & 0xFFFFu) << n;
+            n += c >> 16;
+        }
+    }
+    return pat;
+}
+
+// staging -> HBM: the first `nw` words of the window go to dst; the partial word moves to the
+// window's start, the rest is zeroed (only words up to nw + 1 were ever written)
+__device__ __forceinline__ void em_flush(uint32_t* stg, uint32_t* dst, uint32_t nw) {
+    const int lane = lane_id();
+    for (uint32_t i = lane; i < nw; i += 64) dst[i] = stg[i];
+    wave_sync();
+    const uint32_t part = stg[nw];
+    wave_sync();
+    for (uint32_t i = lane; i <= nw + 1; i += 64) stg[i] = i == 0 ? part : 0u;
+    wave_sync();
+}
+
+template <int SEG, bool RAW>
+__device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
+    const int lane = lane_id();
+    const uint64_t base = seg * (uint64_t)SEG;
+    const uint32_t nb = (uint32_t)min((uint64_t)SEG, A.n - base);
+    const bool is_final = (seg + 1 == A.nseg) && A.final_last;
+    uint32_t* const slot = reinterpret_cast<uint32_t*>(A.slots + seg * (uint64_t)A.slot_bytes);
+    // token source: level 1 reads the input's words (four literals each; the segment base is
+    // 4-aligned when the input is: SEG is a multiple of 4), levels 2-3 the front kernel's words
+    const uint8_t* const inb = A.in + base;
+    const uintptr_t mis = reinterpret_cast<uintptr_t>(inb) & 3;
+    const uint32_t* const inw = reinterpret_cast<const uint32_t*>(inb - mis);
+    const uint64_t in_words_end = (A.n - base + mis + 3) / 4;  // readable words from inw
+    auto raw_word = [&](uint32_t k) -> uint32_t {  // input bytes 4k .. 4k + 3 of the segment
+        const uint32_t x = 4 * k + (uint32_t)mis;
+        const uint32_t a = inw[x >> 2];
+        const uint32_t b = (x >> 2) + 1 < in_words_end ? inw[(x >> 2) + 1] : 0u;
+        return mis ? __builtin_amdgcn_alignbyte(b, a, x & 3) : a;
+    };
+    const uint32_t ntok = RAW ? (nb + 3) / 4 : A.ntok[seg];
+    const uint32_t* const tok = RAW ? nullptr : A.tok + seg * (uint64_t)A.tok_stride;
+    auto load4 = [&](uint32_t blk, uint32_t (&v)[4]) {
+        const uint32_t i0 = blk * 256 + 4 * lane;
+#pragma unroll
+        for (int j = 0; j < 4; j++) v[j] = 0;
+        if (RAW) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (i0 + j < ntok) v[j] = raw_word(i0 + j);
+        } else if (i0 + 3 < ntok) {
+            const uint4 q = *reinterpret_cast<const uint4*>(tok + i0);  // tok_stride % 4 == 0
+            v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (i0 + j < ntok) v[j] = tok[i0 + j];
+        }
+    };
+    auto count_of = [&](uint32_t v, uint32_t idx) -> uint32_t {  // literals in the word
+        if (RAW) return min(4u, nb - 4 * idx);
+        return (v >> 31) ? 0u : (v >> 24) & 3u;
+    };
+    const uint32_t nblk = (ntok + 255) / 256;
+    const uint64_t stored_bytes = 5ull + nb + (is_final ? 0 : 5);
+
+    if (A.level != 0) {
+        // ---- histogram ------------------------------------------------------------------
+        for (int i = lane; i < EM_SYM; i += 64) W.freq[i] = 0;
+        wave_sync();
+        for (uint32_t blk = 0; blk < nblk; blk++) {
+            uint32_t v[4];
+            load4(blk, v);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t idx = blk * 256 + 4 * lane + j;
+                if (idx >= ntok) continue;
+                if (!RAW && (v[j] >> 31)) {
+                    atomicAdd(&W.freq[len_sym(((v[j] >> 16) & 0xFFu) + 3)], 1u);
+                    atomicAdd(&W.freq[EM_LIT + dist_sym((v[j] & 0x7FFFu) + 1)], 1u);
+                } else {
+                    const uint32_t cnt = count_of(v[j], idx);
+#pragma unroll
+                    for (uint32_t i = 0; i < (RAW ? 4u : 3u); i++)
+                        if (i < cnt) atomicAdd(&W.freq[(v[j] >> (8 * i)) & 0xFFu], 1u);
+                }
+            }
+        }
+        if (lane == 0) atomicAdd(&W.freq[256], 1u);  // end-of-block
+        wave_sync();
+        const EmCodes ec = em_build_codes(W);
+
+        // ---- dynamic header: RLE runs over (len[0..nlit), len[288..288+ndist)) -------------
+        const uint32_t nlit = ec.nlit, ndist = ec.ndist, nall = nlit + ndist;
+        auto seqv = [&](uint32_t i) -> uint32_t { return i < nlit ? W.len[i] : W.len[EM_LIT + i - nlit]; };
+        uint64_t rm[5];  // run starts, one ballot per chunk of 64 positions
+        if (lane < 20) W.prefreq[lane] = 0;
+#pragma unroll
+        for (int c = 0; c < 5; c++) {
+            const uint32_t i = 64 * c + lane;
+            bool start = false;
+            if (i < nall) start = i == 0 || i == nlit || seqv(i - 1) != seqv(i);
+            rm[c] = __ballot(start);
+        }
+        wave_sync();
+        for (int c = 0; c < 5; c++) {
+            uint32_t rl = 0;
+            if ((rm[c] >> lane) & 1) {
+                const uint32_t i = 64 * c + lane;
+                uint32_t j = nall;
+                const uint64_t m = lane < 63 ? rm[c] & (~0ull << (lane + 1)) : 0ull;
+                if (m) j = 64 * c + (uint32_t)__builtin_ctzll(m);
+                else
+                    for (int c2 = 4; c2 > c; c2--)
+                        if (rm[c2]) j = 64 * c2 + (uint32_t)__builtin_ctzll(rm[c2]);
+                rl = min(j, nall) - i;
+                const uint32_t v = seqv(i);
+                const RunPlan p = plan_run(v, rl);
+                if (p.n18) atomicAdd(&W.prefreq[18], p.n18);
+                if (p.n17) atomicAdd(&W.prefreq[17], p.n17);
+                if (p.n16) atomicAdd(&W.prefreq[16], p.n16);
+                if (p.nlit) atomicAdd(&W.prefreq[v], p.nlit);
+            }
+            W.rk[64 * c + lane] = (uint16_t)rl;
+        }
+        wave_sync();
+        wave_build_lengths64(W.prefreq, 19, 7, W.prelen);
+        wave_sync();
+        wave_assign_codes(W.prelen, 19, W.precode);
+        wave_sync();
+        const uint32_t pv = lane < 19 ? W.prelen[kPerm[lane]] : 0u;
+        const uint64_t nzp = __ballot(pv != 0u);
+        const uint32_t hclen = max(4u, nzp ? 64u - (uint32_t)__clzll(nzp) : 0u);
+        uint32_t rtot = 0;  // run bit offsets (exclusive scan in position order) -> W.rk
+        for (int c = 0; c < 5; c++) {
+            const uint32_t rl = W.rk[64 * c + lane];
+            uint32_t b = 0;
+            if (rl) {
+                const uint32_t v = seqv(64 * c + lane);
+                const RunPlan p = plan_run(v, rl);
+                b = p.n18 * (W.prelen[18] + 7) + p.n17 * (W.prelen[17] + 3) + p.n16 * (W.prelen[16] + 2) +
+                    p.nlit * W.prelen[v];
+            }
+            const uint32_t inc = wave_incl_scan(b);
+            W.rk[64 * c + lane] = (uint16_t)(rl ? rtot + inc - b : 0xFFFFu);
+            rtot += __shfl(inc, 63, 64);
+        }
+        wave_sync();
+        const uint32_t hdr_bits = 14 + 3 * hclen + rtot;
+
+        // ---- block type by exact size (reference deflate.hpp:739-746 picks the smallest) ----
+        const uint64_t dyn_bits = 3ull + hdr_bits + ec.dyn_tok;
+        const uint64_t fix_bits = 3ull + ec.fix_tok;
+        const bool use_dyn = dyn_bits <= fix_bits;
+        const uint64_t bits = use_dyn ? dyn_bits : fix_bits;
+        const uint64_t hbytes = is_final ? (bits + 7) / 8 : (bits + 3 + 7) / 8 + 4;
+        if (hbytes < stored_bytes) {
+            if (!use_dyn) {
+                for (int s = lane; s < EM_SYM; s += 64)
+                    W.code[s] = s < EM_LIT ? (s < 286 ? (fixed_lit_len(s) << 16) | fixed_lit_code(s) : 0u)
+                                           : (s - EM_LIT < 30 ? (5u << 16) | bitrev(s - EM_LIT, 5) : 0u);
+            }
+            for (int i = lane; i < EM_STG; i += 64) W.stg[i] = 0;
+            wave_sync();
+            // ---- header bits ------------------------------------------------------------
+            if (lane == 0) {
+                uint64_t h = (is_final ? 1u : 0u) | ((use_dyn ? 2u : 1u) << 1);
+                if (use_dyn) h |= ((uint64_t)(nlit - 257) << 3) | ((uint64_t)(ndist - 1) << 8) | ((uint64_t)(hclen - 4) << 13);
+                em_put(W.stg, 0, h, use_dyn ? 17 : 3);
+            }
+            if (use_dyn) {
+                if (lane < (int)hclen) em_put(W.stg, 17 + 3 * lane, pv, 3);
+                const uint32_t rb = 17 + 3 * hclen;
+                for (int c = 0; c < 5; c++) {
+                    const uint32_t ro = W.rk[64 * c + lane];
+                    if (ro == 0xFFFFu) continue;
+                    const uint32_t i = 64 * c + lane;
+                    const uint32_t v = seqv(i);
+                    uint32_t j = nall;  // the run's end: the next start
+                    const uint64_t m = lane < 63 ? rm[c] & (~0ull << (lane + 1)) : 0ull;
+                    if (m) j = 64 * c + (uint32_t)__builtin_ctzll(m);
+                    else
+                        for (int c2 = 4; c2 > c; c2--)
+                            if (rm[c2]) j = 64 * c2 + (uint32_t)__builtin_ctzll(rm[c2]);
+                    const RunPlan p = plan_run(v, min(j, nall) - i);
+                    uint32_t pos = rb + ro;
+                    auto put = [&](uint32_t sym, uint32_t extra, uint32_t xb) {
+                        const uint32_t pc = W.precode[sym];
+                        const uint32_t l = pc >> 16;
+                        em_put(W.stg, pos, (uint64_t)(pc & 0xFFFFu) | ((uint64_t)extra << l), l + xb);
+                        pos += l + xb;
+                    };
+                    if (v == 0) {
+                        for (uint32_t q = 0; q < p.n18; q++) put(18, (q + 1 == p.n18 ? p.last18 : 138) - 11, 7);
+                        if (p.n17) put(17, p.r17 - 3, 3);
+                        for (uint32_t q = 0; q < p.nlit; q++) put(0, 0, 0);
+                    } else {
+                        put(v, 0, 0);
+                        for (uint32_t q = 0; q < p.n16; q++) put(16, (q + 1 == p.n16 ? p.last16 : 6) - 3, 2);
+                        for (uint32_t q = 1; q < p.nlit; q++) put(v, 0, 0);
+                    }
+                }
+            }
+            wave_sync();
+            // ---- tokens -------------------------------------------------------------------
+            uint32_t cur = 3 + (use_dyn ? hdr_bits : 0u);  // bit position in the window
+            uint32_t* dst = slot;                          // next HBM word of the slot
+            for (uint32_t blk = 0; blk < nblk; blk++) {
+                uint32_t v[4], nbit[4];
+                uint64_t pat[4];
+                load4(blk, v);
+                uint32_t mine = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t idx = blk * 256 + 4 * lane + j;
+                    nbit[j] = 0;
+                    pat[j] = 0;
+                    if (idx < ntok) pat[j] = em_pattern<RAW>(W, v[j], count_of(v[j], idx), nbit[j]);
+                    mine += nbit[j];
+                }
+                const uint32_t inc = wave_incl_scan(mine);
+                uint32_t pos = cur + inc - mine;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    em_put(W.stg, pos, pat[j], nbit[j]);
+                    pos += nbit[j];
+                }
+                cur += __shfl(inc, 63, 64);
+                wave_sync();
+                if (cur >= 32u * EM_FLUSH) {
+                    const uint32_t nw = cur >> 5;
+                    em_flush(W.stg, dst, nw);
+                    dst += nw;
+                    cur &= 31;
+                }
+            }
+            // ---- end of block, then (non-final) the empty stored block 000|pad|0000|FFFF ----
+            const uint32_t eob = W.code[256];
+            if (lane == 0) em_put(W.stg, cur, eob & 0xFFFFu, eob >> 16);
+            const uint32_t end_bits = cur + (eob >> 16);
+            const uint32_t tail = is_final ? (end_bits + 7) / 8 : (end_bits + 3 + 7) / 8 + 4;  // bytes in the window
+            wave_sync();
+            if (lane == 0 && !is_final) {
+                atomicOr(&W.stg[(tail - 2) >> 2], 0xFFu << (((tail - 2) & 3) * 8));
+                atomicOr(&W.stg[(tail - 1) >> 2], 0xFFu << (((tail - 1) & 3) * 8));
+            }
+            wave_sync();
+            const uint32_t nw = (tail + 3) / 4;
+            for (uint32_t i = lane; i < nw; i += 64) dst[i] = W.stg[i];
+            if (lane == 0)
+                A.sizes[seg] = (uint32_t)((reinterpret_cast<uint8_t*>(dst) - reinterpret_cast<uint8_t*>(slot)) + tail);
+            return;
+        }
+    }
+    // ---- stored block: [BFINAL|00][LEN][NLEN][data] (+ the empty stored block) ------------
+    const uint32_t total = (uint32_t)stored_bytes;
+    const uint32_t nw = (total + 3) / 4;
+    for (uint32_t k = lane; k < nw; k += 64) {
+        // output word k = bytes 4k .. 4k + 3; data byte i is output byte 5 + i
+        uint32_t w = 0;
+        if (k >= 2 && 4 * k + 3 < 5 + nb) {
+            const uint32_t x = 4 * k - 5 + (uint32_t)mis;  // aligned-base byte of the first
+            const uint32_t a = inw[x >> 2];
+            const uint32_t b = (x >> 2) + 1 < in_words_end ? inw[(x >> 2) + 1] : 0u;
+            w = __builtin_amdgcn_alignbyte(b, a, x & 3);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t pos = 4 * k + j;
+                uint32_t byte;
+                if (pos == 0) byte = is_final ? 1u : 0u;
+                else if (pos == 1) byte = nb & 0xFFu;
+                else if (pos == 2) byte = (nb >> 8) & 0xFFu;
+                else if (pos == 3) byte = ~nb & 0xFFu;
+                else if (pos == 4) byte = (~nb >> 8) & 0xFFu;
+                else if (pos < 5 + nb) byte = inb[pos - 5];
+                else byte = (!is_final && pos >= 5 + nb + 3 && pos < total) ? 0xFFu : 0u;
+                w |= byte << (8 * j);
+            }
+        }
+        slot[k] = w;
+    }
+    if (lane == 0) A.sizes[seg] = total;
+}
+
+// RAW: level 1 (the input's bytes are the tokens) and level 0; else the front kernel's words
+template <int SEG, bool RAW>
+__global__ __launch_bounds__(64 * EM_NW) void k_deflate_emit(DeflateArgs A) {
+    __shared__ EmWave Ws[EM_NW];
+    const uint64_t seg = (uint64_t)blockIdx.x * EM_NW + (threadIdx.x >> 6);
+    if (seg >= A.nseg) return;
+    em_segment<SEG, RAW>(A, Ws[threadIdx.x >> 6], seg);
 }
 
 // exclusive scan of segment sizes -> offsets (single workgroup of 1024 threads).  Thread t owns
@@ -1731,11 +1763,22 @@ hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t 
     const uint64_t fit = (uint64_t)max(ncu, 1) * (uint64_t)max(per, 1);
     const uint32_t grid = (uint32_t)std::min<uint64_t>(A.nseg, fit);  // host min(int, int) would truncate
     if (ev_main0) (void)hipEventRecord(ev_main0, st);
-    if (grid) {
+    if (grid && A.level >= 2) {  // match finding + parse -> token words (levels 0-1 have none)
         if (seg_bytes == 32768)
             hipLaunchKernelGGL(k_deflate_segments<32768>, dim3(grid), dim3(DF_NT), 0, st, A);
         else
             hipLaunchKernelGGL(k_deflate_segments16, dim3(grid), dim3(DF_NT), 0, st, A);
+    }
+    if (A.nseg) {  // entropy coding and bit packing, one wavefront per segment
+        const uint32_t eg = (uint32_t)((A.nseg + EM_NW - 1) / EM_NW);
+        const bool raw = A.level < 2;
+        if (seg_bytes == 32768) {
+            if (raw) hipLaunchKernelGGL((k_deflate_emit<32768, true>), dim3(eg), dim3(64 * EM_NW), 0, st, A);
+            else hipLaunchKernelGGL((k_deflate_emit<32768, false>), dim3(eg), dim3(64 * EM_NW), 0, st, A);
+        } else {
+            if (raw) hipLaunchKernelGGL((k_deflate_emit<16384, true>), dim3(eg), dim3(64 * EM_NW), 0, st, A);
+            else hipLaunchKernelGGL((k_deflate_emit<16384, false>), dim3(eg), dim3(64 * EM_NW), 0, st, A);
+        }
     }
     if (ev_main1) (void)hipEventRecord(ev_main1, st);
     hipLaunchKernelGGL(k_scan_sizes, dim3(1), dim3(1024), 0, st, A.sizes, A.offsets, A.nseg, A.total);

@@ -62,6 +62,7 @@ struct dmx_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     DevBuf in, out, slots, sizes, offs, scal, cands, tiles, tileoffs, recs, status, dbg;
+    DevBuf dtok, dntok;                  // deflate: the front kernel's token words and counts
     DevBuf rtmp, rchain;                 // chain repair: scratch output, chain / offsets / sizes
     DevBuf ltok, ltokoff, lntok, lcaps;  // lane decoder token lists (mode 4)
     DevBuf lheavy;                       // heavy-candidate list for the workgroup decoder (mode 6)
@@ -191,8 +192,10 @@ int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, 
     }
     const uint64_t nseg = (n + c->seg - 1) / c->seg;
     const uint32_t slot_bytes = c->seg + 256;
+    const uint32_t tok_stride = level >= 2 ? deflate_tok_stride(c->seg) : 0u;
     if (!c->slots.ensure(nseg * (size_t)slot_bytes) || !c->sizes.ensure(nseg * 4) ||
-        !c->offs.ensure(nseg * 8) || !c->scal.ensure(sizeof(Scal)))
+        !c->offs.ensure(nseg * 8) || !c->scal.ensure(sizeof(Scal)) ||
+        !c->dtok.ensure(std::max<uint64_t>(1, nseg * (uint64_t)tok_stride) * 4) || !c->dntok.ensure(nseg * 4))
         return DMX_ERR_NOMEM;
     DeflateArgs A;
     A.in = d_in;
@@ -202,19 +205,15 @@ int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, 
     A.final_last = final_last ? 1 : 0;
     A.slots = c->slots.as<uint8_t>();
     A.slot_bytes = slot_bytes;
+    A.tok = c->dtok.as<uint32_t>();
+    A.tok_stride = tok_stride;
+    A.ntok = c->dntok.as<uint32_t>();
     A.sizes = c->sizes.as<uint32_t>();
     A.offsets = c->offs.as<uint64_t>();
     A.total = &c->scal.as<Scal>()->total;
     A.out = d_out;
     A.cap = cap;
     A.dbg = phase_buf(c, nseg);
-    {
-        static const uint32_t dev_flags = [] {
-            const char* e = std::getenv("DMX_DF_FLAGS");
-            return e ? (uint32_t)std::atoi(e) : 0u;
-        }();
-        A.dev_flags = dev_flags;
-    }
     HIPCHK(launch_deflate(A, c->seg, st, c->timing ? c->ev[1] : nullptr, c->timing ? c->ev[2] : nullptr));
     if (A.dbg) phase_dump(c, "deflate", nseg, st);
     uint64_t total = 0;
@@ -616,7 +615,12 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
             k = (uint64_t)(it - hc.begin());
         }
         uint64_t slot = A.slot ? A.slot : c->seg;
-        if (ok) {
+        // (when the repair's own scratch does not fit, the stream still decodes on path 5 or the
+        // serial decoder, which need only the output: ADVICE r3)
+        uint8_t* const a_out = A.out;
+        const uint64_t a_cap = A.cap;
+        do {
+            if (!ok) break;
             if (fixed_out && tot > cap) return DMX_ERR_CAPACITY;
             uint8_t* dst = fixed_out ? fixed_out : out;
             const uint64_t need = (chain.back() + 1) * slot;
@@ -631,7 +635,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
                     for (int pi = 0; pi < np; pi++)
                         if (plan[pi][0] == 4 || plan[pi][0] == 6 || plan[pi][0] == 3) plan[pi][1] = (uint32_t)slot;
                 }
-                if (!c->rtmp.ensure(ncand * slot)) return DMX_ERR_NOMEM;
+                if (!c->rtmp.ensure(ncand * slot)) break;
                 A.out = c->rtmp.as<uint8_t>();
                 A.cap = ncand * slot;
                 InflateResult r2{};
@@ -639,11 +643,11 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
                 if (rc != DMX_OK) return rc;
                 src = A.out;
             } else {  // every slot is in `out` (== dst): place into scratch, copy back
-                if (!c->rtmp.ensure(tot ? tot : 1)) return DMX_ERR_NOMEM;
+                if (!c->rtmp.ensure(tot ? tot : 1)) break;
                 place = c->rtmp.as<uint8_t>();
             }
             const uint64_t nch = chain.size();
-            if (!c->rchain.ensure(nch * 20)) return DMX_ERR_NOMEM;
+            if (!c->rchain.ensure(nch * 20)) break;
             uint64_t* dch = c->rchain.as<uint64_t>();
             uint64_t* doffs = dch + nch;
             uint32_t* dsz = reinterpret_cast<uint32_t*>(doffs + nch);
@@ -660,7 +664,9 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
             *total_out = tot;
             if (dev_out) *dev_out = dst;
             return DMX_OK;
-        }
+        } while (0);
+        A.out = a_out;  // not repaired: the later paths decode into the caller's buffer
+        A.cap = a_cap;
     }
 
     if (path_env == -1 || path_env == 5) {

@@ -11,16 +11,23 @@ struct DeflateArgs {
     uint64_t nseg;
     int level;
     int final_last;       // set BFINAL on the last segment
-    uint8_t* slots;       // nseg * slot_bytes scratch
+    uint8_t* slots;       // nseg * slot_bytes scratch: each segment's bitstream
     uint32_t slot_bytes;
+    uint32_t* tok;        // nseg * tok_stride words: the front kernel's token words (levels 2-3)
+    uint32_t tok_stride;  // words per segment (a multiple of 4), deflate_tok_stride(segment bytes)
+    uint32_t* ntok;       // nseg token word counts
     uint32_t* sizes;      // nseg
     uint64_t* offsets;    // nseg
     uint64_t* total;      // 1
     uint8_t* out;
     uint64_t cap;
     uint64_t* dbg;        // optional per-block phase timestamps (DMX_PHASES), else nullptr
-    uint32_t dev_flags;   // developer experiments (DMX_DF_FLAGS), 0 in production
 };
+
+// Token words per segment of the front kernel: a literal word covers 1-3 input bytes, a match
+// word at least 3, so at most seg / 2 words (one literal between every two 3-byte matches), plus
+// one partial literal word per thread's token range (1024 threads).
+constexpr uint32_t deflate_tok_stride(uint32_t seg) { return seg / 2 + 1024 + 64; }
 
 hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t st, hipEvent_t ev0,
                           hipEvent_t ev1);
