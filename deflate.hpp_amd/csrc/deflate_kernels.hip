@@ -92,6 +92,8 @@ constexpr uint32_t DF_L3_RP = DMX_L3_RP;
 #define DMX_DF_SKIP 1
 #endif
 constexpr bool DF_SKIP = DMX_DF_SKIP != 0;
+// token-word count of a segment without any match (k_deflate_emit then reads its input's bytes)
+constexpr uint32_t EM_ALL_LITERALS = 0xFFFFFFFFu;
 
 // ---------------------------------------------------------------------------------------
 // block primitives
@@ -338,7 +340,6 @@ __device__ __forceinline__ uint32_t matchlen_u(const uint32_t* w, uint32_t p, ui
 // the next LDS array, and the result is clamped to maxl.  Same value as matchlen().
 __device__ __forceinline__ uint32_t matchlen4(const uint32_t* w, uint32_t p, uint32_t q,
                                               uint32_t maxl, uint32_t sub) {
-    const int qb = lane_id() & ~3;
     uint32_t L = 0;
     while (L < maxl) {
         const uint32_t o = L + 16 * sub;
@@ -359,11 +360,12 @@ __device__ __forceinline__ uint32_t matchlen4(const uint32_t* w, uint32_t p, uin
                 off = 4 * k;
             }
         }
-        const uint32_t mine = x ? off + ((uint32_t)__builtin_ctz(x) >> 3) : 16u;
-        const uint32_t qbits = (uint32_t)(__ballot(x != 0) >> qb) & 0xFu;
-        if (qbits) {
-            const uint32_t f = (uint32_t)__builtin_ctz(qbits);
-            L += 16 * f + (uint32_t)__shfl((int)mine, qb + (int)f, 64);
+        // the quad's first mismatch: a min over the quad by two DPP steps (no LDS round trip)
+        uint32_t v = x ? 16 * sub + off + ((uint32_t)__builtin_ctz(x) >> 3) : 64u;
+        v = min(v, xor_lane<1>(v));
+        v = min(v, xor_lane<2>(v));
+        if (v < 64) {
+            L += v;
             break;
         }
         L += 64;
@@ -429,7 +431,7 @@ struct DfSmem {
     uint32_t tokmap[SEG / 32];  // token-start bitmap (parse walk; chunks share boundary words)
     uint16_t lasttok[NWALK + 1];  // last token start of each parse chunk
     uint32_t scan[4 * DF_NT / 64];
-    uint32_t sh[48];
+    uint32_t sh[64];  // 44: run candidate, 46: mismatch tag, 48..62: divisor-period tags
 };
 
 // Persistent workgroups: the next segment of this workgroup (seg + gridDim.x) is loaded straight
@@ -500,6 +502,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         for (uint32_t i = nb + t; i < ((nb + 3) & ~3u) + 32; i += DF_NT) dbytes[i] = 0;
         if (t < NMAP) S.tokmap[t] = 0;
         if (t == 0) S.sh[46] = 0;  // the match rounds' mismatch tag (run continuation)
+        if (t >= 48 && t < 63) S.sh[t] = 0;  // its divisor-period tags
         if (level >= 2)
             for (int i = t; i < 2 * HT; i += DF_NT) S.U[i] = 0;
     }
@@ -657,15 +660,34 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                         bool tested = false;
                         if (SKIP && pend) {
                             pend = false;
-                            const uint32_t dl = __builtin_amdgcn_readfirstlane(dlr);
+                            uint32_t dl = __builtin_amdgcn_readfirstlane(dlr);
                             wait -= wait ? 1u : 0u;
 #ifdef DMX_DF_SKIPDBG
                             if (seg == 10 && t == 0) printf("seg %u round %u dl %u wait %u\n", (unsigned)seg, rr, dl, wait);
 #endif
                             if (!wait && dl) {
+                                tested = true;
+                                // Periodic data: the trigger's candidate is a first occurrence in an
+                                // earlier round, often a multiple of the period.  The largest k <= 16
+                                // (dl % k == 0) whose dl / k repeats the 256 bytes at r0 gives the
+                                // tested distance (64 threads per k, one word each; a mismatch tags
+                                // sh[48 + k - 2] with the round); the test below then verifies it.
+                                {
+                                    const uint32_t ki = (uint32_t)t >> 6, k = ki + 2, bq = r0 + 4 * ((uint32_t)t & 63);
+                                    if (ki < 15 && dl % k == 0 && bq + 4 <= nb) {
+                                        const uint32_t dk = dl / k, ia = (bq - dk) >> 2, sk = (bq - dk) & 3;
+                                        if (S.data32[bq >> 2] != __builtin_amdgcn_alignbyte(S.data32[ia + 1], S.data32[ia], sk))
+                                            atomicMax(&S.sh[48 + ki], rr + 1);
+                                    }
+                                }
+                                __syncthreads();  // (uniform: dl and wait are the same in every wave)
+                                uint32_t dsel = dl;
+#pragma unroll
+                                for (uint32_t k = 2; k <= 16; k++)
+                                    dsel = (dl % k == 0 && S.sh[48 + k - 2] != rr + 1) ? dl / k : dsel;
+                                dl = __builtin_amdgcn_readfirstlane(dsel);
                                 // words r0 / 4 + t + 1024 j (neighbouring lanes, neighbouring words:
                                 // no bank conflicts) against the words dl bytes before them
-                                tested = true;
                                 skip_d = dl;
                                 const uint32_t sa = (r0 - dl) & 3;  // (r0 is a multiple of 4)
                                 uint32_t mm = 0xFFFFFFFFu;
@@ -731,11 +753,14 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                     };
                     using Full = std::integral_constant<bool, true>;
                     using Part = std::integral_constant<bool, false>;
+                    const DeflateArgs& Ar = A;  // (shadowed by the round states below)
                     RoundState A = {0, 0, 0, 0, 0, false, false}, B = A;
                     uint32_t r0 = 0, rr = 0;
                     for (; r0 + 2 * RP + 3 <= nb; r0 += 2 * RP, rr += 2) {  // two full rounds
                         round(r0, rr, A, B, Full{});
+                        if (rr == 0) DMX_PHASE(Ar.dbg, seg, 12);
                         round(r0 + RP, rr + 1, B, A, Full{});
+                        if (rr == 0) DMX_PHASE(Ar.dbg, seg, 13);
                     }
                     for (; r0 < nb; r0 += RP, rr++) {  // the rest (the last may be partial)
                         round(r0, rr, A, B, Part{});
@@ -1048,12 +1073,14 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         // ---- token ranges (TokRange): per-word token counts, block scan into the match
         //      bitmap (dead after the parse), binary search for the thread's first token ------
         TokRange tr;
+        uint32_t tr_total;  // tokens of the segment
         {
             const uint32_t c = t < NMAP ? (uint32_t)__popc(S.tokmap[t]) : 0u;
             uint32_t tot;
             const uint32_t ex = block_excl_scan(c, S.scan, &tot);
             if (t < NMAP) S.mmap[t] = ex;
             __syncthreads();
+            tr_total = tot;
             const uint32_t K = (tot + DF_NT - 1) / DF_NT;
             const uint32_t first = min((uint32_t)t * K, tot);
             tr.n = min(first + K, tot) - first;
@@ -1078,8 +1105,13 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         }
         DMX_PHASE(A.dbg, seg, 15);
         // ---- token words for k_deflate_emit, in position order: literal runs of up to three
-        //      bytes per word, one word per match (count, block scan of the counts, write) -----
-        {
+        //      bytes per word, one word per match (count, block scan of the counts, write).  A
+        //      segment without a match (every position a token: incompressible data) writes none:
+        //      the emission kernel reads its literals from the input -----
+        const bool all_lit = tr_total == nb;
+        if (all_lit) {
+            if (t == 0) A.ntok[seg] = EM_ALL_LITERALS;
+        } else {
             auto walk = [&](auto emit) {
                 uint32_t w = tr.w, m = tr.m, lit = 0, nl = 0;
                 for (uint32_t i = 0; i < tr.n; i++) {
@@ -1344,11 +1376,10 @@ __device__ __forceinline__ void em_put(uint32_t* stg, uint32_t pos, uint64_t pat
 }
 
 // bit pattern of one token word under the codes in W.code (n <= 36)
-template <bool RAW>
-__device__ __forceinline__ uint64_t em_pattern(const EmWave& W, uint32_t v, uint32_t cnt, uint32_t& n) {
+__device__ __forceinline__ uint64_t em_pattern(const EmWave& W, uint32_t v, uint32_t cnt, uint32_t& n, bool raw) {
     uint64_t pat = 0;
     n = 0;
-    if (!RAW && (v >> 31)) {
+    if (!raw && (v >> 31)) {
         const uint32_t L = ((v >> 16) & 0xFFu) + 3, d = (v & 0x7FFFu) + 1;
         const uint32_t ls = len_sym(L), ds = dist_sym(d);
         const uint32_t lc = W.code[ls], dc = W.code[EM_LIT + ds];
@@ -1363,7 +1394,7 @@ __device__ __forceinline__ uint64_t em_pattern(const EmWave& W, uint32_t v, uint
         return pat;
     }
 #pragma unroll
-    for (uint32_t i = 0; i < (RAW ? 4u : 3u); i++) {
+    for (uint32_t i = 0; i < 4u; i++) {
         if (i < cnt) {
             const uint32_t c = W.code[(v >> (8 * i)) & 0xFFu];
             pat |= (uint64_t)(c & 0xFFFFu) << n;
@@ -1377,17 +1408,27 @@ __device__ __forceinline__ uint64_t em_pattern(const EmWave& W, uint32_t v, uint
 // window's start, the rest is zeroed (only words up to nw + 1 were ever written)
 __device__ __forceinline__ void em_flush(uint32_t* stg, uint32_t* dst, uint32_t nw) {
     const int lane = lane_id();
+    // (not unrolled: eight unrolled stores held eight 64-bit addresses, the kernel's register peak)
+#pragma unroll 2
     for (uint32_t i = lane; i < nw; i += 64) dst[i] = stg[i];
     wave_sync();
     const uint32_t part = stg[nw];
     wave_sync();
+#pragma unroll 2
     for (uint32_t i = lane; i <= nw + 1; i += 64) stg[i] = i == 0 ? part : 0u;
     wave_sync();
 }
 
+// DMX_PHASES: one stamp per wave (its lane 0) into the segment's slots 4..9
+#define EM_PHASE(dbg, seg, slot)                                                          \
+    do {                                                                                  \
+        if ((dbg) && lane_id() == 0) (dbg)[(seg) * kPhaseSlots + (slot)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+
 template <int SEG, bool RAW>
 __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
     const int lane = lane_id();
+    EM_PHASE(A.dbg, seg, 4);
     const uint64_t base = seg * (uint64_t)SEG;
     const uint32_t nb = (uint32_t)min((uint64_t)SEG, A.n - base);
     const bool is_final = (seg + 1 == A.nseg) && A.final_last;
@@ -1404,13 +1445,15 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
         const uint32_t b = (x >> 2) + 1 < in_words_end ? inw[(x >> 2) + 1] : 0u;
         return mis ? __builtin_amdgcn_alignbyte(b, a, x & 3) : a;
     };
-    const uint32_t ntok = RAW ? (nb + 3) / 4 : A.ntok[seg];
-    const uint32_t* const tok = RAW ? nullptr : A.tok + seg * (uint64_t)A.tok_stride;
+    // (a segment the front kernel found no match in is all literals: its input's words too)
+    const bool raw = RAW || A.ntok[seg] == EM_ALL_LITERALS;
+    const uint32_t ntok = raw ? (nb + 3) / 4 : A.ntok[seg];
+    const uint32_t* const tok = raw ? nullptr : A.tok + seg * (uint64_t)A.tok_stride;
     auto load4 = [&](uint32_t blk, uint32_t (&v)[4]) {
         const uint32_t i0 = blk * 256 + 4 * lane;
 #pragma unroll
         for (int j = 0; j < 4; j++) v[j] = 0;
-        if (RAW) {
+        if (raw) {
 #pragma unroll
             for (int j = 0; j < 4; j++)
                 if (i0 + j < ntok) v[j] = raw_word(i0 + j);
@@ -1424,7 +1467,7 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
         }
     };
     auto count_of = [&](uint32_t v, uint32_t idx) -> uint32_t {  // literals in the word
-        if (RAW) return min(4u, nb - 4 * idx);
+        if (raw) return min(4u, nb - 4 * idx);
         return (v >> 31) ? 0u : (v >> 24) & 3u;
     };
     const uint32_t nblk = (ntok + 255) / 256;
@@ -1441,20 +1484,22 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
             for (int j = 0; j < 4; j++) {
                 const uint32_t idx = blk * 256 + 4 * lane + j;
                 if (idx >= ntok) continue;
-                if (!RAW && (v[j] >> 31)) {
+                if (!raw && (v[j] >> 31)) {
                     atomicAdd(&W.freq[len_sym(((v[j] >> 16) & 0xFFu) + 3)], 1u);
                     atomicAdd(&W.freq[EM_LIT + dist_sym((v[j] & 0x7FFFu) + 1)], 1u);
                 } else {
                     const uint32_t cnt = count_of(v[j], idx);
 #pragma unroll
-                    for (uint32_t i = 0; i < (RAW ? 4u : 3u); i++)
+                    for (uint32_t i = 0; i < 4u; i++)
                         if (i < cnt) atomicAdd(&W.freq[(v[j] >> (8 * i)) & 0xFFu], 1u);
                 }
             }
         }
         if (lane == 0) atomicAdd(&W.freq[256], 1u);  // end-of-block
         wave_sync();
+        EM_PHASE(A.dbg, seg, 5);
         const EmCodes ec = em_build_codes(W);
+        EM_PHASE(A.dbg, seg, 6);
 
         // ---- dynamic header: RLE runs over (len[0..nlit), len[288..288+ndist)) -------------
         const uint32_t nlit = ec.nlit, ndist = ec.ndist, nall = nlit + ndist;
@@ -1513,6 +1558,7 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
         }
         wave_sync();
         const uint32_t hdr_bits = 14 + 3 * hclen + rtot;
+        EM_PHASE(A.dbg, seg, 7);
 
         // ---- block type by exact size (reference deflate.hpp:739-746 picks the smallest) ----
         const uint64_t dyn_bits = 3ull + hdr_bits + ec.dyn_tok;
@@ -1526,6 +1572,7 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
                     W.code[s] = s < EM_LIT ? (s < 286 ? (fixed_lit_len(s) << 16) | fixed_lit_code(s) : 0u)
                                            : (s - EM_LIT < 30 ? (5u << 16) | bitrev(s - EM_LIT, 5) : 0u);
             }
+#pragma unroll 3
             for (int i = lane; i < EM_STG; i += 64) W.stg[i] = 0;
             wave_sync();
             // ---- header bits ------------------------------------------------------------
@@ -1581,7 +1628,7 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
                     const uint32_t idx = blk * 256 + 4 * lane + j;
                     nbit[j] = 0;
                     pat[j] = 0;
-                    if (idx < ntok) pat[j] = em_pattern<RAW>(W, v[j], count_of(v[j], idx), nbit[j]);
+                    if (idx < ntok) pat[j] = em_pattern(W, v[j], count_of(v[j], idx), nbit[j], raw);
                     mine += nbit[j];
                 }
                 const uint32_t inc = wave_incl_scan(mine);
@@ -1600,6 +1647,7 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
                     cur &= 31;
                 }
             }
+            EM_PHASE(A.dbg, seg, 8);
             // ---- end of block, then (non-final) the empty stored block 000|pad|0000|FFFF ----
             const uint32_t eob = W.code[256];
             if (lane == 0) em_put(W.stg, cur, eob & 0xFFFFu, eob >> 16);
@@ -1612,15 +1660,18 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
             }
             wave_sync();
             const uint32_t nw = (tail + 3) / 4;
+#pragma unroll 2
             for (uint32_t i = lane; i < nw; i += 64) dst[i] = W.stg[i];
             if (lane == 0)
                 A.sizes[seg] = (uint32_t)((reinterpret_cast<uint8_t*>(dst) - reinterpret_cast<uint8_t*>(slot)) + tail);
+            EM_PHASE(A.dbg, seg, 9);
             return;
         }
     }
     // ---- stored block: [BFINAL|00][LEN][NLEN][data] (+ the empty stored block) ------------
     const uint32_t total = (uint32_t)stored_bytes;
     const uint32_t nw = (total + 3) / 4;
+#pragma unroll 2
     for (uint32_t k = lane; k < nw; k += 64) {
         // output word k = bytes 4k .. 4k + 3; data byte i is output byte 5 + i
         uint32_t w = 0;

@@ -59,6 +59,9 @@ struct dmx_ctx {
     int device = 0;
     uint32_t seg = 32768;
     uint32_t flags = 0;
+    int inflate_pass = -1;     // dmx_config.dev_inflate_pass - 1: forced pass, -1 = the plan
+    uint32_t heavy_bytes = 0;  // dmx_config.dev_heavy_bytes
+    uint32_t diag = 0;         // DIAG_* bits, read once from the environment at dmx_create
     hipStream_t stream = nullptr;
     std::mutex mu;
     DevBuf in, out, slots, sizes, offs, scal, cands, tiles, tileoffs, recs, status, dbg;
@@ -70,17 +73,41 @@ struct dmx_ctx {
     // block-parallel path (path 5): scan counts / hits / offsets, hit list, unit starts, token
     // offsets and words, unit records, chain (unit index, offset, size), 16-bit image
     DevBuf fbc, fbh, fbo, fbl, fbs, fbt, fbk, fbu, fbch, fbco, fbcs, fbimg, fbstop, fbwin, fbopen, fbp32;
+    DevBuf fbvm, fbvh;  // per-unit start mode and code state (virtual / repair units)
     DevBuf ck;  // checksum scratch (checksum.hip) + the 4-byte result at its start
     bool timing = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev_df = nullptr;          // end of the last deflate's work (its scratch is reused)
+    bool df_pending = false;
     dmx_stats stats{};
+    std::vector<dmx_ctx*> subs;          // n_gpus > 1: one context per shard / piece
 };
 
 namespace {
 
-// DMX_DEBUG=1 names the failing HIP call on stderr (developer aid)
+// Diagnostics (never steer results): read from the environment once, at dmx_create.
+//   DMX_DEBUG=1       names the failing HIP call on stderr (process-wide)
+//   DMX_PHASES=<file> per-phase s_memtime timelines of the segmented kernels
+//   DMX_FB_DEBUG=1    block-parallel path: unit outcomes and chain breaks on stderr
+//   DMX_RECS=1        segmented inflate: per-candidate outcome of each pass on stderr
+enum : uint32_t { DIAG_PHASES = 1, DIAG_FB = 2, DIAG_RECS = 4, DIAG_DEBUG = 8 };
+struct Diag {
+    uint32_t bits = 0;
+    std::string phases_path;
+};
+static const Diag& diag_env() {  // first use (a dmx_create) reads the environment
+    static const Diag d = [] {
+        Diag r;
+        if (std::getenv("DMX_DEBUG")) r.bits |= DIAG_DEBUG;
+        if (const char* e = std::getenv("DMX_PHASES")) r.bits |= DIAG_PHASES, r.phases_path = e;
+        if (const char* e = std::getenv("DMX_FB_DEBUG"); e && *e) r.bits |= DIAG_FB;
+        if (std::getenv("DMX_RECS")) r.bits |= DIAG_RECS;
+        return r;
+    }();
+    return d;
+}
 static void hipchk_report(const char* what, hipError_t e, int line) {
-    if (std::getenv("DMX_DEBUG"))
+    if (diag_env().bits & DIAG_DEBUG)
         std::fprintf(stderr, "dmx: %s failed (dmx_host.cpp:%d): %s\n", what, line, hipGetErrorString(e));
 }
 #define HIPCHK(x)                                   \
@@ -104,14 +131,14 @@ struct Scal {  // small device-side scalars, one allocation
 // DMX_PHASES=<file>: kernels record s_memtime per phase and segment; the host appends one line
 // "<kernel> <nsegs> <mean cycles of phase k - phase k-1 ...>" per call (developer profiling).
 uint64_t* phase_buf(dmx_ctx* c, uint64_t nidx) {
-    if (!std::getenv("DMX_PHASES")) return nullptr;
+    if (!(c->diag & DIAG_PHASES)) return nullptr;
     if (!c->dbg.ensure(nidx * kPhaseSlots * 8)) return nullptr;
     (void)hipMemset(c->dbg.p, 0, nidx * kPhaseSlots * 8);
     return c->dbg.as<uint64_t>();
 }
 void phase_dump(dmx_ctx* c, const char* kernel, uint64_t nidx, hipStream_t st) {
-    const char* path = std::getenv("DMX_PHASES");
-    if (!path || !c->dbg.p) return;
+    if (!(c->diag & DIAG_PHASES) || !c->dbg.p) return;
+    const char* path = diag_env().phases_path.c_str();
     std::vector<uint64_t> h(nidx * kPhaseSlots);
     (void)hipStreamSynchronize(st);
     (void)hipMemcpy(h.data(), c->dbg.p, h.size() * 8, hipMemcpyDeviceToHost);
@@ -175,15 +202,27 @@ void end_timing(dmx_ctx* c, hipStream_t st) {
     c->stats.ms_main_kernel = b;
 }
 
+// d_total != nullptr: asynchronous (dmx_deflate_device_async): the length goes to that device
+// word, nothing waits for the work.  Every deflate on a context waits for the previous one's work
+// (ev_df), whatever streams they run on: the slots, sizes and token words are reused.
 int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, uint32_t flags,
-                          uint8_t* d_out, size_t cap, size_t* out_len, hipStream_t st) {
+                          uint8_t* d_out, size_t cap, size_t* out_len, hipStream_t st,
+                          uint64_t* d_total = nullptr) {
     if (level < 0 || level > 3) level = 1;  // reference switch has no default (deflate.hpp:699)
     const bool final_last = (flags & DMX_DEFLATE_NOT_FINAL) == 0;
-    begin_timing(c, st);
+    const bool async = d_total != nullptr;
+    if (c->df_pending) HIPCHK(hipStreamWaitEvent(st, c->ev_df, 0));
+    if (!async) begin_timing(c, st);
     if (n == 0) {
         // empty input: one empty fixed-Huffman final block, as the reference's levels 1-3
         static const uint8_t empty_final[2] = {0x03, 0x00};
-        *out_len = final_last ? 2 : 0;
+        static const uint64_t lens[2] = {0, 2};
+        if (out_len) *out_len = final_last ? 2 : 0;
+        if (async) {
+            if (final_last && cap >= 2) HIPCHK(hipMemcpyAsync(d_out, empty_final, 2, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(d_total, &lens[final_last ? 1 : 0], 8, hipMemcpyHostToDevice, st));
+            return DMX_OK;
+        }
         if (!final_last) return DMX_OK;
         if (cap < 2) return DMX_ERR_CAPACITY;
         HIPCHK(hipMemcpyAsync(d_out, empty_final, 2, hipMemcpyHostToDevice, st));
@@ -210,11 +249,15 @@ int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, 
     A.ntok = c->dntok.as<uint32_t>();
     A.sizes = c->sizes.as<uint32_t>();
     A.offsets = c->offs.as<uint64_t>();
-    A.total = &c->scal.as<Scal>()->total;
+    A.total = async ? d_total : &c->scal.as<Scal>()->total;
     A.out = d_out;
     A.cap = cap;
-    A.dbg = phase_buf(c, nseg);
-    HIPCHK(launch_deflate(A, c->seg, st, c->timing ? c->ev[1] : nullptr, c->timing ? c->ev[2] : nullptr));
+    A.dbg = async ? nullptr : phase_buf(c, nseg);
+    const bool tm = c->timing && !async;
+    HIPCHK(launch_deflate(A, c->seg, st, tm ? c->ev[1] : nullptr, tm ? c->ev[2] : nullptr));
+    HIPCHK(hipEventRecord(c->ev_df, st));
+    c->df_pending = true;
+    if (async) return DMX_OK;
     if (A.dbg) phase_dump(c, "deflate", nseg, st);
     uint64_t total = 0;
     HIPCHK(hipMemcpyAsync(&total, A.total, 8, hipMemcpyDeviceToHost, st));
@@ -232,14 +275,8 @@ int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, 
 // stream to the serial decoder (no chain from bit 0 to a BFINAL block, a unit that errors or
 // runs out of token space, a copy from before the stream start): results and error codes are
 // then the serial decoder's, i.e. the reference's.
-// DMX_FB_SERIAL=1: path 5 decodes every unit with one wavefront (A/B reference for k_fb_pdecode)
-static bool fb_serial_only() {
-    static const bool v = [] {
-        const char* e = std::getenv("DMX_FB_SERIAL");
-        return e && *e == '1';
-    }();
-    return v;
-}
+// DMX_CFG_FB_SERIAL: path 5 decodes every unit with one wavefront (A/B reference for k_fb_pdecode)
+static bool fb_serial_only(const dmx_ctx* c) { return (c->flags & DMX_CFG_FB_SERIAL) != 0; }
 
 int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_out, size_t cap,
                       size_t* total_out, uint8_t** dev_out, hipStream_t st, bool* handled, uint32_t iflags) {
@@ -265,54 +302,113 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         HIPCHK(hipStreamSynchronize(st));
     }
     // units: bit 0, then every hit (sorted: chunks in order, lanes in order within a chunk);
-    // dynamic-header hits are "strong" (practically never false), stored-header hits "weak"
+    // dynamic-header hits are "strong" (practically never false), stored-header hits "weak".
+    // A gap of more than kVirtGap bits between two of them is a run of blocks the scan cannot
+    // split (fixed-code blocks -- zlib's Z_FIXED, the reference's own level-1 chunks -- or one
+    // huge block): virtual units start every kVirtStep bits inside it, each decoded from a
+    // warm-up before its start bit under the code of the gap's first block (FB_V_VIRTUAL).  The
+    // chain walk below verifies every link; a unit whose guess or warm-up failed is redone from
+    // its predecessor's exact end (FB_V_EXACT repair rounds).
     constexpr uint64_t kStored = 1ull << 62;
-    std::vector<uint64_t> starts{0};
-    std::vector<uint8_t> strong{1};
-    for (uint64_t h : hits) {
-        const uint64_t b = h & ~kStored;
-        if (b > starts.back()) {
-            starts.push_back(b);
-            strong.push_back((h & kStored) ? 0 : 1);
+    constexpr uint64_t kVirtStep = 1ull << 18, kVirtGap = 4 * kVirtStep;
+    constexpr int kRepairRounds = 4;
+    const uint64_t nbits = 8ull * n;
+    std::vector<uint64_t> starts, vhdr;
+    std::vector<uint8_t> strong, vmode;
+    {
+        std::vector<uint64_t> hs{0};
+        std::vector<uint8_t> hstr{1};
+        for (uint64_t h : hits) {
+            const uint64_t b = h & ~kStored;
+            if (b > hs.back()) {
+                hs.push_back(b);
+                hstr.push_back((h & kStored) ? 0 : 1);
+            }
+        }
+        for (size_t i = 0; i < hs.size(); i++) {
+            starts.push_back(hs[i]);
+            strong.push_back(hstr[i]);
+            vmode.push_back(FB_V_HEADER);
+            vhdr.push_back(0);
+            const uint64_t next = i + 1 < hs.size() ? hs[i + 1] : nbits;
+            if (next - hs[i] > kVirtGap)
+                for (uint64_t b = hs[i] + kVirtStep; b + kVirtStep / 2 < next; b += kVirtStep) {
+                    starts.push_back(b);
+                    strong.push_back(0);
+                    vmode.push_back(FB_V_VIRTUAL);
+                    vhdr.push_back(hs[i]);
+                }
         }
     }
     const uint64_t K = starts.size();
-    const uint64_t nbits = 8ull * n;
-    // a unit stops after passing the next strong start (or on landing on any start): stops[k];
-    // token words: at most one per bit up to where it can stop, plus room for the block that
-    // crosses that start; a weak unit (a stored block -- two words -- then possibly fixed-code
-    // blocks up to the next dynamic one) gets 64 Ki words, and overflowing them sends the
-    // stream to the serial decoder.  16-B groups.
-    std::vector<uint64_t> stops(K), tokoff(K + 1);
-    uint64_t next_strong = ~0ull >> 1;  // no strong start after: never stop on passing one
-    for (uint64_t k = K; k-- > 0;) {
-        stops[k] = next_strong | (strong[k] ? 0ull : 1ull << 63);  // bit 63: stored-header unit
-        if (strong[k]) next_strong = starts[k];
+    // stops: a unit stops after passing the next strong start (or on landing on any start); when
+    // the next unit is virtual, at the first token boundary at or past its start bit (soft).
+    // Token words: at most one per bit up to where it can stop, plus room for the block that
+    // crosses that start; a weak unit with a hard stop (a stored block -- two words -- then
+    // possibly fixed-code blocks up to the next dynamic one) gets 64 Ki words, and overflowing
+    // them sends the stream to the serial decoder.  16-B groups.
+    auto next_strong_after = [&](uint64_t pos) -> uint64_t {  // first scanned strong start > pos
+        for (uint64_t k = (uint64_t)(std::upper_bound(starts.begin(), starts.begin() + K, pos) - starts.begin()); k < K; k++)
+            if (strong[k]) return starts[k];
+        return FB_STOP_MASK;
+    };
+    auto stop_of = [&](uint64_t pos, bool weak) -> uint64_t {  // the stop of a unit starting at pos
+        const uint64_t k = (uint64_t)(std::upper_bound(starts.begin(), starts.begin() + K, pos) - starts.begin());
+        const uint64_t st = (k < K && vmode[k] == FB_V_VIRTUAL) ? (starts[k] | FB_STOP_SOFT) : next_strong_after(pos);
+        return st | (weak ? FB_STOP_WEAK : 0ull);
+    };
+    auto words_of = [&](uint64_t pos, uint64_t stop) -> uint64_t {
+        const bool bounded = !(stop & FB_STOP_WEAK) || (stop & FB_STOP_SOFT);
+        const uint64_t w = bounded ? std::min<uint64_t>(stop & FB_STOP_MASK, nbits) - std::min(pos, nbits) + 4096 : 4096 + 65536;
+        return (w + 63) & ~63ull;
+    };
+    const uint64_t R = std::max<uint64_t>(256, K / 4), Kcap = K + R;  // room for repair units
+    std::vector<uint64_t> stops(Kcap), tokoff(Kcap + 1);
+    starts.resize(Kcap);
+    vhdr.resize(Kcap);
+    vmode.resize(Kcap);
+    {
+        uint64_t next_strong = FB_STOP_MASK;
+        for (uint64_t k = K; k-- > 0;) {
+            if (k + 1 < K && vmode[k + 1] == FB_V_VIRTUAL) stops[k] = starts[k + 1] | FB_STOP_SOFT;
+            else stops[k] = next_strong;
+            if (vmode[k] == FB_V_HEADER && !strong[k]) stops[k] |= FB_STOP_WEAK;
+            if (strong[k]) next_strong = starts[k];
+        }
     }
     tokoff[0] = 0;
-    for (uint64_t k = 0; k < K; k++) {
-        // (a strong unit's stop has bit 63 clear: std::min, not the host min(int, int))
-        const uint64_t words = strong[k] ? std::min<uint64_t>(stops[k], nbits) - starts[k] + 4096 : 4096 + 65536;
-        tokoff[k + 1] = tokoff[k] + ((words + 63) & ~63ull);
-    }
-    if (!c->fbs.ensure(K * 8) || !c->fbt.ensure((K + 1) * 8) || !c->fbk.ensure(tokoff[K] * 4) ||
-        !c->fbu.ensure(K * sizeof(FbUnit)) || !c->fbstop.ensure(K * 8))
+    for (uint64_t k = 0; k < K; k++) tokoff[k + 1] = tokoff[k] + words_of(starts[k], stops[k]);
+    const uint64_t rep_words = std::min<uint64_t>(tokoff[K] + 4096 * R, 1ull << 28);  // repairs' tokens
+    if (!c->fbs.ensure(Kcap * 8) || !c->fbt.ensure((Kcap + 1) * 8) || !c->fbk.ensure((tokoff[K] + rep_words) * 4) ||
+        !c->fbu.ensure(Kcap * sizeof(FbUnit)) || !c->fbstop.ensure(Kcap * 8) || !c->fbvm.ensure(Kcap) ||
+        !c->fbvh.ensure(Kcap * 8))
         return DMX_OK;
-    HIPCHK(hipMemcpyAsync(c->fbs.p, starts.data(), K * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->fbstop.p, stops.data(), K * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->fbt.p, tokoff.data(), (K + 1) * 8, hipMemcpyHostToDevice, st));
-    static const bool fb_debug = [] {  // developer aid: unit outcomes, chain breaks
-        const char* e = std::getenv("DMX_FB_DEBUG");
-        return e && *e;
-    }();
+    auto upload = [&](uint64_t k0, uint64_t cnt) -> int {
+        HIPCHK(hipMemcpyAsync(c->fbs.as<uint64_t>() + k0, &starts[k0], cnt * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(c->fbstop.as<uint64_t>() + k0, &stops[k0], cnt * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(c->fbt.as<uint64_t>() + k0, &tokoff[k0], (cnt + 1) * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(c->fbvm.as<uint8_t>() + k0, &vmode[k0], cnt, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(c->fbvh.as<uint64_t>() + k0, &vhdr[k0], cnt * 8, hipMemcpyHostToDevice, st));
+        return DMX_OK;
+    };
+    if (upload(0, K) != DMX_OK) return DMX_ERR_DEVICE;
+    const bool fb_debug = (c->diag & DIAG_FB) != 0;  // developer aid: unit outcomes, chain breaks
     uint32_t* dstats = nullptr;
     if (fb_debug && c->fbopen.ensure(64)) {
         dstats = c->fbopen.as<uint32_t>();
         HIPCHK(hipMemsetAsync(dstats, 0, 40, st));
     }
-    HIPCHK(launch_fb_decode(words, misalign, n, c->fbs.as<uint64_t>(), c->fbstop.as<uint64_t>(), K,
-                            c->fbt.as<uint64_t>(), c->fbk.as<uint32_t>(), c->fbu.as<FbUnit>(), c->flags | iflags,
-                            !fb_serial_only(), dstats, st));
+    std::vector<FbUnit> units(Kcap);
+    auto decode = [&](uint64_t u0, uint64_t cnt) -> int {
+        HIPCHK(launch_fb_decode(words, misalign, n, c->fbs.as<uint64_t>(), c->fbstop.as<uint64_t>(),
+                                c->fbvm.as<uint8_t>(), c->fbvh.as<uint64_t>(), K, u0, cnt, c->fbt.as<uint64_t>(),
+                                c->fbk.as<uint32_t>(), c->fbu.as<FbUnit>(), c->flags | iflags, !fb_serial_only(c),
+                                dstats, st));
+        HIPCHK(hipMemcpyAsync(&units[u0], c->fbu.as<FbUnit>() + u0, cnt * sizeof(FbUnit), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        return DMX_OK;
+    };
+    if (decode(0, K) != DMX_OK) return DMX_ERR_DEVICE;
     if (dstats) {
         uint32_t hs[10];
         HIPCHK(hipMemcpyAsync(hs, dstats, 40, hipMemcpyDeviceToHost, st));
@@ -322,32 +418,92 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
                      "stream-start copy %u\n",
                      (unsigned long long)K, hs[0], hs[1], hs[2], hs[3], hs[4], hs[5], hs[6], hs[7], hs[8], hs[9]);
     }
-    std::vector<FbUnit> units(K);
-    HIPCHK(hipMemcpyAsync(units.data(), c->fbu.p, K * sizeof(FbUnit), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    // chain from bit 0: each unit must end where the next one on the chain starts
+    // chain from bit 0: each unit must end exactly where the next one on the chain starts (its
+    // recorded start: a virtual unit's is the token boundary its warm-up found).  Every break --
+    // an end where no decoded unit starts -- gets a repair unit that starts exactly there, in
+    // the code state the unit before it ended in; the walk goes on optimistically past a break
+    // (from the next unit that starts after it), so one round repairs them all.
     std::vector<uint32_t> chain;
     std::vector<uint64_t> coffs, csizes;
-    uint64_t total = 0, k = 0;
+    uint64_t total = 0, Ku = K;
     auto chain_break = [&](const char* why, uint64_t k) {
         if (fb_debug)
-            std::fprintf(stderr, "dmx fb: chain breaks at unit %llu of %llu (%s): start %llu end %llu size %llu flags %u strong %d\n",
-                         (unsigned long long)k, (unsigned long long)K, why, (unsigned long long)units[k].start,
-                         (unsigned long long)units[k].end, (unsigned long long)units[k].size, units[k].flags,
-                         (int)strong[k]);
+            std::fprintf(stderr, "dmx fb: chain breaks at unit %llu of %llu (%s): start %llu end %llu size %llu flags %u\n",
+                         (unsigned long long)k, (unsigned long long)Ku, why, (unsigned long long)units[k].start,
+                         (unsigned long long)units[k].end, (unsigned long long)units[k].size, units[k].flags);
         return DMX_OK;
     };
-    for (;;) {
-        const FbUnit& u = units[k];
-        if (u.flags & ~SEGF_FINAL) return chain_break("unit error", k);
-        chain.push_back((uint32_t)k);
-        coffs.push_back(total);
-        csizes.push_back(u.size);
-        total += u.size;
-        if (u.flags & SEGF_FINAL) break;
-        const auto it = std::lower_bound(starts.begin() + k + 1, starts.end(), u.end);
-        if (it == starts.end() || *it != u.end) return chain_break("end is no unit start", k);
-        k = (uint64_t)(it - starts.begin());
+    uint64_t rep_used = 0;
+    for (int round = 0;; round++) {
+        std::vector<std::pair<uint64_t, uint32_t>> by;  // (recorded start, unit) of units decoded without error
+        by.reserve(Ku);
+        for (uint64_t k = 0; k < Ku; k++)
+            if (!(units[k].flags & SEGF_ERRORS)) by.emplace_back(units[k].start, (uint32_t)k);
+        std::sort(by.begin(), by.end());
+        chain.clear();
+        coffs.clear();
+        csizes.clear();
+        total = 0;
+        std::vector<std::pair<uint64_t, uint64_t>> breaks;  // (end bit, code state)
+        bool fin = false;
+        if (units[0].flags & SEGF_ERRORS) return chain_break("unit error", 0);
+        uint64_t k = 0;
+        // the BFINAL bit of the block in force where the walk stands: a virtual unit that passed
+        // no block header only guessed it (not final), its predecessor's reading holds
+        bool final_in_force = false;
+        for (;;) {
+            const FbUnit& u = units[k];
+            chain.push_back((uint32_t)k);
+            coffs.push_back(total);
+            csizes.push_back(u.size);
+            total += u.size;
+            if (u.flags & SEGF_FINAL) {
+                fin = true;
+                break;
+            }
+            uint64_t state = u.hdr;
+            if (state != FB_AT_HEADER) {
+                const bool own = vmode[k] != FB_V_VIRTUAL || (u.flags & SEGF_CROSSED);
+                if (!own) state = (state & ~FB_STATE_FINAL) | (final_in_force ? FB_STATE_FINAL : 0ull);
+                final_in_force = (state & FB_STATE_FINAL) != 0;
+            }
+            auto it = std::lower_bound(by.begin(), by.end(), std::make_pair(u.end, 0u));
+            if (it != by.end() && it->first == u.end) {
+                // inside a final block a virtual unit is right only up to a soft stop: one that
+                // passed a header or ended at one read past the final end of block (its guess
+                // said not final), and is redone from here with the final state
+                const FbUnit& v = units[it->second];
+                const bool in_final = state != FB_AT_HEADER && (state & FB_STATE_FINAL);
+                if (!(in_final && vmode[it->second] == FB_V_VIRTUAL &&
+                      ((v.flags & SEGF_CROSSED) || v.hdr == FB_AT_HEADER))) {
+                    k = it->second;
+                    continue;
+                }
+            }
+            breaks.emplace_back(u.end, state);
+            if (it == by.end()) break;
+            k = it->second;  // (optimistic: the first unit starting after the break)
+        }
+        if (fin && breaks.empty()) break;
+        if (breaks.empty() || round == kRepairRounds || Ku + breaks.size() > Kcap)
+            return chain_break(fin ? "repairs exhausted" : "no final block", chain.back());
+        // repair units, appended at [Ku, Ku + breaks)
+        const uint64_t k0 = Ku;
+        for (const auto& br : breaks) {
+            const uint64_t e = br.first;
+            starts[Ku] = e;
+            vmode[Ku] = br.second == FB_AT_HEADER ? FB_V_HEADER : FB_V_EXACT;
+            vhdr[Ku] = br.second == FB_AT_HEADER ? 0 : br.second;
+            stops[Ku] = stop_of(e, false);
+            const uint64_t w = words_of(e, stops[Ku]);
+            if (rep_used + w > rep_words) return chain_break("repair token space", chain.back());
+            tokoff[Ku + 1] = tokoff[Ku] + w;
+            rep_used += w;
+            Ku++;
+        }
+        if (upload(k0, Ku - k0) != DMX_OK || decode(k0, Ku - k0) != DMX_OK) return DMX_ERR_DEVICE;
+        if (fb_debug)
+            std::fprintf(stderr, "dmx fb: repair round %d: %llu units\n", round, (unsigned long long)(Ku - k0));
     }
     // the path's own scratch first: when it does not fit, the stream still decodes on the
     // serial decoder, which needs only the output
@@ -371,13 +527,13 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     // the parallel window hand-off when its scratch fits (nch * 128 KiB), else the serial one
     uint32_t *win = nullptr, *open = nullptr;
     const uint64_t went = fb_window_entries(nch);
-    if (went && !fb_serial_only() && c->fbwin.ensure(went * 4) && c->fbopen.ensure(fb_window_rounds(nch) * 4)) {
+    if (went && !fb_serial_only(c) && c->fbwin.ensure(went * 4) && c->fbopen.ensure(fb_window_rounds(nch) * 4)) {
         win = c->fbwin.as<uint32_t>();
         open = c->fbopen.as<uint32_t>();
     }
     // the workgroup replay needs a 32-bit image of the output
     uint32_t* p32 = nullptr;
-    if (!fb_serial_only() && c->fbp32.ensure(total * 4 + 16)) p32 = c->fbp32.as<uint32_t>();
+    if (!fb_serial_only(c) && c->fbp32.ensure(total * 4 + 16)) p32 = c->fbp32.as<uint32_t>();
     HIPCHK(launch_fb_resolve(d_in, c->fbs.as<uint64_t>(), c->fbch.as<uint32_t>(), c->fbco.as<uint64_t>(),
                              c->fbcs.as<uint64_t>(), nch, c->fbt.as<uint64_t>(), c->fbk.as<uint32_t>(),
                              c->fbu.as<FbUnit>(), c->fbimg.as<uint16_t>(), total, out, &ds->fb_err, win, open,
@@ -464,10 +620,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     // segment sizes; then the wave-per-segment decoder, which places segments of any size
     // <= 32 KiB by look-back.  Each pass runs only if the previous one reported status 1 (a
     // segment outside its layout or sizes not uniform); status 2 goes to the serial decoder.
-    static const int path_env = [] {
-        const char* e = std::getenv("DMX_INFLATE_PATH");
-        return e ? std::atoi(e) : -1;
-    }();
+    const int path_env = c->inflate_pass;  // developer A/B (dmx_config.dev_inflate_pass)
     // Heavy candidates (mode 6): a lane decodes about one symbol per 1000 cycles, so the lane
     // decoder takes as long as the serial decode of the densest segment in a wave (a 24 MiB
     // bitmap: 6 ms for ~10K symbols).  Candidates spanning more than heavy_bytes compressed
@@ -477,8 +630,8 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     // more dense segments than that keep the lanes' throughput: 1 GiB of text).
     // A stream of at most one candidate per CU takes one round of workgroups, which beats the
     // lanes' ~0.3 ms floor (a wave's header, table and token phases) from 256 bytes up.
-    static const char* const heavy_env = std::getenv("DMX_HEAVY_BYTES");
-    static const uint32_t heavy_bytes = heavy_env ? (uint32_t)std::strtoul(heavy_env, nullptr, 10) : 2048u;
+    const bool heavy_env = c->heavy_bytes != 0;
+    const uint32_t heavy_bytes = heavy_env ? c->heavy_bytes : 2048u;
     const bool few_bits = n / ncand < 4096;
     uint32_t plan[8][2];
     int np = 0;
@@ -546,7 +699,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
             if (A.dbg) phase_dump(c, "inflate", ncand, st);
             HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
-            if (std::getenv("DMX_RECS")) {  // developer aid: per-candidate outcome of this pass
+            if (c->diag & DIAG_RECS) {  // developer aid: per-candidate outcome of this pass
                 std::vector<SegRecord> h(ncand);
                 (void)hipMemcpy(h.data(), A.recs, ncand * sizeof(SegRecord), hipMemcpyDeviceToHost);
                 uint64_t fl[8] = {0}, shown = 0;
@@ -778,6 +931,183 @@ struct DeviceGuard {
     }
 };
 
+// ---- n_gpus > 1: the host-buffer API over several devices ---------------------
+// Deflate: contiguous segment-aligned shards, one per sub-context, each deflated NOT_FINAL except
+// the last non-empty one; one host thread per shard (the pageable H2D / D2H copies of different
+// devices then overlap), sizes first, then every shard's bytes straight to its offset in `out`.
+// Segments are independent (the reference resets its window per chunk, deflate.hpp:689-697), so
+// the bytes equal the one-device stream.
+template <class F>
+void run_parallel(size_t G, F&& f) {
+    std::vector<std::thread> th;
+    for (size_t g = 1; g < G; g++) th.emplace_back(f, g);
+    f((size_t)0);
+    for (auto& t : th) t.join();
+}
+
+int deflate_multi(dmx_ctx* c, const uint8_t* in, size_t n, int level, uint8_t* out, size_t cap,
+                  size_t* out_len) {
+    const size_t G = c->subs.size(), seg = c->seg;
+    size_t per = (n + G - 1) / G;
+    per = (per + seg - 1) / seg * seg;
+    std::vector<size_t> b(G), e(G), len(G, 0);
+    std::vector<int> rc(G, DMX_OK);
+    size_t last = 0, used = 0;
+    for (size_t g = 0; g < G; g++) {
+        b[g] = std::min(n, g * per);
+        e[g] = std::min(n, b[g] + per);
+        if (e[g] > b[g]) last = g, used++;
+    }
+    run_parallel(G, [&](size_t g) {
+        if (e[g] == b[g]) return;
+        dmx_ctx* s = c->subs[g];
+        std::lock_guard<std::mutex> lk(s->mu);
+        DeviceGuard dg(s->device);
+        const size_t m = e[g] - b[g];
+        if (!dg.ok) rc[g] = DMX_ERR_DEVICE;
+        else if (!s->in.ensure(m + 16) || !s->out.ensure(dmx_deflate_bound(m))) rc[g] = DMX_ERR_NOMEM;
+        else if (hipMemcpyAsync(s->in.p, in + b[g], m, hipMemcpyHostToDevice, s->stream) != hipSuccess) rc[g] = DMX_ERR_DEVICE;
+        else rc[g] = deflate_device_locked(s, s->in.as<uint8_t>(), m, level, g == last ? 0u : DMX_DEFLATE_NOT_FINAL,
+                                           s->out.as<uint8_t>(), s->out.cap, &len[g], s->stream);
+    });
+    size_t total = 0;
+    for (size_t g = 0; g < G; g++) {
+        if (rc[g] != DMX_OK) return rc[g];
+        total += len[g];
+    }
+    *out_len = total;
+    if (total > cap) return DMX_ERR_CAPACITY;
+    std::vector<size_t> off(G, 0);
+    for (size_t g = 1; g < G; g++) off[g] = off[g - 1] + len[g - 1];
+    run_parallel(G, [&](size_t g) {
+        if (!len[g]) return;
+        dmx_ctx* s = c->subs[g];
+        DeviceGuard dg(s->device);
+        if (hipMemcpyAsync(out + off[g], s->out.p, len[g], hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
+            hipStreamSynchronize(s->stream) != hipSuccess)
+            rc[g] = DMX_ERR_DEVICE;
+    });
+    for (size_t g = 0; g < G; g++)
+        if (rc[g] != DMX_OK) return rc[g];
+    c->stats = dmx_stats{};
+    c->stats.in_bytes = n;
+    c->stats.out_bytes = total;
+    c->stats.shards = (uint32_t)used;
+    return DMX_OK;
+}
+
+// Inflate: sub-context 0 indexes the candidate segment starts (the bytes after every 00 00 FF FF)
+// and proves cuts near equal shares of them with a piece-mode decode of the segment there (it must
+// end on another candidate: a marker inside stored data is no cut); every sub-context decodes its
+// piece (closed with an empty final block; pieces after the first in piece mode, where a
+// reference before the piece is an error), then the outputs land at their offsets: in `out`
+// (at most cap bytes, *written) or in a malloc'd buffer (*alloc).  Returns 1 when the stream does
+// not split (fewer than G proven cuts' worth of candidates, or a piece fails): the caller then
+// decodes it on one device, so the result never depends on the split.
+int inflate_multi(dmx_ctx* c, const uint8_t* in, size_t n, uint8_t* out, size_t cap, uint8_t** alloc,
+                  size_t* written, size_t* total_out) {
+    const size_t G = c->subs.size();
+    dmx_ctx* s0 = c->subs[0];
+    std::vector<uint64_t> starts;
+    {
+        DeviceGuard dg(s0->device);
+        if (!dg.ok) return 1;
+        {
+            std::lock_guard<std::mutex> lk(s0->mu);
+            if (!s0->in.ensure(n + 16) || hipMemcpyAsync(s0->in.p, in, n, hipMemcpyHostToDevice, s0->stream) != hipSuccess)
+                return 1;
+        }
+        size_t cnt = 0;
+        if (dmx_segment_starts_device(s0, s0->in.p, n, nullptr, 0, &cnt, nullptr) != DMX_OK || cnt + 1 < 2 * G) return 1;
+        starts.resize(cnt);
+        if (dmx_segment_starts_device(s0, s0->in.p, n, starts.data(), cnt, &cnt, nullptr) != DMX_OK) return 1;
+        // cut candidates: up to 8 around each target, proven in one batched check
+        std::vector<uint64_t> near;
+        for (size_t r = 1; r < G; r++) {
+            const size_t t = r * starts.size() / G;
+            for (size_t j = (t >= 4 ? t - 4 : 0); j < std::min(starts.size(), t + 4); j++)
+                if (starts[j] < n) near.push_back(starts[j]);
+        }
+        std::sort(near.begin(), near.end());
+        near.erase(std::unique(near.begin(), near.end()), near.end());
+        std::vector<uint64_t> ends(near.size());
+        if (dmx_segment_check_device(s0, s0->in.p, n, near.data(), near.size(), ends.data(), nullptr) != DMX_OK) return 1;
+        std::vector<uint64_t> ok;
+        for (size_t i = 0; i < near.size(); i++)
+            if (ends[i] != UINT64_MAX && ends[i] > near[i] &&
+                (ends[i] == n || std::binary_search(starts.begin(), starts.end(), ends[i])))
+                ok.push_back(near[i]);
+        std::vector<uint64_t> cut{0};
+        for (size_t r = 1; r < G; r++) {
+            const uint64_t target = starts[r * starts.size() / G];
+            uint64_t best = 0, bd = UINT64_MAX;
+            for (uint64_t x : ok)
+                if (x > cut.back() && (x > target ? x - target : target - x) < bd) best = x, bd = x > target ? x - target : target - x;
+            if (!best) return 1;
+            cut.push_back(best);
+        }
+        cut.push_back(n);
+        starts = cut;
+    }
+    std::vector<size_t> len(G, 0);
+    std::vector<int> rc(G, DMX_OK);
+    std::vector<uint8_t*> dev(G, nullptr);
+    run_parallel(G, [&](size_t g) {
+        dmx_ctx* s = c->subs[g];
+        std::lock_guard<std::mutex> lk(s->mu);
+        DeviceGuard dg(s->device);
+        const size_t a = starts[g], m = starts[g + 1] - a;
+        static const uint8_t close[2] = {0x03, 0x00};  // an empty final block ends the piece
+        const bool closes = g + 1 < G;
+        if (!dg.ok || !s->in.ensure(m + 16) ||
+            hipMemcpyAsync(s->in.p, in + a, m, hipMemcpyHostToDevice, s->stream) != hipSuccess ||
+            (closes && hipMemcpyAsync(s->in.as<uint8_t>() + m, close, 2, hipMemcpyHostToDevice, s->stream) != hipSuccess)) {
+            rc[g] = DMX_ERR_DEVICE;
+            return;
+        }
+        rc[g] = inflate_device_locked(s, s->in.as<uint8_t>(), m + (closes ? 2 : 0), nullptr, 0, &len[g], &dev[g],
+                                      s->stream, g ? DMX_IFLAG_PIECE : 0u);
+    });
+    for (size_t g = 0; g < G; g++)
+        if (rc[g] != DMX_OK) return 1;
+    size_t total = 0;
+    std::vector<size_t> off(G, 0);
+    for (size_t g = 0; g < G; g++) {
+        off[g] = total;
+        total += len[g];
+    }
+    uint8_t* dst = out;
+    size_t lim = cap;
+    if (alloc) {
+        dst = static_cast<uint8_t*>(std::malloc(total ? total : 1));
+        if (!dst) return DMX_ERR_NOMEM;
+        lim = total;
+    }
+    run_parallel(G, [&](size_t g) {
+        const size_t w = off[g] >= lim ? 0 : std::min(len[g], lim - off[g]);
+        if (!w) return;
+        dmx_ctx* s = c->subs[g];
+        DeviceGuard dg(s->device);
+        if (hipMemcpyAsync(dst + off[g], dev[g], w, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
+            hipStreamSynchronize(s->stream) != hipSuccess)
+            rc[g] = DMX_ERR_DEVICE;
+    });
+    for (size_t g = 0; g < G; g++)
+        if (rc[g] != DMX_OK) {
+            if (alloc) std::free(dst);
+            return DMX_ERR_DEVICE;
+        }
+    if (alloc) *alloc = dst;
+    if (written) *written = std::min(total, lim);
+    *total_out = total;
+    c->stats = dmx_stats{};
+    c->stats.in_bytes = n;
+    c->stats.out_bytes = total;
+    c->stats.path = 4;
+    c->stats.shards = (uint32_t)G;
+    return DMX_OK;
+}
+
 bool is_gfx950(int dev) {
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, dev) != hipSuccess) return false;
@@ -792,6 +1122,9 @@ void dmx_config_default(dmx_config* cfg) {
     cfg->device = -1;
     cfg->segment_bytes = 32768;
     cfg->flags = 0;
+    cfg->n_gpus = 1;
+    cfg->dev_inflate_pass = 0;
+    cfg->dev_heavy_bytes = 0;
 }
 
 int dmx_create(dmx_ctx** out, const dmx_config* cfg) {
@@ -813,36 +1146,75 @@ int dmx_create(dmx_ctx** out, const dmx_config* cfg) {
     c->device = dev;
     c->seg = cfg->segment_bytes;
     c->flags = cfg->flags;
+    c->inflate_pass = (int)cfg->dev_inflate_pass - 1;
+    c->heavy_bytes = cfg->dev_heavy_bytes;
+    c->diag = diag_env().bits;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return DMX_ERR_DEVICE;
     }
     for (auto& e : c->ev) (void)hipEventCreate(&e);
+    if (hipEventCreateWithFlags(&c->ev_df, hipEventDisableTiming) != hipSuccess) {
+        dmx_destroy(c);
+        return DMX_ERR_DEVICE;
+    }
+    if (cfg->n_gpus > 1) {  // one context per shard, round-robin over the visible devices
+        dmx_config sc = *cfg;
+        sc.n_gpus = 1;
+        for (uint32_t i = 0; i < cfg->n_gpus; i++) {
+            sc.device = (dev + (int)i) % ndev;
+            dmx_ctx* s = nullptr;
+            const int rc = is_gfx950(sc.device) ? dmx_create(&s, &sc) : DMX_ERR_DEVICE;
+            if (rc != DMX_OK) {
+                dmx_destroy(c);
+                return rc;
+            }
+            c->subs.push_back(s);
+        }
+    }
     *out = c;
     return DMX_OK;
 }
 
 void dmx_destroy(dmx_ctx* c) {
     if (!c) return;
+    for (dmx_ctx* s : c->subs) dmx_destroy(s);
+    c->subs.clear();
     DeviceGuard dg(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->in, &c->out, &c->slots, &c->sizes, &c->offs, &c->scal, &c->cands,
                       &c->tiles, &c->tileoffs, &c->recs, &c->status, &c->dbg, &c->ltok,
                       &c->ltokoff, &c->lntok, &c->lcaps, &c->lheavy, &c->rtmp, &c->rchain, &c->fbc, &c->fbh, &c->fbo, &c->fbl,
-                      &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg, &c->fbstop, &c->fbwin, &c->fbopen, &c->fbp32,
+                      &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg, &c->fbstop, &c->fbwin, &c->fbopen, &c->fbp32, &c->fbvm, &c->fbvh,
                       &c->ck})
         b->release();
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->ev_df) (void)hipEventDestroy(c->ev_df);
     (void)hipStreamDestroy(c->stream);
     delete c;
+}
+
+static std::mutex g_default_mu;
+static dmx_config g_default_cfg;
+static bool g_default_set = false, g_default_made = false;
+
+int dmx_set_default_config(const dmx_config* cfg) {
+    if (!cfg) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(g_default_mu);
+    if (g_default_made) return DMX_ERR_ARG;
+    g_default_cfg = *cfg;
+    g_default_set = true;
+    return DMX_OK;
 }
 
 dmx_ctx* dmx_default_ctx(void) {
     static std::once_flag once;
     static dmx_ctx* ctx = nullptr;
     std::call_once(once, [] {
-        if (dmx_create(&ctx, nullptr) != DMX_OK) ctx = nullptr;
+        std::lock_guard<std::mutex> g(g_default_mu);
+        g_default_made = true;
+        if (dmx_create(&ctx, g_default_set ? &g_default_cfg : nullptr) != DMX_OK) ctx = nullptr;
     });
     return ctx;
 }
@@ -858,6 +1230,17 @@ int dmx_deflate_device(dmx_ctx* c, const void* d_in, size_t n, int level, uint32
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     return deflate_device_locked(c, (const uint8_t*)d_in, n, level, flags, (uint8_t*)d_out, cap,
                                  out_len, st);
+}
+
+int dmx_deflate_device_async(dmx_ctx* c, const void* d_in, size_t n, int level, uint32_t flags,
+                             void* d_out, size_t cap, uint64_t* d_out_len, void* stream) {
+    if (!c || (!d_in && n) || !d_out || !d_out_len) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return deflate_device_locked(c, (const uint8_t*)d_in, n, level, flags, (uint8_t*)d_out, cap,
+                                 nullptr, st, d_out_len);
 }
 
 int dmx_inflate_device(dmx_ctx* c, const void* d_in, size_t n, void* d_out, size_t cap,
@@ -888,6 +1271,8 @@ int dmx_deflate(dmx_ctx* c, const uint8_t* in, size_t n, int level, uint8_t* out
     if (!c) return DMX_ERR_DEVICE;
     if ((!in && n) || !out_len || (!out && cap)) return DMX_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->subs.size() > 1 && n >= 2 * c->subs.size() * (size_t)c->seg)
+        return deflate_multi(c, in, n, level, out, cap, out_len);
     DeviceGuard dg(c->device);
     if (!dg.ok) return DMX_ERR_DEVICE;
     const size_t bound = dmx_deflate_bound(n);
@@ -922,6 +1307,13 @@ int dmx_inflate(dmx_ctx* c, const uint8_t* in, size_t n, uint8_t* out, size_t ca
     size_t tot = 0;
     *written = 0;
     if (total) *total = 0;
+    if (c->subs.size() > 1 && n >= 4 * c->subs.size() * (size_t)c->seg) {
+        const int mr = inflate_multi(c, in, n, out, cap, nullptr, written, &tot);
+        if (mr != 1) {
+            if (total) *total = tot;
+            return mr;
+        }
+    }
     int rc = inflate_host(c, in, n, &dev, &tot);
     if (rc != DMX_OK) return rc;
     const size_t w = tot < cap ? tot : cap;
@@ -943,6 +1335,13 @@ int dmx_inflate_alloc(dmx_ctx* c, const uint8_t* in, size_t n, uint8_t** out, si
     *len = 0;
     uint8_t* dev = nullptr;
     size_t tot = 0;
+    if (c->subs.size() > 1 && n >= 4 * c->subs.size() * (size_t)c->seg) {
+        const int mr = inflate_multi(c, in, n, nullptr, 0, out, nullptr, &tot);
+        if (mr != 1) {
+            if (mr == DMX_OK) *len = tot;
+            return mr;
+        }
+    }
     int rc = inflate_host(c, in, n, &dev, &tot);
     if (rc != DMX_OK) return rc;
     uint8_t* h = static_cast<uint8_t*>(std::malloc(tot ? tot : 1));

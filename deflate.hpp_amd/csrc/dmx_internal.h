@@ -125,12 +125,38 @@ hipError_t launch_inflate_validate(const InflateArgs& A, ValidateWords* W, Infla
 
 // block-parallel inflate of arbitrary streams (inflate_blocks.hip, path 5)
 struct FbUnit {         // per-unit record written by k_fb_pdecode / k_fb_decode
-    uint64_t start;     // stream bit of the unit's first block
-    uint64_t end;       // stream bit just past its last block
+    uint64_t start;     // stream bit of the unit's first token (a block header, or for a virtual
+                        // unit the token boundary its warm-up found)
+    uint64_t end;       // stream bit where it stopped: past its last block, or (soft stop) the
+                        // first token boundary at or past its stop
     uint64_t size;      // output bytes
+    uint64_t hdr;       // state at `end`: FB_AT_HEADER, else the code in force (FB_STATE_*)
     uint32_t ntok;      // token words
     uint32_t flags;     // SEGF_*
 };
+// Units and their stops (path 5).  stops[u]: the stream bit where unit u ends, with
+constexpr uint64_t FB_STOP_WEAK = 1ull << 63;  // a stored-header (weak) unit
+constexpr uint64_t FB_STOP_SOFT = 1ull << 62;  // the next unit starts inside a block: end at the
+                                               // first token boundary at or past the stop
+constexpr uint64_t FB_STOP_MASK = FB_STOP_SOFT - 1;
+// A code state (FbUnit.hdr, the per-unit vhdr): the stream bit of the dynamic block header whose
+// code is in force, or FB_STATE_FIXED for the fixed code; FB_STATE_FINAL: that block has BFINAL.
+constexpr uint64_t FB_STATE_FIXED = 1ull << 62;
+constexpr uint64_t FB_STATE_FINAL = 1ull << 61;
+constexpr uint64_t FB_STATE_POS = FB_STATE_FINAL - 1;
+constexpr uint64_t FB_AT_HEADER = ~0ull;       // the unit ended at a block header
+// how a unit starts (vmode)
+enum : uint8_t {
+    FB_V_HEADER = 0,   // at a block header (bit 0, a scanned dynamic or stored header)
+    FB_V_VIRTUAL = 1,  // near its start bit inside a long run of blocks: warm-up decode from
+                       // before it, under the code of vhdr's block (a guess the chain verifies)
+    FB_V_EXACT = 2,    // exactly at its start bit inside a block whose code is vhdr (a repair)
+};
+constexpr uint32_t SEGF_SOFT = 1u << 30;  // internal: decode_huffman reached the soft stop
+// FbUnit flag (not an error): the unit's decode passed at least one block header after its
+// start, so the BFINAL bit of its end state is its own reading, not a virtual unit's guess
+constexpr uint32_t SEGF_CROSSED = 1u << 29;
+constexpr uint32_t SEGF_ERRORS = ~(SEGF_FINAL | SEGF_CROSSED);
 uint64_t fb_scan_chunks(uint64_t n);
 uint32_t fb_hits_per_chunk();
 // header scan of every bit offset: counts[nchunks], hits[nchunks * fb_hits_per_chunk()],
@@ -141,8 +167,10 @@ hipError_t launch_fb_scan(const uint32_t* in_words, uint64_t misalign, uint64_t 
 hipError_t launch_fb_compact(const uint32_t* counts, const uint64_t* offs, const uint64_t* hits,
                              uint64_t nchunks, uint64_t* list, hipStream_t st);
 // hits carry bit 62 for a stored-block header; stops[u] = the next dynamic-header start after u
+// units [u0, u0 + count) of the nunits listed; vmode / vhdr as above
 hipError_t launch_fb_decode(const uint32_t* in_words, uint64_t misalign, uint64_t n,
-                            const uint64_t* starts, const uint64_t* stops, uint64_t nunits,
+                            const uint64_t* starts, const uint64_t* stops, const uint8_t* vmode,
+                            const uint64_t* vhdr, uint64_t nunits, uint64_t u0, uint64_t count,
                             const uint64_t* tokoff, uint32_t* tok, FbUnit* units, uint32_t flags,
                             bool parallel, uint32_t* stats, hipStream_t st);
 // replay + window hand-off + final resolve; *err (zeroed by the caller) becomes nonzero when a

@@ -485,8 +485,11 @@ struct FbDecodeArgs {
     const uint32_t* in_words;
     uint64_t misalign, n;
     const uint64_t* starts;
-    const uint64_t* stops;
+    const uint64_t* stops;   // FB_STOP_* flags
+    const uint8_t* vmode;    // FB_V_*
+    const uint64_t* vhdr;    // code state of FB_V_VIRTUAL / FB_V_EXACT units
     uint64_t nunits;
+    uint64_t u0;             // this launch decodes units u0 + blockIdx.x
     const uint64_t* tokoff;
     uint32_t* tok;
     FbUnit* units;
@@ -495,28 +498,46 @@ struct FbDecodeArgs {
                       // start, serially after a parallel first block, weak units
 };
 
+// A fixed block that follows inside a unit is decoded serially only when it lies within this
+// many bits of the unit's stop; farther ones end the unit at their header, and the host starts a
+// unit there that decodes the run of fixed blocks lane-parallel (repair round).
+constexpr uint64_t FB_SER_FIXED_MAX = 16384;
+
 // One wavefront: realDecompress (inflate.hpp:277-322) for unit u from stream bit `from`
 // (relative to stream bit 0), appending to a token list that already holds n0 words for bytes0
 // output bytes; the unit's record is written at the end.  first: the block at `from` is the
-// unit's first, decoded before any stop check.
+// unit's first, decoded before any stop check.  mid: FB_AT_HEADER, or `from` lies inside a
+// block whose code state is mid (FB_STATE_*): that block's rest is decoded first.
 __device__ __attribute__((noinline)) void fb_serial(const FbDecodeArgs& A, uint64_t u, Tables& T, uint32_t* ring, uint64_t from,
-                          uint32_t n0, uint64_t bytes0, bool first) {
+                          uint32_t n0, uint64_t bytes0, bool first, uint64_t mid = FB_AT_HEADER) {
     if (lane_id() == 0) T.fixed_loaded = 0;
     wave_sync();
     const uint64_t start = A.starts[u];
     // A unit ends after the first block that lands exactly on another unit's start, or that
     // passes the next dynamic-header start (stored-header starts can be false: passing one
-    // inside a block is no reason to stop, landing on one is a chain link).
-    // A unit at a stored-header start (bit 63 of its stop) decodes stored and fixed-code blocks
+    // inside a block is no reason to stop, landing on one is a chain link); with a soft stop (the
+    // next unit starts inside a block) at the first token boundary at or past it.
+    // A unit at a stored-header start (FB_STOP_WEAK) decodes stored and fixed-code blocks
     // and ends before the first dynamic block (whose start is a scanned hit): such a start can
     // be false, and a false one then costs a bounded copy, or at most a fixed-code decode up to
     // the next dynamic-header start.  (Fixed blocks are not scanned, so a stored block followed
     // by fixed ones -- zlib's small blocks -- needs the weak unit to carry on through them.)
-    const bool weak = (A.stops[u] >> 63) != 0;
-    const uint64_t stop = A.stops[u] & ~(1ull << 63);
-    uint64_t jn = u + 1;  // first unit start not below the current position
-    uint64_t end_at = 0;  // (weak units) stream bit of the first block they leave undecoded
+    const bool weak = (A.stops[u] & FB_STOP_WEAK) != 0;
+    const bool soft = (A.stops[u] & FB_STOP_SOFT) != 0;
+    const uint64_t stop = A.stops[u] & FB_STOP_MASK;
+    uint64_t jn = 0;  // first listed unit start above the unit's start (repair units are
+    {                 // appended after the sorted list: search it)
+        uint64_t hi = A.nunits;
+        while (jn < hi) {
+            const uint64_t mid = (jn + hi) >> 1;
+            if (A.starts[mid] <= start) jn = mid + 1;
+            else hi = mid;
+        }
+    }
+    uint64_t end_at = 0;  // stream bit of the first block the unit leaves undecoded (weak units,
+                          // a far fixed block), else 0
     const uint64_t base = A.misalign * 8;  // stream bit 0 in the aligned image
+    const uint64_t soft_abs = soft ? base + stop : ~0ull;
     RingIn br;
     br.init(A.in_words, A.misalign, A.n, ring);
     br.seek(base + from);
@@ -532,7 +553,30 @@ __device__ __attribute__((noinline)) void fb_serial(const FbDecodeArgs& A, uint6
     const bool rfc = (A.flags & DMX_CFG_RFC_STRICT) != 0;
     uint32_t err = 0;
     bool fin = false;
-    for (bool f = first;; f = false) {
+    uint64_t state = FB_AT_HEADER;  // the code in force while inside a block
+    bool midend = false;            // stopped inside a block (soft stop)
+    const uint64_t nwords = (A.misalign + A.n + 3) / 4;
+    if (mid != FB_AT_HEADER) {  // the rest of a block whose code is `mid`
+        state = mid;
+        if (mid & FB_STATE_FIXED) {
+            load_fixed(T);
+            T.fixed_loaded = 1;
+        } else {
+            uint64_t hp = base + (mid & FB_STATE_POS) + 3;
+            err = fast_header(BitInWords{nullptr, 0, 0, A.in_words, nwords, A.misalign + A.n}, &hp,
+                              br.end_bits, T, rfc, true);
+        }
+        if (!err) err = decode_huffman(br, T, sk, soft_abs);
+        if (err == SEGF_SOFT) {
+            err = 0;
+            midend = true;
+        } else if (!err && (mid & FB_STATE_FINAL)) {
+            fin = true;
+        }
+        first = false;
+    }
+    bool crossed = false;  // a block header was read after the unit's start
+    for (bool f = first; !err && !fin && !midend; f = false) {
         if (!f) {
             const uint64_t pos = br.abspos() - base;
             if (pos >= stop) break;
@@ -544,7 +588,12 @@ __device__ __attribute__((noinline)) void fb_serial(const FbDecodeArgs& A, uint6
         const uint32_t bfinal = br.bits(1);
         const uint32_t btype = br.bits(2);
         if (br.over()) { err = SEGF_OVERREAD; break; }
+        if (!f) crossed = true;
         if (weak && btype == 2) {
+            end_at = hpos;
+            break;
+        }
+        if (!f && btype == 1 && stop - (hpos - base) > FB_SER_FIXED_MAX) {  // a far fixed run
             end_at = hpos;
             break;
         }
@@ -563,17 +612,23 @@ __device__ __attribute__((noinline)) void fb_serial(const FbDecodeArgs& A, uint6
                 load_fixed(T);
                 T.fixed_loaded = 1;
             }
-            err = decode_huffman(br, T, sk);
-            if (err) break;
+            state = FB_STATE_FIXED | (bfinal ? FB_STATE_FINAL : 0ull);
+            err = decode_huffman(br, T, sk, soft_abs);
         } else if (btype == 2) {
             T.fixed_loaded = 0;
+            state = (hpos - base) | (bfinal ? FB_STATE_FINAL : 0ull);
             uint64_t hp = br.abspos();
             err = fast_header(reader_words(br), &hp, br.end_bits, T, rfc, true);
             if (err) break;
             br.seek(hp);
-            err = decode_huffman(br, T, sk);
-            if (err) break;
+            err = decode_huffman(br, T, sk, soft_abs);
         }  // BTYPE 3: an empty block (inflate.hpp:292 has no case 3)
+        if (err == SEGF_SOFT) {
+            err = 0;
+            midend = true;
+            break;
+        }
+        if (err) break;
         if (bfinal) {
             fin = true;
             break;
@@ -586,18 +641,27 @@ __device__ __attribute__((noinline)) void fb_serial(const FbDecodeArgs& A, uint6
         r.end = (end_at ? end_at : br.abspos()) - base;
         r.size = sk.pos;
         r.ntok = sk.n;
-        r.flags = err | (fin ? SEGF_FINAL : 0u);
+        r.hdr = midend ? state : FB_AT_HEADER;
+        r.flags = err | (fin ? SEGF_FINAL : 0u) | (crossed ? SEGF_CROSSED : 0u);
         A.units[u] = r;
     }
 }
 
-// the serial decoder alone, one wavefront per unit (DMX_FB_SERIAL=1: A/B reference)
+// the serial decoder alone, one wavefront per unit (DMX_CFG_FB_SERIAL: A/B reference)
 __global__ __launch_bounds__(64) void k_fb_decode(FbDecodeArgs A) {
     __shared__ Tables T;
     __shared__ uint32_t ring[FB_RW];
-    const uint64_t u = blockIdx.x;
+    const uint64_t u = A.u0 + blockIdx.x;
     if (u >= A.nunits) return;
-    fb_serial(A, u, T, ring, A.starts[u], 0, 0, true);
+    const uint8_t vm = A.vmode[u];
+    if (vm == FB_V_VIRTUAL) {  // a guessed start: only the lane-parallel decoder's warm-up finds
+        if (threadIdx.x == 0) { // the token boundary near it (the chain repairs around it)
+            FbUnit r{A.starts[u], A.starts[u], 0, FB_AT_HEADER, 0, SEGF_ERR_DATA};
+            A.units[u] = r;
+        }
+        return;
+    }
+    fb_serial(A, u, T, ring, A.starts[u], 0, 0, true, vm == FB_V_EXACT ? A.vhdr[u] : FB_AT_HEADER);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -626,6 +690,7 @@ constexpr uint32_t FBP_IN = 14336;    // staged words (a block body of up to ~56
                                       // blocks of 16 K symbols at up to ~27 bits each)
 constexpr uint32_t FBP_MINBITS = 128;  // shortest range a lane decodes
 constexpr uint32_t FBP_WARM = 320;     // warm-up bits before a range
+constexpr uint32_t TK_NOP = 4;         // a fixed block's end of block + the next fixed header
 constexpr int FBP_ROUNDS = 1024;  // a settle cascade (data that re-synchronises slowly) still
                                    // beats the serial decoder by far
 struct FbpSmem {
@@ -642,7 +707,11 @@ struct FbpSmem {
     uint32_t kind;            // 0 parallel, 1 serial from the unit start, 2 serial continuation,
                               // 3 an error the serial decoder would report (S.err), 4 again
     uint32_t btype, bfinal, hs, nst, words, bytes, err;
+    uint32_t vs0;             // FB_V_VIRTUAL: the first token boundary the warm-up found
+    uint32_t midend;          // the unit stopped inside a block (soft stop)
+    uint32_t crossed;         // the settled path passed a fixed-block header (TK_NOP)
     uint64_t ws, he, hecap, endbit;
+    uint64_t vstate;          // the code in force (FB_STATE_*)
 };
 static_assert(sizeof(FbpSmem) <= 160 * 1024, "LDS");
 
@@ -658,45 +727,73 @@ __device__ __attribute__((noinline)) uint32_t fbp_header(Tables& T, uint32_t bty
     const StagedWords src{in, ws, nst};
     return fast_header(src, hp, end_bits, T, rfc, false);
 }
+// the same for the header of the block a mid-block unit starts in, read from HBM
+__device__ __attribute__((noinline)) uint32_t fbp_header_g(Tables& T, const uint32_t* words, uint64_t nwords,
+                                                           uint64_t end_bytes, uint64_t* hp, bool rfc) {
+    return fast_header(BitInWords{nullptr, 0, 0, words, nwords, end_bytes}, hp, end_bytes * 8, T, rfc, false);
+}
 
 __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
     __shared__ __attribute__((aligned(16))) FbpSmem S;
     constexpr int NW = FBP_NT / 64;
     const int t = threadIdx.x;
     const int wave = t >> 6;
-    const uint64_t u = blockIdx.x;
+    const uint64_t u = A.u0 + blockIdx.x;
     const uint64_t start = A.starts[u];
-    const bool weak = (A.stops[u] >> 63) != 0;
-    const uint64_t stop = A.stops[u] & ~(1ull << 63);
+    const uint32_t vm = A.vmode[u];
+    const bool weak = (A.stops[u] & FB_STOP_WEAK) != 0;
+    const bool soft = (A.stops[u] & FB_STOP_SOFT) != 0;
+    const uint64_t stop = A.stops[u] & FB_STOP_MASK;
     const uint64_t base = A.misalign * 8;
     const uint64_t end_bytes = A.misalign + A.n;
     const uint64_t nwords = (end_bytes + 3) / 4;
     const uint64_t nbits = 8 * A.n;
     const bool rfc = (A.flags & DMX_CFG_RFC_STRICT) != 0;
     const bool stream_start = u == 0 && !(A.flags & DMX_IFLAG_PIECE);
-    // ---- 1. block type, staging window ----
+    auto hdr3 = [&](uint64_t b) -> uint32_t {  // the 3 header bits at aligned-image bit b
+        const uint32_t w0 = A.in_words[b >> 5];
+        const uint32_t w1 = (b >> 5) + 1 < nwords ? A.in_words[(b >> 5) + 1] : 0u;
+        return __builtin_amdgcn_alignbit(w1, w0, (uint32_t)(b & 31)) & 7u;
+    };
+    // ---- 1. block type (the code in force), staging window ----
     if (t == 0) {
         uint32_t kind = 1;
         const uint64_t b = base + start;
-        const uint32_t w0 = A.in_words[b >> 5];
-        const uint32_t w1 = (b >> 5) + 1 < nwords ? A.in_words[(b >> 5) + 1] : 0u;
-        const uint32_t h = __builtin_amdgcn_alignbit(w1, w0, (uint32_t)(b & 31));
-        const uint32_t btype = (h >> 1) & 3;
-        // The block must end by he: first the stop (the next dynamic-header start), then -- if
-        // no end of block comes before it: a false header hit inside the block -- as far as the
-        // staging reaches.  Staged: as many words as fit.
-        const uint64_t ws = b >> 5;
+        uint32_t btype, bfinal;
+        uint64_t state;
+        if (vm == FB_V_HEADER) {
+            const uint32_t h = hdr3(b);
+            btype = (h >> 1) & 3;
+            bfinal = h & 1;
+            state = (btype == 1 ? FB_STATE_FIXED : start) | (bfinal ? FB_STATE_FINAL : 0ull);
+        } else {  // inside a block: the code of vhdr's block (a virtual unit's is a guess)
+            const uint64_t vh = A.vhdr[u];
+            const uint32_t h = (vh & FB_STATE_FIXED) ? 2u : hdr3(base + (vh & FB_STATE_POS));
+            btype = ((h >> 1) & 3) == 2 ? 2u : 1u;  // a stored or fixed first block: fixed blocks follow
+            bfinal = btype == 2 ? (h & 1) : ((vh & FB_STATE_FIXED) && (vh & FB_STATE_FINAL) ? 1u : 0u);
+            state = (btype == 1 ? FB_STATE_FIXED : (vh & FB_STATE_POS)) | (bfinal ? FB_STATE_FINAL : 0ull);
+        }
+        // The block run must end by he: first the stop (the next unit start), then -- if no end of
+        // block comes before a hard stop: a false header hit inside the block -- as far as the
+        // staging reaches.  Staged: as many words as fit (a virtual unit's from its warm-up on).
+        const uint64_t ws = (vm == FB_V_VIRTUAL ? b - FBP_WARM - 64 : b) >> 5;
         const uint64_t hecap = min(nbits, (ws + FBP_IN - 16) * 32 - base);
-        if (!weak && (btype == 1 || btype == 2) && start + 3 < hecap) {
+        if (!weak && (btype == 1 || btype == 2) && start + (vm == FB_V_HEADER ? 3 : 0) < hecap) {
             kind = 0;
             S.ws = ws;
             S.nst = (uint32_t)(min(ws + FBP_IN - 13, nwords) - ws);
             S.he = min(stop, hecap);
             S.hecap = hecap;
         }
+        if (vm == FB_V_VIRTUAL && kind != 0) kind = 3;  // no serial decode from a guessed start
         S.kind = kind;
+        S.err = SEGF_ERR_DATA;
         S.btype = btype;
-        S.bfinal = h & 1;
+        S.bfinal = bfinal;
+        S.vstate = state;
+        S.vs0 = 0;
+        S.midend = 0;
+        S.crossed = 0;
     }
     __syncthreads();
     if (S.kind == 0) {
@@ -715,14 +812,25 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
         __syncthreads();
         if (wave == 0) {
             uint64_t hp = base + start + 3;
-            const uint32_t err = fbp_header(S.T, S.btype, S.in, ws, nst, &hp, end_bytes * 8, rfc);
+            uint32_t err = 0;
+            if (vm == FB_V_HEADER) {
+                err = fbp_header(S.T, S.btype, S.in, ws, nst, &hp, end_bytes * 8, rfc);
+            } else {
+                if (S.btype == 1) {
+                    load_fixed(S.T);
+                } else {
+                    uint64_t hq = base + (S.vstate & FB_STATE_POS) + 3;
+                    err = fbp_header_g(S.T, A.in_words, nwords, end_bytes, &hq, rfc);
+                }
+                hp = base + start;  // the body starts at the unit's start bit
+            }
             if (lane_id() == 0) {
                 const uint64_t hs = hp - ws * 32;
                 if (err) {  // the serial decoder fails here too: the unit's record says so
                     S.kind = 3;
                     S.err = err;
                 } else if (base + S.hecap - ws * 32 <= hs) {
-                    S.kind = 1;
+                    S.kind = vm == FB_V_VIRTUAL ? 3u : 1u;
                     if (A.stats) atomicAdd(&A.stats[4], 1u);
                 } else if (base + S.he - ws * 32 <= hs) {
                     S.he = S.hecap;  // the stop lies inside the header
@@ -737,6 +845,17 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
         }
         __syncthreads();
     }
+    // a fixed-code block whose end of block is followed by a non-final fixed-block header runs on
+    // into it (the same code): a run of fixed blocks decodes as one block
+    const bool fixcont = S.btype == 1 && !S.bfinal;
+    auto tok = [&](const uint32_t* win, uint32_t* pa, uint32_t* a, uint32_t* d) -> uint32_t {
+        const uint32_t k = pj_token(win, pa, S.llut, S.dlut, S.T, a, d);
+        if (k == TK_EOB && fixcont && (lds_peek32(win, *pa) & 7u) == 2u) {  // BFINAL 0, BTYPE 01
+            *pa += 3;
+            return TK_NOP;
+        }
+        return k;
+    };
     for (int attempt = 0; attempt < 2 && S.kind == 0; attempt++) {
         const uint32_t* win = S.in;
         const uint32_t hs = S.hs, hlen = (uint32_t)(base + S.he - S.ws * 32 - hs);
@@ -750,27 +869,32 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
         __syncthreads();
         // ---- 2. warm-up, first pass ----
         uint32_t s0 = sp;
-        if (r > 0 && r < nl) {
-            uint32_t p = sp > FBP_WARM ? sp - FBP_WARM : 0u, pa = hs + p;
+        if ((r > 0 || vm == FB_V_VIRTUAL) && r < nl) {
+            // (a virtual unit's range 0 warms up before the unit's start bit, inside the staging)
+            int32_t p = (int32_t)sp - (int32_t)FBP_WARM;
+            if (vm != FB_V_VIRTUAL && p < 0) p = 0;
+            uint32_t pa = (uint32_t)((int32_t)hs + p);
             bool ok = true;
-            while (p < sp) {
+            while (p < (int32_t)sp) {
                 uint32_t a, d;
-                const uint32_t k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
+                const uint32_t k = tok(win, &pa, &a, &d);
                 if (k == TK_BAD || k == TK_EOB) { ok = false; break; }
-                p = pa - hs;
+                p = (int32_t)(pa - hs);
             }
-            if (ok && p < sp1) s0 = p;
+            if (ok && p < (int32_t)sp1) s0 = (uint32_t)p;
         }
+        if (r == 0) S.vs0 = s0;
         uint32_t e1, st1 = 0, w1 = 0, b1 = 0;
         {
             uint32_t p = s0, pa = hs + s0, pn = 0;
             while (p < sp1) {
                 atomicOr(&S.bmap[p >> 5], 1u << (p & 31));
                 uint32_t a, d;
-                const uint32_t k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
+                const uint32_t k = tok(win, &pa, &a, &d);
                 if (k == TK_BAD) { st1 = 2; break; }
                 p = pa - hs;
                 if (k == TK_EOB) { st1 = 1; break; }
+                if (k == TK_NOP) continue;
                 if (k == TK_LIT) {
                     if (pn == 3) { w1++; pn = 0; }
                     pn++;
@@ -812,7 +936,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
                         break;
                     }
                     uint32_t a, d;
-                    const uint32_t k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
+                    const uint32_t k = tok(win, &pa, &a, &d);
                     if (k == TK_BAD) { stn = 2; break; }
                     p = pa - hs;
                     if (k == TK_EOB) { stn = 1; break; }
@@ -824,13 +948,20 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
         }
         // ---- 4. the block's end; recount ranges that moved ----
         if (t == 0 && !settled) {
-            S.kind = 1;
+            S.kind = vm == FB_V_VIRTUAL ? 3u : 1u;
             if (A.stats) atomicAdd(&A.stats[5], 1u);
         } else if (t == 0 && te >= (uint32_t)FBP_NT) {
-            // no end of block before he: again up to the staging's end, else serially
-            S.kind = S.he < S.hecap ? 4u : 1u;
-            if (S.kind == 4) S.he = S.hecap;
-            if (A.stats) atomicAdd(&A.stats[6], 1u);
+            if (soft && S.he == stop) {
+                // the soft stop: the unit ends at the first token boundary at or past it, inside
+                // the block run (the next unit starts there)
+                S.midend = 1;
+                S.endbit = S.ws * 32 + hs + S.endp[nl - 1] - base;
+            } else {
+                // no end of block before he: again up to the staging's end, else serially
+                S.kind = S.he < S.hecap ? 4u : (vm == FB_V_VIRTUAL ? 3u : 1u);
+                if (S.kind == 4) S.he = S.hecap;
+                if (A.stats) atomicAdd(&A.stats[6], 1u);
+            }
         }
         if (r == te && settled) {
             // a code that decodes to nothing, or an end past the stream: the serial decoder
@@ -856,9 +987,10 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             w1 = b1 = 0;
             while (p < sp1) {
                 uint32_t a, d;
-                const uint32_t k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
+                const uint32_t k = tok(win, &pa, &a, &d);
                 p = pa - hs;
                 if (k == TK_BAD || k == TK_EOB) break;
+                if (k == TK_NOP) continue;
                 if (k == TK_LIT) {
                     if (pn == 3) { w1++; pn = 0; }
                     pn++;
@@ -899,7 +1031,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             S.words = tw;
             S.bytes = tb;
             if (tw > cap) {
-                S.kind = 1;
+                S.kind = vm == FB_V_VIRTUAL ? 3u : 1u;
                 if (A.stats) atomicAdd(&A.stats[8], 1u);
             }
         }
@@ -911,9 +1043,13 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             bool drop = false;
             while (p < sp1) {
                 uint32_t a, d;
-                const uint32_t k = pj_token(win, &pa, S.llut, S.dlut, S.T, &a, &d);
+                const uint32_t k = tok(win, &pa, &a, &d);
                 p = pa - hs;
                 if (k == TK_BAD || k == TK_EOB) break;
+                if (k == TK_NOP) {
+                    S.crossed = 1;
+                    continue;
+                }
                 if (k == TK_LIT) {
                     if (pn == 3) {
                         tk[nw++] = (3u << 24) | pend;
@@ -934,17 +1070,19 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             }
             if (pn) tk[nw++] = (pn << 24) | pend;
             if (drop) {
-                S.kind = 1;
+                S.kind = vm == FB_V_VIRTUAL ? 3u : 1u;
                 if (A.stats) atomicAdd(&A.stats[9], 1u);
             }
         }
         __syncthreads();
-        // the unit ends after this block unless the serial decoder would go on
-        if (t == 0 && S.kind == 0 && !S.bfinal) {
+        // the unit ends after this block unless the serial decoder would go on; a fixed block
+        // far from the stop ends it too (the host starts a lane-parallel unit at its header)
+        if (t == 0 && S.kind == 0 && !S.bfinal && !S.midend) {
             const uint64_t pos = S.endbit;
-            bool ends = pos >= stop;
+            bool ends = pos >= stop ||
+                        (((hdr3(base + pos) >> 1) & 3) == 1 && stop - pos > FB_SER_FIXED_MAX);
             if (!ends) {
-                uint64_t lo = u + 1, hi = A.nunits;  // first start >= pos
+                uint64_t lo = 0, hi = A.nunits;  // first listed start >= pos
                 while (lo < hi) {
                     const uint64_t mid = (lo + hi) >> 1;
                     if (A.starts[mid] < pos) lo = mid + 1;
@@ -959,19 +1097,27 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
     }
     const uint32_t kind = S.kind;
     if (A.stats && t == 0) atomicAdd(&A.stats[weak ? 3 : kind == 3 ? 0 : kind], 1u);
+    // a virtual unit starts at the token boundary its warm-up found
+    const uint64_t rstart = vm == FB_V_VIRTUAL && kind != 3 ? S.ws * 32 + S.hs + S.vs0 - base : start;
     if (kind == 0 || kind == 3) {
         if (t == 0) {
             FbUnit rec;
-            rec.start = start;
+            rec.start = rstart;
             rec.end = kind == 0 ? S.endbit : start;
             rec.size = kind == 0 ? S.bytes : 0;
             rec.ntok = kind == 0 ? S.words : 0;
-            rec.flags = kind == 3 ? S.err : S.bfinal ? SEGF_FINAL : 0u;
+            rec.hdr = kind == 0 && S.midend ? S.vstate : FB_AT_HEADER;
+            rec.flags = kind == 3 ? S.err : ((S.bfinal && !S.midend) ? SEGF_FINAL : 0u) | (S.crossed ? SEGF_CROSSED : 0u);
             A.units[u] = rec;
         }
     } else if (wave == 0) {
-        if (kind == 1) fb_serial(A, u, S.T, S.in, start, 0, 0, true);
+        const uint32_t crossed = S.crossed;
+        if (kind == 1) fb_serial(A, u, S.T, S.in, start, 0, 0, true, vm == FB_V_EXACT ? A.vhdr[u] : FB_AT_HEADER);
         else fb_serial(A, u, S.T, S.in, S.endbit, S.words, S.bytes, false);
+        if (lane_id() == 0) {
+            A.units[u].start = rstart;
+            if (kind == 2 && crossed) A.units[u].flags |= SEGF_CROSSED;
+        }
     }
 }
 
@@ -1470,14 +1616,16 @@ hipError_t launch_fb_compact(const uint32_t* counts, const uint64_t* offs, const
 }
 
 hipError_t launch_fb_decode(const uint32_t* in_words, uint64_t misalign, uint64_t n,
-                            const uint64_t* starts, const uint64_t* stops, uint64_t nunits,
+                            const uint64_t* starts, const uint64_t* stops, const uint8_t* vmode,
+                            const uint64_t* vhdr, uint64_t nunits, uint64_t u0, uint64_t count,
                             const uint64_t* tokoff, uint32_t* tok, FbUnit* units, uint32_t flags,
                             bool parallel, uint32_t* stats, hipStream_t st) {
-    const FbDecodeArgs A{in_words, misalign, n, starts, stops, nunits, tokoff, tok, units, flags, stats};
+    if (!count) return hipSuccess;
+    const FbDecodeArgs A{in_words, misalign, n, starts, stops, vmode, vhdr, nunits, u0, tokoff, tok, units, flags, stats};
     if (parallel)
-        hipLaunchKernelGGL(k_fb_pdecode, dim3((uint32_t)nunits), dim3(FBP_NT), 0, st, A);
+        hipLaunchKernelGGL(k_fb_pdecode, dim3((uint32_t)count), dim3(FBP_NT), 0, st, A);
     else
-        hipLaunchKernelGGL(k_fb_decode, dim3((uint32_t)nunits), dim3(64), 0, st, A);
+        hipLaunchKernelGGL(k_fb_decode, dim3((uint32_t)count), dim3(64), 0, st, A);
     return hipGetLastError();
 }
 

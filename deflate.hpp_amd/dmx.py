@@ -22,6 +22,7 @@ DMX_ERR_OVERREAD = -5
 DMX_ERR_CAPACITY = -6
 DMX_ERR_CHECKSUM = -8
 DMX_CFG_RFC_STRICT = 1
+DMX_CFG_FB_SERIAL = 2
 DMX_VERIFY = 1
 DMX_DEFLATE_NOT_FINAL = 1
 
@@ -35,7 +36,7 @@ EXPORTS = [
     "dmx_corpus_generate", "dmx_adler32_device", "dmx_crc32_device", "dmx_adler32", "dmx_crc32",
     "dmx_framed_bound", "dmx_deflate_zlib", "dmx_deflate_gzip", "dmx_inflate_zlib", "dmx_inflate_gzip",
     "dmx_deflate_file", "dmx_inflate_file", "dmx_segment_starts_device", "dmx_inflate_piece_device",
-    "dmx_segment_check_device",
+    "dmx_segment_check_device", "dmx_set_default_config", "dmx_deflate_device_async",
 ]
 
 
@@ -46,13 +47,15 @@ class DmxError(RuntimeError):
 
 
 class Config(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int), ("segment_bytes", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+    _fields_ = [("device", ctypes.c_int), ("segment_bytes", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("n_gpus", ctypes.c_uint32), ("dev_inflate_pass", ctypes.c_uint32),
+                ("dev_heavy_bytes", ctypes.c_uint32)]
 
 
 class Stats(ctypes.Structure):
     _fields_ = [("ms_main_kernel", ctypes.c_double), ("ms_device_total", ctypes.c_double),
                 ("segments", ctypes.c_uint64), ("in_bytes", ctypes.c_uint64),
-                ("out_bytes", ctypes.c_uint64), ("path", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("out_bytes", ctypes.c_uint64), ("path", ctypes.c_uint32), ("shards", ctypes.c_uint32)]
 
 
 _lib = None
@@ -87,6 +90,8 @@ def lib():
     L.dmx_strerror.argtypes = [ctypes.c_int]
     L.dmx_strerror.restype = ctypes.c_char_p
     L.dmx_deflate_device.argtypes = [vp, vp, sz, ctypes.c_int, ctypes.c_uint32, vp, sz, ctypes.POINTER(sz), vp]
+    L.dmx_deflate_device_async.argtypes = [vp, vp, sz, ctypes.c_int, ctypes.c_uint32, vp, sz, vp, vp]
+    L.dmx_set_default_config.argtypes = [ctypes.POINTER(Config)]
     L.dmx_inflate_device.argtypes = [vp, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
     L.dmx_set_timing.argtypes = [vp, ctypes.c_int]
     L.dmx_last_stats.argtypes = [vp, ctypes.POINTER(Stats)]
@@ -143,12 +148,21 @@ def corpus_into(kind, n, ptr, offset=0):
 class Context:
     """A libdmx context bound to one HIP device (dmx_create / dmx_destroy)."""
 
-    def __init__(self, device=-1, segment_bytes=32768, rfc_strict=False):
+    def __init__(self, device=-1, segment_bytes=32768, rfc_strict=False, n_gpus=1, **dev):
+        """dev: developer A/B controls -- inflate_pass=k forces pass k of the segmented inflate
+        plan, heavy_bytes=b sets the lane decoder's heavy-candidate threshold, fb_serial=True
+        makes the block-parallel path decode every unit with one wavefront."""
         cfg = Config()
         lib().dmx_config_default(ctypes.byref(cfg))
         cfg.device = device
         cfg.segment_bytes = segment_bytes
         cfg.flags = DMX_CFG_RFC_STRICT if rfc_strict else 0
+        cfg.n_gpus = n_gpus
+        if dev.get("fb_serial"):
+            cfg.flags |= DMX_CFG_FB_SERIAL
+        if dev.get("inflate_pass") is not None:
+            cfg.dev_inflate_pass = int(dev["inflate_pass"]) + 1
+        cfg.dev_heavy_bytes = int(dev.get("heavy_bytes") or 0)
         h = ctypes.c_void_p()
         _check(lib().dmx_create(ctypes.byref(h), ctypes.byref(cfg)), "dmx_create")
         self.h = h
@@ -296,6 +310,14 @@ class Context:
                                       ctypes.c_void_p(stream) if stream else None)
         _check(rc, "deflate_device")
         return out_len.value
+
+    def deflate_device_async(self, d_in, n, level, d_out, cap, d_len, stream=None, not_final=False):
+        """Enqueue a device deflate; the stream length lands in the 8-byte device buffer d_len."""
+        rc = lib().dmx_deflate_device_async(self.h, ctypes.c_void_p(d_in), n, level,
+                                            DMX_DEFLATE_NOT_FINAL if not_final else 0,
+                                            ctypes.c_void_p(d_out), cap, ctypes.c_void_p(d_len),
+                                            ctypes.c_void_p(stream) if stream else None)
+        _check(rc, "deflate_device_async")
 
     def inflate_device(self, d_in, n, d_out, cap, stream=None):
         out_len = ctypes.c_size_t()

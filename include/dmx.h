@@ -42,18 +42,40 @@ typedef struct dmx_config {
                                32768 mirrors the reference's per-chunk LZ77 reset
                                (deflate.hpp:689-697).                                          */
     uint32_t flags;         /* DMX_CFG_*                                                        */
+    uint32_t n_gpus;        /* 0 or 1: one device.  N > 1: the host-buffer API (dmx_deflate,
+                               dmx_inflate, dmx_inflate_alloc, hence deflate::compress and
+                               inflate::decompress) splits each large call over N devices,
+                               `device`, device + 1, ... (mod the visible count: fewer GPUs than N
+                               run several shards each).  Deflate: contiguous segment-aligned
+                               shards, NOT_FINAL except the last -- segments are independent
+                               (deflate.hpp:689-697), so the bytes equal the one-device stream.
+                               Inflate: cuts at segment starts proven by a piece-mode decode
+                               (dmx_segment_check_device), one piece per device, the outputs
+                               concatenated; a stream that does not split decodes on one.      */
+    /* developer controls for A/B runs; dmx_config_default sets both to 0 = the product plan */
+    uint32_t dev_inflate_pass; /* k + 1 forces inflate pass k of the segmented plan
+                                  (0 wave, 1 workgroup, 2 look-back, 4 lanes, 5 block-parallel) */
+    uint32_t dev_heavy_bytes;  /* lane decoder: candidates spanning more compressed bytes go to
+                                  the workgroup decoder; 0 = the built-in 2048 and CU rule      */
 } dmx_config;
 
 /* Inflate code-length RLE per RFC 1951 (repeat may span HLIT/HDIST, code 16 repeats the
  * previous length) instead of the reference's behaviour (SURVEY A-11/A-12, inflate.hpp:166-224).
  * Default off: output is bit-exact to the reference. */
 #define DMX_CFG_RFC_STRICT 1u
+/* Developer A/B: the block-parallel path decodes every unit with one wavefront. */
+#define DMX_CFG_FB_SERIAL 2u
 
 void dmx_config_default(dmx_config* cfg);
 int dmx_create(dmx_ctx** ctx, const dmx_config* cfg);
 void dmx_destroy(dmx_ctx* ctx);
-/* process-wide context on the current device with the default config (never destroyed) */
+/* process-wide context (never destroyed), created on first use with the config set by
+ * dmx_set_default_config, else the default config on the current device.  This is the context
+ * include/deflate.hpp and include/inflate.hpp use: a caller of the reference's class API turns
+ * on the whole node with one call, e.g. cfg.n_gpus = 8, before its first compress. */
 dmx_ctx* dmx_default_ctx(void);
+/* DMX_ERR_ARG once the default context exists (the config is read at its creation). */
+int dmx_set_default_config(const dmx_config* cfg);
 
 /* ---- host-buffer API (what include/deflate.hpp / inflate.hpp call) ---------------------- */
 
@@ -110,6 +132,15 @@ const char* dmx_strerror(int code);
  * the context's own stream.  Returns DMX_ERR_CAPACITY if cap < the produced size. */
 int dmx_deflate_device(dmx_ctx* ctx, const void* d_in, size_t n, int level, uint32_t flags,
                        void* d_out, size_t cap, size_t* out_len, void* stream);
+
+/* The same without a host synchronisation: every step is enqueued on `stream` and the stream
+ * length lands in *d_out_len (8 bytes of DEVICE memory) when the work completes; the call
+ * returns once it is enqueued (graph-capturable, and a multi-GPU caller can keep every device
+ * busy from one thread).  A length above cap means the output did not fit: only the segments
+ * that fit were written.  Calls on one context are ordered even across streams (the context's
+ * scratch is reused). */
+int dmx_deflate_device_async(dmx_ctx* ctx, const void* d_in, size_t n, int level, uint32_t flags,
+                             void* d_out, size_t cap, uint64_t* d_out_len, void* stream);
 
 /* Device-resident inflate.  Returns DMX_ERR_CAPACITY (and the needed size in *out_len) when
  * the decoded stream does not fit in cap. */
@@ -190,7 +221,8 @@ typedef struct dmx_stats {
                                    markers (zlib's, libdeflate's, the reference's own):
                                    header scan, one wavefront per unit of blocks, window
                                    hand-off                                                  */
-    uint32_t reserved;
+    uint32_t shards;        /* host-buffer API with n_gpus > 1: the pieces the call was split
+                               into (0 or 1: one device)                                       */
 } dmx_stats;
 
 /* Enable (1) / disable (0) per-call HIP-event timing on a context (off by default). */

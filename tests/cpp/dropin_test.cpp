@@ -8,6 +8,7 @@
 #include <inflate.hpp>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iterator>
@@ -33,6 +34,24 @@ static std::vector<uint8_t> slurp(const std::string& p) {
 int main(int argc, char** argv) {
     const std::string dir = argc > 1 ? argv[1] : "tests/golden";
     const std::string tmp = argc > 2 ? argv[2] : "/tmp";
+    // argv[3] = N: the whole program runs with dmx_config.n_gpus = N behind the reference's API
+    const int ngpus = argc > 3 ? std::atoi(argv[3]) : 1;
+    if (ngpus > 1) {
+        dmx_config cfg;
+        dmx_config_default(&cfg);
+        cfg.n_gpus = (uint32_t)ngpus;
+        CHECK(dmx_set_default_config(&cfg) == DMX_OK, "dmx_set_default_config before first use");
+        std::vector<uint8_t> big(6u << 20);
+        for (size_t i = 0; i < big.size(); i++) big[i] = (uint8_t)((i * 2654435761u) >> 13) & 0x3F;
+        std::vector<uint8_t> z = deflate::compress(big, 2);
+        dmx_stats st{};
+        dmx_last_stats(dmx_default_ctx(), &st);
+        CHECK((int)st.shards == ngpus, "deflate::compress split over n_gpus shards");
+        CHECK(inflate::decompress(z) == big, "n_gpus round trip through the reference API");
+        dmx_last_stats(dmx_default_ctx(), &st);
+        CHECK((int)st.shards == ngpus, "inflate::decompress split over n_gpus pieces");
+        CHECK(dmx_set_default_config(&cfg) == DMX_ERR_ARG, "the default config is fixed once in use");
+    }
     std::vector<uint8_t> bmp = slurp(dir + "/test.bmp");
     CHECK(bmp.size() == 21898, "test.bmp fixture present");
     for (int level = 0; level <= 3; level++) {

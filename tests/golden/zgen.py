@@ -19,12 +19,20 @@ def zgen_stream(spec):
 
 
 def stream_of(v, gold_dir):
-    """The stream bytes of manifest vector v (a committed file, or regenerated and SHA-checked)."""
+    """The stream bytes of manifest vector v: a committed file when it has one, else regenerated
+    and SHA-checked.  A zlib that makes other bytes (zlib-ng, another release) skips the vector
+    under pytest, naming the version; the committed vectors still run."""
     import os
-    if "zgen" in v:
+    if "zgen" in v and "stream" not in v:
         s = zgen_stream(v["zgen"])
         if hashlib.sha256(s).hexdigest() != v["stream_sha256"]:
-            raise RuntimeError(f"{v['name']}: zlib {zlib.ZLIB_RUNTIME_VERSION} produced another stream")
+            msg = (f"{v['name']}: zlib {zlib.ZLIB_RUNTIME_VERSION} produced another stream than the "
+                   "1.2.11 one the reference's output was recorded on")
+            try:
+                import pytest
+            except ImportError:
+                raise RuntimeError(msg)
+            pytest.skip(msg)
         return s
     with open(os.path.join(gold_dir, v["stream"]), "rb") as f:
         return f.read()

@@ -1,0 +1,124 @@
+"""Block-parallel inflate (path 5) of third-party streams the header scan cannot split (VERDICT
+r3 item 2): runs of fixed-code blocks (zlib Z_FIXED, the reference's own level-1 output), one
+huge block, and zlib-1 zeros.  Each is checked bit-exact against the oracle (the CPU restatement
+of the reference inflate, inflate.hpp:277-322) and timed against the reference's own inflate on
+one core of the same host; the decode must take path 5 (virtual units), not the serial decoder.
+"""
+import time
+import zlib
+
+import pytest
+
+import dmx
+import streams
+from oracle_bind import Reference
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_inflate(ctx, s, n):
+    import torch
+    d_in = torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda()
+    d_o = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    ctx.set_timing(True)
+    best = 1e30
+    for _ in range(3):
+        olen = ctx.inflate_device(d_in.data_ptr(), len(s), d_o.data_ptr(), n + 64)
+        best = min(best, ctx.stats().ms_device_total)
+    path = ctx.stats().path
+    ctx.set_timing(False)
+    return d_o[:olen].cpu().numpy().tobytes(), path, best
+
+
+def _ref_ms(s):
+    """The reference's inflate::decompress of the stream on one host core (compiled from its
+    headers, oracle/_ref), best of 2; None without the reference build."""
+    if not Reference.available():
+        return None
+    r = Reference()
+    best = 1e30
+    for _ in range(2):
+        t = time.perf_counter()
+        r.decompress(s)
+        best = min(best, (time.perf_counter() - t) * 1e3)
+    return best
+
+
+CASES = {
+    "zfixed_text_64MiB": lambda: (dmx.corpus("text", 64 << 20), None),
+    "zlib1_zeros_256MiB": lambda: (dmx.corpus("zeros", 256 << 20), None),
+    "single_block_16MiB": lambda: (dmx.corpus("mixed", 16 << 20), None),
+    "zfixed_mixed_32MiB": lambda: (dmx.corpus("mixed", 32 << 20), None),
+}
+
+
+def _stream(name, data):
+    if name.startswith("zfixed"):
+        return streams.zfixed(data)
+    if name.startswith("zlib1"):
+        return streams.zlib_raw(data, 1)
+    return streams.single_fixed_block(data)
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_path5_streams_without_unit_starts(ctx, oracle, name):
+    data, _ = CASES[name]()
+    s = _stream(name, data)
+    out, path, ms = _gpu_inflate(ctx, s, len(data))
+    assert out == data
+    assert path == 5, f"{name}: path {path}"
+    assert oracle.inflate(s) == data
+    ref = _ref_ms(s)
+    print(f"{name}: stream {len(s)} B, GPU {ms:.3f} ms ({len(data) / ms / 1e6:.2f} GB/s), "
+          f"reference 1 core {ref if ref is None else round(ref, 1)} ms")
+    if ref is not None:
+        assert ms < ref, (name, ms, ref)
+
+
+def test_path5_reference_fixed_block_stream(ctx, oracle):
+    """The reference's own level-2 output of periodic data is a fixed-code block per 32 KiB
+    chunk with no marker and no dynamic header (SURVEY A-4: 2,049 fixed blocks on the repeat
+    corpus); it is lossy (A-1), so the expected bytes are the oracle's -- the reference inflate's
+    -- not the input."""
+    if not Reference.available():
+        pytest.skip("reference build (oracle/_ref) not present")
+    data = dmx.corpus("repeat", 8 << 20)
+    s = Reference().compress(data, 2)
+    want = oracle.inflate(s)
+    out, path, ms = _gpu_inflate(ctx, s, len(want))
+    assert out == want
+    assert path == 5
+
+
+def _unmark(sync_flushed, filler):
+    """A sync-flushed stream ends in the empty stored block 000|pad|00 00 FF FF; give that block
+    a payload instead (LEN = len(filler)), so the junction carries no 00 00 FF FF marker and
+    its stored header (not byte-aligned, after a Huffman block) is no scanned start."""
+    assert sync_flushed.endswith(b"\x00\x00\xff\xff")
+    n = len(filler)
+    return sync_flushed[:-4] + n.to_bytes(2, "little") + (n ^ 0xFFFF).to_bytes(2, "little") + filler
+
+
+@pytest.mark.parametrize("final_fixed", [False, True])
+def test_path5_dynamic_then_fixed_run(ctx, oracle, final_fixed):
+    """Dynamic blocks, a small stored block, then a long run of fixed-code blocks (zlib Z_FIXED)
+    and (optionally) a huge final fixed block: the dynamic unit ends at the first far fixed
+    header and repair units decode the run lane-parallel."""
+    a = dmx.corpus("text", 3 << 20)
+    b = dmx.corpus("mixed", 6 << 20, offset=5 << 20)
+    c = dmx.corpus("bmp", 4 << 20)
+    f1, f2 = b"gap-1", b"gap-2!"
+    z = zlib.compressobj(6, zlib.DEFLATED, -15)
+    s1 = _unmark(z.compress(a) + z.flush(zlib.Z_SYNC_FLUSH), f1)
+    zf = zlib.compressobj(6, zlib.DEFLATED, -15, 8, zlib.Z_FIXED)
+    if final_fixed:
+        s2 = _unmark(zf.compress(b) + zf.flush(zlib.Z_SYNC_FLUSH), f2) + streams.single_fixed_block(c)
+        want = a + f1 + b + f2 + c
+    else:
+        s2 = zf.compress(b) + zf.flush()
+        want = a + f1 + b
+    s = s1 + s2
+    assert b"\x00\x00\xff\xff" not in s[len(s1) - 16: len(s1) + 16]
+    out, path, ms = _gpu_inflate(ctx, s, len(want))
+    assert out == want == oracle.inflate(s)
+    assert path == 5

@@ -1,0 +1,59 @@
+"""Single-process multi-GPU through the C-ABI (dmx_config.n_gpus) and the
+non-blocking device deflate.  On a one-GPU box the shards are virtual: every sub-context lives on
+device 0, which exercises the split, the per-shard streams and the reassembly exactly as on a
+node (the reference's chunks are independent, deflate.hpp:689-697)."""
+import pytest
+
+import dmx
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("g", [2, 3, 8])
+def test_n_gpus_host_api_matches_one_device(ctx, oracle, g):
+    data = dmx.corpus("mixed", 9 << 20, offset=12345)
+    one = ctx.compress(data, 2)
+    multi = dmx.Context(n_gpus=g)
+    try:
+        s = multi.compress(data, 2)
+        assert s == one  # shards NOT_FINAL + the last final: the one-device bytes
+        assert multi.stats().shards == g
+        assert multi.decompress(s) == data
+        assert multi.stats().shards == g  # the stream was split at proven segment starts
+        assert multi.decompress(s, cap=1000) == data[:1000]
+        assert oracle.inflate(s) == data
+        # a stream without markers (zlib's) does not split: one device decodes it
+        import zlib
+        z = zlib.compressobj(6, zlib.DEFLATED, -15)
+        zs = z.compress(data) + z.flush()
+        assert multi.decompress(zs) == data
+        # small inputs stay on one device
+        assert multi.compress(data[:1000], 2) == ctx.compress(data[:1000], 2)
+    finally:
+        multi.close()
+
+
+def test_deflate_device_async_leaves_length_on_device(ctx):
+    import torch
+    data = dmx.corpus("text", 5 << 20)
+    d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    cap = dmx.deflate_bound(len(data)) + 64
+    a = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    b = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(2, dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    ctx.deflate_device_async(d_in.data_ptr(), len(data), 2, a.data_ptr(), cap, d_len.data_ptr(), stream=st)
+    ctx.deflate_device_async(d_in.data_ptr(), len(data), 3, b.data_ptr(), cap, d_len.data_ptr() + 8, stream=st,
+                             not_final=True)
+    torch.cuda.synchronize()
+    la, lb = (int(x) for x in d_len.tolist())
+    n2 = ctx.deflate_device(d_in.data_ptr(), len(data), 2, b.data_ptr(), cap)
+    assert la == n2
+    ref = b[:n2].clone()
+    assert torch.equal(a[:la], ref)
+    assert ctx.decompress(a[:la].cpu().numpy().tobytes()) == data
+    assert lb > 0
+    # too small: the length says so, the call itself does not fail
+    ctx.deflate_device_async(d_in.data_ptr(), len(data), 2, a.data_ptr(), 1000, d_len.data_ptr(), stream=st)
+    torch.cuda.synchronize()
+    assert int(d_len[0]) == la > 1000

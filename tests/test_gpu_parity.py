@@ -357,11 +357,14 @@ def test_device_roundtrip_1GiB_repeat_checksum(ctx):
     assert olen == n and torch.equal(d_o[:n], d_in)
 
 
-def test_dropin_cpp_program():
+@pytest.mark.parametrize("ngpus", [1, 3])
+def test_dropin_cpp_program(ngpus):
+    """The C++ caller of the reference's class API; with 3, the default context is configured
+    with dmx_config.n_gpus = 3 (dmx_set_default_config) before its first call."""
     exe = os.path.join(ROOT, "tests", "cpp", "dropin_test")
     if not os.path.exists(exe):
         subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "cpp")], check=True)
-    r = subprocess.run([exe, GOLD, "/tmp"], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([exe, GOLD, "/tmp", str(ngpus)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
 
 

@@ -1,0 +1,13 @@
+# One GPU call for a development round: the GPU suite (path-5 foreign streams first), kernel
+# stats + DMX_PHASES timelines, the foreign-stream probe with the reference's 1-core times.
+# Everything lands under gpurun_out/.  usage: bash tools/gpu_round.sh [quick]
+set -e
+mkdir -p gpurun_out && cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest tests/test_gpu_foreign.py -x -v -s --timeout 300 --timeout-method thread > gpurun_out/p5v.log 2>&1 || { tail -60 gpurun_out/p5v.log; exit 1; }
+grep -E "GPU |passed|failed" gpurun_out/p5v.log | tail -12
+if [ "$1" != quick ]; then
+  timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+  tail -2 gpurun_out/gpu_tests.log
+fi
+SPECS=${SPECS:-"repeat:2 text:2 random:2"} PH_KINDS=${PH_KINDS:-repeat,text} bash tools/gpu_kstats.sh > gpurun_out/kstats.log 2>&1 || { tail -30 gpurun_out/kstats.log; exit 1; }
+grep -E "^(repeat|text|random|mixed|zeros|bmp) |k_deflate|k_inflate|^deflate|^# " gpurun_out/kstats.log | cut -c1-400

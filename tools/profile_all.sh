@@ -18,7 +18,7 @@ if [ "$mode" = collect ]; then
     c=${spec%%:*}; l=${spec#*:}
     [ -d $P/s_$c$l ] || continue
     cp $(find $P/s_$c$l -name "*kernel_stats.csv" | head -1) profiles/${tag}_kstats_${c}_L$l.csv
-    for k in k_deflate_segments k_inflate_lanes k_inflate_resolve k_inflate_pj_list; do
+    for k in k_deflate_segments k_deflate_emit k_inflate_lanes k_inflate_resolve k_inflate_pj_list; do
       python3 tools/traffic.py $P/f_$c$l $P/w_$c$l $c:$N:$l:$k $k profiles/traffic.json || true
     done
   done
