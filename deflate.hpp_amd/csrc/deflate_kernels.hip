@@ -80,7 +80,7 @@ constexpr bool DF_L3_LINK_ROUNDS = DMX_L3_LINK_ROUNDS != 0;
 // level 3's chain search: 1 = the tail test as one unaligned 4-byte LDS read, 2 = also the match
 // lengths by unaligned 8-byte reads, 3 = those but the first link's length by aligned words
 // (0 = aligned words and alignbyte throughout)
-constexpr int DF_L3_U = DMX_L3_U;
+[[maybe_unused]] constexpr int DF_L3_U = DMX_L3_U;
 #ifndef DMX_L3_RP
 #define DMX_L3_RP 512
 #endif
@@ -92,6 +92,14 @@ constexpr uint32_t DF_L3_RP = DMX_L3_RP;
 #define DMX_DF_SKIP 1
 #endif
 constexpr bool DF_SKIP = DMX_DF_SKIP != 0;
+// level 3: the chain search feeds lanes from per-wave position lists (balanced chains)
+#ifndef DMX_L3_QUEUE
+#define DMX_L3_QUEUE 0
+#endif
+// level 2-3: the parse walk reads match lengths computed for every position beforehand
+#ifndef DMX_DF_PRELEN
+#define DMX_DF_PRELEN 0
+#endif
 // token-word count of a segment without any match (k_deflate_emit then reads its input's bytes)
 constexpr uint32_t EM_ALL_LITERALS = 0xFFFFFFFFu;
 
@@ -511,6 +519,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
     staged = false;
 
     if (level != 0) {
+        [[maybe_unused]] uint32_t skipm = 0;  // level 2: bit r = round r (2 * DF_NT positions) taken by the run continuation
         // ---- match candidates: rounds of 2*DF_NT positions, two per thread ---------------
         if (level >= 2) {
             // Table entries carry a fingerprint of the 4-byte key (product bits below the hash
@@ -626,6 +635,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                                                       ((FULL || p1 + 4 <= nb ? skip_d : 0u) << 16);
                                 cur = RoundState{NOH, NOH, p0, 0, 0, false, false};
                                 skipped = true;
+                                skipm |= 1u << rr;
                                 return;
                             }
                             skip_d = 0;
@@ -719,6 +729,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                                 cur = RoundState{NOH, NOH, p0, 0, 0, false, false};
                                 backoff = 1;
                                 skipped = true;
+                                skipm |= 1u << rr;
                                 return;
                             }
                             skip_d = 0;
@@ -777,6 +788,91 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
             }
             DMX_PHASE(A.dbg, seg, 14);
         }
+#if DMX_L3_QUEUE
+        if (level == 3) {
+            // ---- level 3: deeper search along the candidate chains, lanes fed from a queue ------
+            // Same search and same results as the lockstep form below (#else), but a lane whose
+            // chain ends takes the next position of its wave's list at once, so a wave costs its
+            // total hops / 64 instead of 64 x its longest chain per position group (text: 6.1
+            // hops per position on average, 2.45x that in lockstep; a third of the positions
+            // have no candidate at all).  The results cannot go to cand[] while chains still read
+            // it, so the segment goes in quarters, last first: a quarter's chains read links in
+            // the quarter and before it (links point backwards), all still the rounds' own;
+            // its results collect in the dead hash table and replace the quarter's entries after
+            // a barrier.  The hash table holds a quarter's results (Q u16) and each wave's list of
+            // its Q / 16 positions that have a candidate (Q u16).
+            constexpr uint32_t Q = SEG / 4, QW = Q / (DF_NT / 64);  // positions per quarter, per wave
+            static_assert(sizeof(S.U) >= 4 * Q, "results + lists live in the hash table");
+            uint16_t* const res = reinterpret_cast<uint16_t*>(S.U);
+            uint16_t* const lst = res + Q;
+            const uint32_t lane = (uint32_t)lane_id(), wv = (uint32_t)t >> 6;
+            const uint64_t below = (1ull << lane) - 1ull;
+            for (int qi = 3; qi >= 0; qi--) {
+                const uint32_t qb = (uint32_t)qi * Q, wb = qb + wv * QW;
+                uint16_t* const wl = lst + wv * QW;
+                // the wave's positions with a candidate, in order (ballot compaction)
+                uint32_t cnt = 0;
+                for (uint32_t g = 0; g < QW; g += 64) {
+                    const uint32_t pp = wb + g + lane;
+                    const bool has = pp < nb && S.cand[pp] != 0;
+                    const uint64_t m = __ballot(has);
+                    if (has) wl[cnt + (uint32_t)__popcll(m & below)] = (uint16_t)pp;
+                    res[pp - qb] = 0;
+                    cnt += (uint32_t)__popcll(m);
+                }
+                wave_sync();
+                // lane state: position p, link position q, best length / distance, tail word
+                uint32_t cur = 0, p = 0, q = 0, bl = 2, bd = 0, tail = 0, hop = 0, maxl = 0;
+                bool act = false;
+                auto take = [&](bool need) {  // lanes with need take the next list entries
+                    const uint64_t m = __ballot(need);
+                    if (need) {
+                        const uint32_t i = cur + (uint32_t)__popcll(m & below);
+                        act = i < cnt;
+                        if (act) {
+                            p = wl[i];
+                            q = p;
+                            bl = 2, bd = 0, tail = 0, hop = 0;
+                            maxl = min(258u, min(p / DF_CHUNK * DF_CHUNK + DF_CHUNK, nb) - p);
+                        }
+                    }
+                    cur += (uint32_t)__popcll(m);
+                };
+                take(true);
+                while (__ballot(act)) {
+                    if (act) {
+                        // one link: the first (q = p) is measured in full, later ones only when
+                        // the 4 bytes ending at the best length match (zlib's scan_end test)
+                        const uint32_t dq = S.cand[q];
+                        bool done = dq == 0;
+                        if (!done) {
+                            q -= dq;
+                            if (bl < 3 || lds_rd32u(S.data32, q + bl - 3) == tail) {
+                                const uint32_t L = matchlen_u(S.data32, p, q, maxl);
+                                if (L > bl) {
+                                    bl = L;
+                                    bd = p - q;
+                                    tail = lds_rd32u(S.data32, p + bl - 3);
+                                }
+                            }
+                            hop++;
+                            done = hop >= (uint32_t)DF_L3_DEPTH || bl >= maxl || bl >= DF_L3_LONG;
+                        }
+                        if (done) {
+                            res[p - qb] = (uint16_t)bd;
+                            act = false;
+                        }
+                    }
+                    // (all lanes: the ballot in take is wave-wide)
+                    take(!act && cur < cnt);
+                }
+                __syncthreads();
+                for (uint32_t i = t; i < Q; i += DF_NT)
+                    if (qb + i < nb) S.cand[qb + i] = res[i];
+                __syncthreads();
+            }
+        }
+#else
         if (level == 3) {
             // ---- level 3: deeper search along the candidate chains ----------------------------
             // cand[q] links q to an earlier occurrence of its 4-byte key, so p -> p - cand[p] ->
@@ -842,7 +938,8 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
             }
             __syncthreads();
         }
-        if (level >= 2) {
+#endif
+        if (level >= 2 && !DMX_DF_PRELEN) {
             // match bitmap from the candidates: bit p = "a candidate starts at p"
             for (uint32_t w = t; w < NMAP; w += DF_NT) {
                 const uint4* c4 = reinterpret_cast<const uint4*>(S.cand + 32 * w);
@@ -862,6 +959,49 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
             }
             __syncthreads();
         }
+#if DMX_DF_PRELEN
+        // ---- short match lengths for the parse walk, every position at once (plen: one byte
+        //      per position in the hash table, dead after the rounds): the first 16 bytes at the
+        //      candidate distance, neighbouring lanes on neighbouring positions.  Exact below 16
+        //      or at the parse chunk's end, else 255 = "measure it" (the walk's matchlen4).  On
+        //      text 99.5 % of the walk's matches are shorter than 16, so the walk reads one byte
+        //      per match instead of the candidate and then two data windows.  Rounds the run
+        //      continuation took (skipm) are left to matchlen4: their matches are long.  The
+        //      same pass builds the match bitmap. -----
+        uint8_t* const plen = reinterpret_cast<uint8_t*>(S.U);
+        static_assert(sizeof(S.U) >= SEG, "plen lives in the hash table");
+        if (level >= 2) {
+#pragma unroll 2
+            for (uint32_t k = 0; k < SEG / DF_NT; k++) {
+                const uint32_t p = (uint32_t)t + DF_NT * k;
+                const uint32_t c = p < nb ? S.cand[p] : 0u;
+                // the match bitmap (bit p = "a candidate starts at p"): a wave's 64 positions
+                // are two bitmap words
+                const uint64_t mb = __ballot(c != 0u);
+                if ((t & 31) == 0) S.mmap[p >> 5] = (uint32_t)(mb >> (t & 32));
+                if ((skipm >> (k >> 1)) & 1u) continue;  // (p >> 11 == k >> 1: uniform)
+                if (c) {
+                    const uint32_t q = p - c, ip = p >> 2, sp = p & 3, iq = q >> 2, sq = q & 3;
+                    uint32_t wa[5], wb[5];
+#pragma unroll
+                    for (int j = 0; j < 5; j++) {
+                        wa[j] = S.data32[ip + j];
+                        wb[j] = S.data32[iq + j];
+                    }
+                    uint32_t m = 16;
+#pragma unroll
+                    for (int j = 3; j >= 0; j--) {
+                        const uint32_t d = __builtin_amdgcn_alignbyte(wa[j + 1], wa[j], sp) ^
+                                           __builtin_amdgcn_alignbyte(wb[j + 1], wb[j], sq);
+                        m = d ? 4 * j + ((uint32_t)__builtin_ctz(d) >> 3) : m;
+                    }
+                    const uint32_t hi = min(p / DF_CHUNK * DF_CHUNK + DF_CHUNK, nb);
+                    plen[p] = (uint8_t)(m < 16 || p + 16 >= hi ? min(m, hi - p) : 255u);
+                }
+            }
+            __syncthreads();
+        }
+#endif
         DMX_PHASE(A.dbg, seg, 2);
 
         // ---- parse walk: one DF_CHUNK-byte chunk per quad of lanes (the four walk in step and
@@ -877,6 +1017,12 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                 return (e >= 32 ? 0xFFFFFFFFu : ((1u << e) - 1u)) & (0xFFFFFFFFu << (a & 31));
             };
             auto full_len = [&](uint32_t q) -> uint32_t {  // < 3 only on a fingerprint collision
+#if DMX_DF_PRELEN
+                if (!((skipm >> (q >> 11)) & 1u)) {
+                    const uint32_t v = plen[q];
+                    if (v != 255u) return v;
+                }
+#endif
                 return matchlen4(S.data32, q, q - S.cand[q], min(258u, hi - q), sub);
             };
             uint32_t p = lo, w = lo >> 5, mw = S.mmap[w], tok = 0, lastp = lo;  // lastp: last token

@@ -324,6 +324,10 @@ struct TokSink {
     bool stream_start;
     uint32_t err;
 
+    // fewer than two groups of room left: the unit stops at this token boundary (a soft end);
+    // the chain walk resumes the block from there in a repair unit, so running out of token
+    // space costs a repair, not the stream's trip to the serial decoder
+    __device__ bool full() const { return n + k + 128 > cap; }
     __device__ bool flush_group() {
         if (n + 64 > cap) {
             err |= SEGF_OVERFLOW;
@@ -579,7 +583,7 @@ __device__ __attribute__((noinline)) void fb_serial(const FbDecodeArgs& A, uint6
     for (bool f = first; !err && !fin && !midend; f = false) {
         if (!f) {
             const uint64_t pos = br.abspos() - base;
-            if (pos >= stop) break;
+            if (pos >= stop || sk.full()) break;
             while (jn < A.nunits && A.starts[jn] < pos) jn++;
             if (jn < A.nunits && A.starts[jn] == pos) break;
         }

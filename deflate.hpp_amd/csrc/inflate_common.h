@@ -693,11 +693,11 @@ __device__ __forceinline__ void lz_copy_lds(uint8_t* win, uint32_t pos, uint32_t
 // decompressHuffmanBlock (inflate.hpp:226-275) with 32-bit table entries: one 32-bit window
 // per half token (code + extra bits), no per-symbol base / extra arithmetic.
 // soft: stop (SEGF_SOFT) at the first token boundary at or past this reader position (path 5's
-// units that end inside a block; ~0 = never)
+// units that end inside a block; ~0 = never), or where the sink is full()
 template <class BR, class Sink>
 __device__ uint32_t decode_huffman(BR& br, const Tables& T, Sink& sk, uint64_t soft = ~0ull) {
     for (;;) {
-        if (br.abspos() >= soft) return SEGF_SOFT;
+        if (br.abspos() >= soft || sk.full()) return SEGF_SOFT;
         uint32_t v = br.window32();
         uint32_t e = T.llut[v & ((1u << LUT_L) - 1)];
         if (!e) {

@@ -33,6 +33,7 @@ struct SegSink {
     uint32_t pos;
     bool stream_start;
     uint32_t err;
+    __device__ bool full() const { return false; }
     __device__ bool literal(uint32_t b) {
         if (pos >= SEG_CAP) { err |= SEGF_OVERFLOW; return false; }
         if (lane_id() == 0) win[pos] = (uint8_t)b;
@@ -69,6 +70,7 @@ struct RingSink {
     bool count_only;
     uint32_t err;
     bool piece;  // a reference before the first byte is an error (DMX_IFLAG_PIECE)
+    __device__ bool full() const { return false; }
     __device__ bool literal(uint32_t b) {
         if (!count_only) {
             if (lane_id() == 0) {

@@ -51,7 +51,11 @@ typedef struct dmx_config {
                                (deflate.hpp:689-697), so the bytes equal the one-device stream.
                                Inflate: cuts at segment starts proven by a piece-mode decode
                                (dmx_segment_check_device), one piece per device, the outputs
-                               concatenated; a stream that does not split decodes on one.      */
+                               concatenated; a stream that does not split decodes on one.
+                               The split assumes the stream's first BFINAL block lies in its
+                               last piece (every stream libdmx, zlib or the reference writes);
+                               bytes after an early BFINAL that still decode as marker-delimited
+                               segments would be inflated too, where one device stops.          */
     /* developer controls for A/B runs; dmx_config_default sets both to 0 = the product plan */
     uint32_t dev_inflate_pass; /* k + 1 forces inflate pass k of the segmented plan
                                   (0 wave, 1 workgroup, 2 look-back, 4 lanes, 5 block-parallel) */

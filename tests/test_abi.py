@@ -54,3 +54,28 @@ def test_dropin_program_links():
     if not os.path.exists(exe):
         subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "cpp")], check=True)
     assert os.path.exists(exe)
+
+
+@pytest.mark.parametrize("cname,pyname", [("dmx_config", "Config"), ("dmx_stats", "Stats")])
+def test_struct_layout_matches_header(tmp_path, cname, pyname):
+    """The ctypes mirrors in dmx.py have the C header's field offsets and size (a field added
+    to one side only would shift every later field)."""
+    import ctypes
+    py = getattr(dmx, pyname)
+    fields = [f[0] for f in py._fields_]
+    src = tmp_path / "layout.c"
+    body = "".join(f'printf("{f} %zu\\n", offsetof({cname}, {f}));' for f in fields)
+    src.write_text("#include <stddef.h>\n#include <stdio.h>\n#include <dmx.h>\n"
+                   f'int main(void){{{body} printf("sizeof %zu\\n", sizeof({cname})); return 0;}}\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", f"-I{ROOT}/include", str(src), "-o", str(exe)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                        text=True).stdout.splitlines())
+    for f in fields:
+        assert int(got[f]) == getattr(py, f).offset, f
+    assert int(got["sizeof"]) == ctypes.sizeof(py)
+    hdr = open(os.path.join(ROOT, "include", "dmx.h")).read()
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), hdr, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    cfields = re.findall(r"\b([a-z_][a-z0-9_]*)\s*;", body)
+    assert cfields == fields

@@ -1,5 +1,5 @@
 # A/B on one box (developer aid): GPU tests of the working tree's build, then per-corpus kernel
-# times of each ab/libdmx_<name>.so given in $LIBS (default "base skip").
+# times of each ab/libdmx_<name>.so given in $LIBS ("base" = the in-tree build).
 # usage: gpurun -- 'bash tools/gpu_ab.sh'   (MIB, KINDS, LEVEL, TESTS=0 to skip the tests)
 set -e
 mkdir -p gpurun_out && cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
@@ -11,6 +11,7 @@ fi
 for r in 1 2; do
   for v in ${LIBS:-base skip}; do
     echo "== $v (pass $r)"
-    DMX_LIB=ab/libdmx_$v.so timeout -k 10 200 python tools/kernel_times.py ${MIB:-1024} ${KINDS:-repeat,text,mixed,bmp,zeros,random} ${LEVEL:-2} 2>&1 | grep -v "^W\|^E\|amdgpu.ids"
+    lib=ab/libdmx_$v.so; [ $v = base ] && lib=deflate.hpp_amd/lib/libdmx.so
+    DMX_LIB=$lib timeout -k 10 200 python tools/kernel_times.py ${MIB:-1024} ${KINDS:-repeat,text,mixed,bmp,zeros,random} ${LEVEL:-2} 2>&1 | grep -v "^W\|^E\|amdgpu.ids"
   done
 done
