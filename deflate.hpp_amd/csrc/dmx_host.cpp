@@ -182,6 +182,13 @@ void phase_dump(dmx_ctx* c, const char* kernel, uint64_t nidx, hipStream_t st) {
     }
     if (inf)
         for (int k = 8; k < kPhaseSlots; k++) std::fprintf(f, " x%d=%.1f", k, xcnt[k] ? xsum[k] / xcnt[k] : 0.0);
+    if (!inf && nidx) {  // raw means of slots 4..7 (counters in a DMX_DF_PDIAG build)
+        for (int k = 4; k < 8; k++) {
+            double a = 0;
+            for (uint64_t i = 0; i < nidx; i++) a += (double)h[i * kPhaseSlots + k];
+            if (a / nidx < 1e12) std::fprintf(f, " r%d=%.1f", k, a / nidx);
+        }
+    }
     std::fprintf(f, "\n");
     std::fclose(f);
 }
@@ -311,7 +318,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     // its predecessor's exact end (FB_V_EXACT repair rounds).
     constexpr uint64_t kStored = 1ull << 62;
     constexpr uint64_t kVirtStep = 1ull << 18, kVirtGap = 4 * kVirtStep;
-    constexpr int kRepairRounds = 4;
+    constexpr int kRepairRounds = 8;
     const uint64_t nbits = 8ull * n;
     std::vector<uint64_t> starts, vhdr;
     std::vector<uint8_t> strong, vmode;
@@ -468,7 +475,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
                 final_in_force = (state & FB_STATE_FINAL) != 0;
             }
             auto it = std::lower_bound(by.begin(), by.end(), std::make_pair(u.end, 0u));
-            if (it != by.end() && it->first == u.end) {
+            if (it != by.end() && it->first == u.end && it->second != k) {
                 // inside a final block a virtual unit is right only up to a soft stop: one that
                 // passed a header or ended at one read past the final end of block (its guess
                 // said not final), and is redone from here with the final state
@@ -481,8 +488,14 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
                 }
             }
             breaks.emplace_back(u.end, state);
-            if (it == by.end()) break;
-            k = it->second;  // (optimistic: the first unit starting after the break)
+            // (optimistic: on with the unit after this one in start order, even one that starts
+            // before the break -- a virtual unit whose warm-up missed the token path records a
+            // start off it, but it re-synchronises within its span, so its end is on the path:
+            // the break there gets its repair in this same round, and a run of such units costs
+            // one round instead of one round each)
+            auto self = std::lower_bound(by.begin(), by.end(), std::make_pair(u.start, (uint32_t)k));
+            if (self == by.end() || self->second != k || ++self == by.end()) break;
+            k = self->second;
         }
         if (fin && breaks.empty()) break;
         if (breaks.empty() || round == kRepairRounds || Ku + breaks.size() > Kcap)
