@@ -92,23 +92,6 @@ constexpr uint32_t DF_L3_RP = DMX_L3_RP;
 #define DMX_DF_SKIP 1
 #endif
 constexpr bool DF_SKIP = DMX_DF_SKIP != 0;
-// level 3: the chain search feeds lanes from per-wave position lists (balanced chains)
-#ifndef DMX_L3_QUEUE
-#define DMX_L3_QUEUE 0
-#endif
-// levels 2-3: the token words in one walk, staged in LDS
-#ifndef DMX_DF_TOKW1
-#define DMX_DF_TOKW1 0
-#endif
-// levels 2-3: two quads parse each chunk, from its start and from its middle (see the walk)
-#ifndef DMX_DF_SPLIT
-#define DMX_DF_SPLIT 0
-#endif
-// level 2: once the run continuation covers the rest of the segment, the remaining rounds'
-// candidates are written in one loop (no per-round bookkeeping)
-#ifndef DMX_DF_BULKSKIP
-#define DMX_DF_BULKSKIP 0
-#endif
 // token-word count of a segment without any match (k_deflate_emit then reads its input's bytes)
 constexpr uint32_t EM_ALL_LITERALS = 0xFFFFFFFFu;
 
@@ -448,7 +431,7 @@ struct DfSmem {
     uint32_t tokmap[SEG / 32];  // token-start bitmap (parse walk; chunks share boundary words)
     uint16_t lasttok[NWALK + 1];  // last token start of each parse chunk
     uint32_t scan[4 * DF_NT / 64];
-    uint32_t sh[64];  // 44: run candidate, 46: mismatch tag, 47: token-word overflow, 48..62: divisor-period tags
+    uint32_t sh[64];  // 44: run candidate, 46: mismatch tag, 48..62: divisor-period tags
 };
 
 // Persistent workgroups: the next segment of this workgroup (seg + gridDim.x) is loaded straight
@@ -518,7 +501,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         // zero padding after the data (match compares read up to 8 bytes past)
         for (uint32_t i = nb + t; i < ((nb + 3) & ~3u) + 32; i += DF_NT) dbytes[i] = 0;
         if (t < NMAP) S.tokmap[t] = 0;
-        if (t == 0) S.sh[46] = 0, S.sh[47] = 0;  // the rounds' mismatch tag, the token-word overflow flag
+        if (t == 0) S.sh[46] = 0;  // the match rounds' mismatch tag (run continuation)
         if (t >= 48 && t < 63) S.sh[t] = 0;  // its divisor-period tags
         if (level >= 2)
             for (int i = t; i < 2 * HT; i += DF_NT) S.U[i] = 0;
@@ -633,23 +616,11 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                     uint32_t skip_d = 0, skip_end = 0, wait = 0, backoff = 1;  // uniform
                     skipped = false;
                     bool pend = false;  // the previous round was a normal one (sh[44] is read)
-                    bool all_done = false;  // (uniform) the rounds of the rest of the segment are written
                     auto round = [&](uint32_t r0, uint32_t rr, RoundState& cur, const RoundState& prev, auto full) {
                         constexpr bool FULL = decltype(full)::value;
-                        if (DMX_DF_BULKSKIP && all_done) return;
                         const uint32_t p0 = r0 + 2 * tt, p1 = p0 + 1;
                         if (SKIP && skip_d) {
                             if (r0 + RP <= skip_end || skip_end >= nb) {  // inside the verified run
-                                if (DMX_DF_BULKSKIP && skip_end >= nb) {  // ... up to the segment end:
-                                    for (uint32_t r = r0; r < nb; r += RP) {  // every remaining round now
-                                        const uint32_t q0 = r + 2 * tt;
-                                        if (q0 < nb)
-                                            cand32[q0 >> 1] = (q0 + 4 <= nb ? skip_d : 0u) | ((q0 + 5 <= nb ? skip_d : 0u) << 16);
-                                    }
-                                    all_done = true;
-                                    skipped = true;
-                                    return;
-                                }
                                 if (FULL || p0 < nb)
                                     cand32[p0 >> 1] = (FULL || p0 + 4 <= nb ? skip_d : 0u) |
                                                       ((FULL || p1 + 4 <= nb ? skip_d : 0u) << 16);
@@ -806,92 +777,6 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
             }
             DMX_PHASE(A.dbg, seg, 14);
         }
-#if DMX_L3_QUEUE
-        if (level == 3) {
-            // ---- level 3: deeper search along the candidate chains, lanes fed from a queue ------
-            // Same search and same results as the lockstep form below (#else), but a lane whose
-            // chain ends takes the next position of its wave's list at once, so a wave costs its
-            // total hops / 64 instead of 64 x its longest chain per position group (text: 6.1
-            // hops per position on average, 2.45x that in lockstep; a third of the positions
-            // have no candidate at all).  The results cannot go to cand[] while chains still read
-            // it, so the segment goes in quarters, last first: a quarter's chains read links in
-            // the quarter and before it (links point backwards), all still the rounds' own;
-            // its results collect in the dead hash table and replace the quarter's entries after
-            // a barrier.  The hash table holds a quarter's results (Q u16) and each wave's list of
-            // its Q / 16 positions that have a candidate (Q u16).
-            constexpr uint32_t Q = SEG / 4, QW = Q / (DF_NT / 64);  // positions per quarter, per wave
-            static_assert(sizeof(S.U) >= 4 * Q, "results + lists live in the hash table");
-            uint16_t* const res = reinterpret_cast<uint16_t*>(S.U);
-            uint16_t* const lst = res + Q;
-            const uint32_t lane = (uint32_t)lane_id(), wv = (uint32_t)t >> 6;
-            const uint64_t below = (1ull << lane) - 1ull;
-            for (int qi = 3; qi >= 0; qi--) {
-                const uint32_t qb = (uint32_t)qi * Q, wb = qb + wv * QW;
-                uint16_t* const wl = lst + wv * QW;
-                // the wave's positions with a candidate, in order (ballot compaction)
-                uint32_t cnt = 0;
-                for (uint32_t g = 0; g < QW; g += 64) {
-                    const uint32_t pp = wb + g + lane;
-                    const bool has = pp < nb && S.cand[pp] != 0;
-                    const uint64_t m = __ballot(has);
-                    if (has) wl[cnt + (uint32_t)__popcll(m & below)] = (uint16_t)pp;
-                    res[pp - qb] = 0;
-                    cnt += (uint32_t)__popcll(m);
-                }
-                wave_sync();
-                // lane state: position p, link position q, best length / distance, tail word
-                uint32_t cur = 0, p = 0, q = 0, bl = 2, bd = 0, tail = 0, hop = 0, maxl = 0;
-                bool act = false;
-                auto take = [&](bool need) {  // lanes with need take the next list entries
-                    const uint64_t m = __ballot(need);
-                    if (need) {
-                        const uint32_t i = cur + (uint32_t)__popcll(m & below);
-                        act = i < cnt;
-                        if (act) {
-                            p = wl[i];
-                            q = p;
-                            bl = 2, bd = 0, tail = 0, hop = 0;
-                            maxl = min(258u, min(p / DF_CHUNK * DF_CHUNK + DF_CHUNK, nb) - p);
-                        }
-                    }
-                    cur += (uint32_t)__popcll(m);
-                };
-                take(true);
-                while (__ballot(act)) {
-                    if (act) {
-                        // one link: the first (q = p) is measured in full, later ones only when
-                        // the 4 bytes ending at the best length match (zlib's scan_end test)
-                        const uint32_t dq = S.cand[q];
-                        bool done = dq == 0;
-                        if (!done) {
-                            q -= dq;
-                            if (bl < 3 || lds_rd32u(S.data32, q + bl - 3) == tail) {
-                                // (the first link up to DF_L3_LONG bytes: that long ends the search)
-                                const uint32_t L = matchlen_u(S.data32, p, q, hop ? maxl : min(maxl, DF_L3_LONG));
-                                if (L > bl) {
-                                    bl = L;
-                                    bd = p - q;
-                                    tail = lds_rd32u(S.data32, p + bl - 3);
-                                }
-                            }
-                            hop++;
-                            done = hop >= (uint32_t)DF_L3_DEPTH || bl >= maxl || bl >= DF_L3_LONG;
-                        }
-                        if (done) {
-                            res[p - qb] = (uint16_t)bd;
-                            act = false;
-                        }
-                    }
-                    // (all lanes: the ballot in take is wave-wide)
-                    take(!act && cur < cnt);
-                }
-                __syncthreads();
-                for (uint32_t i = t; i < Q; i += DF_NT)
-                    if (qb + i < nb) S.cand[qb + i] = res[i];
-                __syncthreads();
-            }
-        }
-#else
         if (level == 3) {
             // ---- level 3: deeper search along the candidate chains ----------------------------
             // cand[q] links q to an earlier occurrence of its 4-byte key, so p -> p - cand[p] ->
@@ -957,7 +842,6 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
             }
             __syncthreads();
         }
-#endif
         if (level >= 2) {
             // match bitmap from the candidates: bit p = "a candidate starts at p"
             for (uint32_t w = t; w < NMAP; w += DF_NT) {
@@ -983,34 +867,11 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         // ---- parse walk: one DF_CHUNK-byte chunk per quad of lanes (the four walk in step and
         //      share the match-length compares, matchlen4); jumps over literal runs with the
         //      match bitmap, ORs token starts into tokmap (neighbouring chunks share words) -----
-        // DMX_DF_SPLIT: two quads per chunk.  Quad A parses from the chunk start up to its first
-        // token boundary at or past the middle; quad B parses the second half from the middle
-        // at the same time, into side storage (its token starts in bmB, lengths in lenB,
-        // collisions in colB -- it must not change cand[], which A may still read).  After a
-        // barrier A goes on greedily from where it stopped until it lands on one of B's token
-        // starts (greedy parses from different starts meet within a few tokens); after a second
-        // barrier B commits its tokens from that point on.  The tokens are exactly the greedy
-        // parse's from the chunk start, except that a long match's smallest-distance probe may
-        // start from a distance B already reduced (a shorter distance of the same length).
-        constexpr bool SPLIT = DMX_DF_SPLIT != 0;
-        constexpr uint32_t NQ = SPLIT ? 8 : 4;        // lanes per chunk
-        constexpr uint32_t MIDOFF = DF_CHUNK / 2;      // B's start in its chunk
-        uint32_t* const bmB = S.U;                     // SPLIT: B's token starts (SEG / 32 words)
-        uint32_t* const colB = S.U + SEG / 32;         //        B's literals at candidates
-        uint16_t* const syncB = reinterpret_cast<uint16_t*>(S.U + SEG / 16);      // per chunk
-        uint16_t* const lastB = syncB + NWALK + 1;                                 // per chunk
-        uint8_t* const lenB = reinterpret_cast<uint8_t*>(lastB + NWALK + 1);      // L - 3 per B position
-        static_assert(!SPLIT || sizeof(S.U) >= SEG / 4 + 4 * (NWALK + 1) + NWALK * (DF_CHUNK - DF_CHUNK / 2),
-                      "split-parse side storage lives in the hash table");
-        const bool wactive = level >= 2 && t < (int)(NQ * NWALK);  // (level: uniform)
-        {
+        if (level >= 2 && t < 4 * NWALK) {
             const uint32_t sub = t & 3;
             const bool lead = sub == 0;
-            const uint32_t ci = (uint32_t)t / NQ;            // chunk
-            const bool isB = SPLIT && ((t >> 2) & 1);
-            const uint32_t lo = ci * DF_CHUNK;
+            const uint32_t lo = (t >> 2) * DF_CHUNK;
             const uint32_t hi = min(lo + DF_CHUNK, nb);
-            const uint32_t mid = min(lo + MIDOFF, hi);
             auto bits_range = [](uint32_t a, uint32_t b, uint32_t w) -> uint32_t {  // [a, b) in word w
                 const uint32_t e = b - w * 32;
                 return (e >= 32 ? 0xFFFFFFFFu : ((1u << e) - 1u)) & (0xFFFFFFFFu << (a & 31));
@@ -1018,215 +879,127 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
             auto full_len = [&](uint32_t q) -> uint32_t {  // < 3 only on a fingerprint collision
                 return matchlen4(S.data32, q, q - S.cand[q], min(258u, hi - q), sub);
             };
+            uint32_t p = lo, w = lo >> 5, mw = S.mmap[w], tok = 0, lastp = lo;  // lastp: last token
             auto mbit = [&](uint32_t q) -> bool {
                 return (S.mmap[q >> 5] >> (q & 31)) & 1u;
             };
-            // MODE 0: the whole chunk (no split) -- 1: A's first part, up to the first token start
-            // >= mid -- 2: A's continuation, up to the first of B's token starts -- 3: B's part.
-            // Returns where it stopped; lastp = its last token start.
-            uint32_t lastp = lo;
-            uint32_t pend = 0;  // A's first part: the length of a match at mid - 1, written later
-            auto walk = [&](auto mode, uint32_t p, uint32_t until) -> uint32_t {
-                constexpr int MODE = decltype(mode)::value;
-                uint32_t* const tmap = MODE == 3 ? bmB : S.tokmap;
-                uint32_t w = p >> 5, mw = S.mmap[w], tok = 0, bw = MODE == 2 ? bmB[w] : 0u;
-                auto flush = [&]() {
-                    if (tok && lead) {
-                        if (MODE == 3) tmap[w] |= tok;  // (B owns its words; A never reads them)
-                        else atomicOr(&tmap[w], tok);
-                    }
-                };
-                while (p < until) {
-                    const uint32_t wi = p >> 5;
-                    if (wi != w) {
-                        flush();
-                        w = wi;
-                        mw = S.mmap[w];
-                        if (MODE == 2) bw = bmB[w];
-                        tok = 0;
-                    }
-                    const uint32_t m = mw & (0xFFFFFFFFu << (p & 31));
-                    uint32_t q = m ? w * 32 + __builtin_ctz(m) : 0xFFFFFFFFu;
-                    if (MODE == 2) {  // the first of B's token starts in [p, next match start]
-                        const uint32_t e = min(min(q, (w + 1) * 32 - 1), until - 1);  // (inclusive)
-                        const uint32_t sm = bw & bits_range(p, e + 1, w);
-                        if (sm) {
-                            const uint32_t s0 = w * 32 + __builtin_ctz(sm);
-                            tok |= bits_range(p, s0, w);
-                            if (s0 > p) lastp = s0 - 1;
-                            p = s0;
-                            break;
-                        }
-                    }
-                    if (q >= until || !m) {  // literals to the end of the word (or part)
-                        const uint32_t e = min((w + 1) * 32, until);
-                        tok |= bits_range(p, e, w);
-                        lastp = e - 1;
-                        p = e;
-                        continue;
-                    }
-                    tok |= bits_range(p, q, w);  // literals before the match
-                    p = q;
-                    lastp = p;
-                    const uint32_t L = full_len(p);
-                    bool lit = L < 3;  // a fingerprint collision, not a match
-                    if (!lit && level == 3 && L < 258 && p + 1 < hi && mbit(p + 1))
-                        lit = full_len(p + 1) > L;  // lazy: literal here, the longer match next
-                    if (lit) {
+            while (p < hi) {
+                const uint32_t wi = p >> 5;
+                if (wi != w) {
+                    if (tok && lead) atomicOr(&S.tokmap[w], tok);
+                    w = wi;
+                    mw = S.mmap[w];
+                    tok = 0;
+                }
+                const uint32_t m = mw & (0xFFFFFFFFu << (p & 31));
+                const uint32_t q = m ? w * 32 + __builtin_ctz(m) : 0xFFFFFFFFu;
+                if (q >= hi || !m) {  // literals to the end of the word (or chunk)
+                    const uint32_t e = min((w + 1) * 32, hi);
+                    tok |= bits_range(p, e, w);
+                    lastp = e - 1;
+                    p = e;
+                    continue;
+                }
+                tok |= bits_range(p, q, w);  // literals before the match
+                p = q;
+                lastp = p;
+                uint32_t L = full_len(p);
+                if (L < 3) {  // fingerprint collision, not a match: a literal
+                    tok |= 1u << (p & 31);
+                    if (lead) S.cand[p] = 0;
+                    p++;
+                    continue;
+                }
+                if (level == 3 && L < 258 && p + 1 < hi && mbit(p + 1)) {
+                    if (full_len(p + 1) > L) {  // lazy: literal here, the longer match next
                         tok |= 1u << (p & 31);
-                        if (lead) {
-                            if (MODE == 3) atomicOr(&colB[p >> 5], 1u << (p & 31));
-                            else S.cand[p] = 0;
-                        }
+                        if (lead) S.cand[p] = 0;
                         p++;
                         continue;
                     }
-                    if (L >= 32) {
-                        // long match: prefer the smallest distance giving the same length -- a short
-                        // period (1..4) or a divisor c / k of the candidate (periodic data: a table,
-                        // an image row, a repeated record).  Equal distances of consecutive matches
-                        // are what the lane decoder merges into one periodic copy.
-                        const uint32_t c = S.cand[p];
-                        const uint32_t ml = min(258u, hi - p);
-                        uint32_t best = c;
-                        {   // periods 1..4: one 16-byte compare round (lane sub tests 1 + sub), then
-                            // full lengths only for the periods that passed, shortest first
-                            const uint32_t dd = 1 + sub;
-                            bool pass = false;
-                            if (dd < c && dd <= p) {
-                                const uint32_t ip = p >> 2, sp = p & 3, iq = (p - dd) >> 2, sq = (p - dd) & 3;
-                                uint32_t x = 0;
+                }
+                if (L >= 32) {
+                    // long match: prefer the smallest distance giving the same length -- a short
+                    // period (1..4) or a divisor c / k of the candidate (periodic data: a table,
+                    // an image row, a repeated record).  Equal distances of consecutive matches
+                    // are what the lane decoder merges into one periodic copy.
+                    const uint32_t c = S.cand[p];
+                    const uint32_t ml = min(258u, hi - p);
+                    uint32_t best = c;
+                    {   // periods 1..4: one 16-byte compare round (lane sub tests 1 + sub), then
+                        // full lengths only for the periods that passed, shortest first
+                        const uint32_t dd = 1 + sub;
+                        bool pass = false;
+                        if (dd < c && dd <= p) {
+                            const uint32_t ip = p >> 2, sp = p & 3, iq = (p - dd) >> 2, sq = (p - dd) & 3;
+                            uint32_t x = 0;
 #pragma unroll
-                                for (int k = 0; k < 4; k++)
-                                    x |= __builtin_amdgcn_alignbyte(S.data32[ip + k + 1], S.data32[ip + k], sp) ^
-                                         __builtin_amdgcn_alignbyte(S.data32[iq + k + 1], S.data32[iq + k], sq);
-                                pass = x == 0;
-                            }
-                            const int qb = lane_id() & ~3;
-                            uint32_t pm = (uint32_t)(__ballot(pass) >> qb) & 0xFu;
-                            while (pm) {
-                                const uint32_t d1 = 1 + (uint32_t)__builtin_ctz(pm);
-                                pm &= pm - 1;
-                                if (matchlen4(S.data32, p, p - d1, ml, sub) >= L) {
-                                    best = d1;
-                                    break;
-                                }
+                            for (int k = 0; k < 4; k++)
+                                x |= __builtin_amdgcn_alignbyte(S.data32[ip + k + 1], S.data32[ip + k], sp) ^
+                                     __builtin_amdgcn_alignbyte(S.data32[iq + k + 1], S.data32[iq + k], sq);
+                            pass = x == 0;
+                        }
+                        const int qb = lane_id() & ~3;
+                        uint32_t pm = (uint32_t)(__ballot(pass) >> qb) & 0xFu;
+                        while (pm) {
+                            const uint32_t d1 = 1 + (uint32_t)__builtin_ctz(pm);
+                            pm &= pm - 1;
+                            if (matchlen4(S.data32, p, p - d1, ml, sub) >= L) {
+                                best = d1;
+                                break;
                             }
                         }
-                        if (!DF_SKIP && best == c) {  // one probe at c / k, k the largest divisor <= 8 (a
-                                                      // probe per k would serialize across lanes that differ in k)
-                            uint32_t k = 1;
+                    }
+                    if (!DF_SKIP && best == c) {  // one probe at c / k, k the largest divisor <= 8 (a
+                                                  // probe per k would serialize across lanes that differ in k)
+                        uint32_t k = 1;
 #pragma unroll
-                            for (uint32_t q2 = 2; q2 <= 8; q2++) k = (c % q2 == 0) ? q2 : k;
-                            if (k > 1 && matchlen4(S.data32, p, p - c / k, ml, sub) >= L) best = c / k;
+                        for (uint32_t q = 2; q <= 8; q++) k = (c % q == 0) ? q : k;
+                        if (k > 1 && matchlen4(S.data32, p, p - c / k, ml, sub) >= L) best = c / k;
+                    }
+                    if (DF_SKIP && best == c) {
+                        // divisors c / k of the candidate, k <= 16 (the run-continuation rounds give
+                        // every position of a run the same, possibly far, multiple of the period): lane sub takes the (sub + 1)-th
+                        // largest k dividing c; one 16-byte compare round for the four, then full
+                        // lengths for those that passed, smallest distance first
+                        uint32_t k = 0, seen = 0;
+#pragma unroll
+                        for (uint32_t q = 16; q >= 2; q--) {
+                            const bool dv = c % q == 0;
+                            k = (dv && seen == sub) ? q : k;
+                            seen += dv ? 1u : 0u;
                         }
-                        if (DF_SKIP && best == c) {
-                            // divisors c / k of the candidate, k <= 16 (the run-continuation rounds give
-                            // every position of a run the same, possibly far, multiple of the period): lane
-                            // sub takes the (sub + 1)-th largest k dividing c; one 16-byte compare round for
-                            // the four, then full lengths for those that passed, smallest distance first
-                            uint32_t k = 0, seen = 0;
+                        const uint32_t dk = k ? c / k : 0u;
+                        bool pass = false;
+                        if (dk > 4) {  // (1..4 were tested above)
+                            const uint32_t ip = p >> 2, sp = p & 3, iq = (p - dk) >> 2, sq = (p - dk) & 3;
+                            uint32_t x = 0;
 #pragma unroll
-                            for (uint32_t q2 = 16; q2 >= 2; q2--) {
-                                const bool dv = c % q2 == 0;
-                                k = (dv && seen == sub) ? q2 : k;
-                                seen += dv ? 1u : 0u;
-                            }
-                            const uint32_t dk = k ? c / k : 0u;
-                            bool pass = false;
-                            if (dk > 4) {  // (1..4 were tested above)
-                                const uint32_t ip = p >> 2, sp = p & 3, iq = (p - dk) >> 2, sq = (p - dk) & 3;
-                                uint32_t x = 0;
-#pragma unroll
-                                for (int j = 0; j < 4; j++)
-                                    x |= __builtin_amdgcn_alignbyte(S.data32[ip + j + 1], S.data32[ip + j], sp) ^
-                                         __builtin_amdgcn_alignbyte(S.data32[iq + j + 1], S.data32[iq + j], sq);
-                                pass = x == 0;
-                            }
-                            const int qb = lane_id() & ~3;
-                            uint32_t pm = (uint32_t)(__ballot(pass) >> qb) & 0xFu;
-                            while (pm) {
-                                const int f = __builtin_ctz(pm);
-                                pm &= pm - 1;
-                                const uint32_t d1 = (uint32_t)__shfl((int)dk, qb + f, 64);
-                                if (matchlen4(S.data32, p, p - d1, ml, sub) >= L) {
-                                    best = d1;
-                                    break;
-                                }
-                            }
+                            for (int j = 0; j < 4; j++)
+                                x |= __builtin_amdgcn_alignbyte(S.data32[ip + j + 1], S.data32[ip + j], sp) ^
+                                     __builtin_amdgcn_alignbyte(S.data32[iq + j + 1], S.data32[iq + j], sq);
+                            pass = x == 0;
                         }
-                        if (lead) S.cand[p] = (uint16_t)best;  // (a valid distance for p either way)
-                    }
-                    tok |= 1u << (p & 31);
-                    if (lead) {
-                        if (MODE == 3) lenB[ci * (DF_CHUNK - MIDOFF) + (p - mid)] = (uint8_t)(L - 3);
-                        else if (MODE == 1 && p + 1 >= mid) pend = L;  // (B may read cand[mid])
-                        else S.cand[p + 1] = (uint16_t)L;
-                    }
-                    p += L;
-                }
-                flush();
-                return p;
-            };
-#ifdef DMX_DF_PDIAG
-            const uint64_t pd_t0 = __builtin_amdgcn_s_memtime();
-#endif
-            if (!SPLIT) {
-                if (wactive) {
-                    walk(std::integral_constant<int, 0>{}, lo, hi);
-                    if (lead) S.lasttok[ci] = (uint16_t)lastp;
-                }
-            } else if (level >= 2) {
-                uint32_t pa = lo;
-                if (wactive && !isB) {
-                    pa = walk(std::integral_constant<int, 1>{}, lo, mid);
-                } else if (wactive && mid < hi) {
-                    // B: clear its side words, then parse [mid, hi)
-                    for (uint32_t wz = (mid >> 5) + sub; wz <= ((hi - 1) >> 5); wz += 4) bmB[wz] = 0, colB[wz] = 0;
-                    lastp = mid;
-                    walk(std::integral_constant<int, 3>{}, mid, hi);
-                    if (lead) lastB[ci] = (uint16_t)lastp;
-                }
-                __syncthreads();
-                if (wactive && !isB) {
-                    if (lead && pend) S.cand[mid] = (uint16_t)pend;
-                    const uint32_t sy = pa < hi ? walk(std::integral_constant<int, 2>{}, pa, hi) : hi;
-                    if (lead) {
-                        syncB[ci] = (uint16_t)(sy - lo);
-                        S.lasttok[ci] = (uint16_t)(sy < hi ? 0u : lastp);
-                    }
-                }
-                __syncthreads();
-                if (wactive && isB && mid < hi) {
-                    // B's tokens from the meeting point on: token starts into tokmap, their lengths
-                    // into cand[p + 1], their collision literals into cand[p] = 0
-                    const uint32_t sy = lo + syncB[ci];
-                    if (sy < hi) {
-                        for (uint32_t wz = (sy >> 5) + sub; wz <= ((hi - 1) >> 5); wz += 4) {
-                            uint32_t bits = bmB[wz] & bits_range(max(sy, wz * 32), min(hi, wz * 32 + 32), wz);
-                            if (!bits) continue;
-                            atomicOr(&S.tokmap[wz], bits);
-                            const uint32_t cb = colB[wz], mb = S.mmap[wz];
-                            while (bits) {
-                                const uint32_t b = (uint32_t)__builtin_ctz(bits);
-                                bits &= bits - 1;
-                                const uint32_t pp = wz * 32 + b;
-                                if ((cb >> b) & 1u) S.cand[pp] = 0;
-                                else if ((mb >> b) & 1u) S.cand[pp + 1] = (uint16_t)(lenB[ci * (DF_CHUNK - MIDOFF) + (pp - mid)] + 3u);
+                        const int qb = lane_id() & ~3;
+                        uint32_t pm = (uint32_t)(__ballot(pass) >> qb) & 0xFu;
+                        while (pm) {
+                            const int f = __builtin_ctz(pm);
+                            pm &= pm - 1;
+                            const uint32_t d1 = (uint32_t)__shfl((int)dk, qb + f, 64);
+                            if (matchlen4(S.data32, p, p - d1, ml, sub) >= L) {
+                                best = d1;
+                                break;
                             }
                         }
-                        if (lead) S.lasttok[ci] = lastB[ci];
                     }
+                    if (lead) S.cand[p] = (uint16_t)best;
                 }
+                tok |= 1u << (p & 31);
+                if (lead) S.cand[p + 1] = (uint16_t)L;
+                p += L;
             }
-#ifdef DMX_DF_PDIAG
-            if (wactive && lead && A.dbg && !isB) {  // per segment: slowest walk, walk cycles summed
-                unsigned long long* const d = reinterpret_cast<unsigned long long*>(A.dbg + seg * kPhaseSlots);
-                const unsigned long long dt = __builtin_amdgcn_s_memtime() - pd_t0;
-                atomicMax(d + 4, dt);
-                atomicAdd(d + 5, dt);
-            }
-#endif
+            if (tok && lead) atomicOr(&S.tokmap[w], tok);
+            if (lead) S.lasttok[t >> 2] = (uint16_t)lastp;
         }
         __syncthreads();
         DMX_PHASE(A.dbg, seg, 3);
@@ -1361,32 +1134,12 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                 if (nl) emit(lit | (nl << 24));
             };
             uint32_t nw = 0;
-#if DMX_DF_TOKW1
-            // one walk: the words go to LDS (the dead hash table, word i of thread t at
-            // i * DF_NT + t), then to HBM once the block scan gives their offset; a thread with more
-            // words than fit walks again straight to HBM (uniform: the flag is read after the scan)
-            constexpr uint32_t KW = (uint32_t)(sizeof(S.U) / 4 / DF_NT);
-            uint32_t* const stage = S.U + t;
-            walk([&](uint32_t v) {
-                if (nw < KW) stage[nw * DF_NT] = v;
-                nw++;
-            });
-            if (nw > KW) S.sh[47] = 1;
-#else
             walk([&](uint32_t) { nw++; });
-#endif
             uint32_t wtot;
             const uint32_t woff = block_excl_scan(nw, S.scan, &wtot);
             uint32_t* const dst = A.tok + seg * (uint64_t)A.tok_stride + woff;
-#if DMX_DF_TOKW1
-            if (!__builtin_amdgcn_readfirstlane(S.sh[47])) {
-                for (uint32_t j = 0; j < nw; j++) dst[j] = stage[j * DF_NT];
-            } else
-#endif
-            {
-                uint32_t j = 0;
-                walk([&](uint32_t v) { dst[j++] = v; });
-            }
+            uint32_t j = 0;
+            walk([&](uint32_t v) { dst[j++] = v; });
             if (t == 0) A.ntok[seg] = wtot;
         }
         DMX_PHASE(A.dbg, seg, 11);
@@ -1667,14 +1420,10 @@ __device__ __forceinline__ void em_flush(uint32_t* stg, uint32_t* dst, uint32_t 
 }
 
 // DMX_PHASES: one stamp per wave (its lane 0) into the segment's slots 4..9
-#ifdef DMX_DF_PDIAG  // diagnostic build: slots 4..7 hold the front kernel's parse-walk counters
-#define EM_PHASE(dbg, seg, slot) do { } while (0)
-#else
 #define EM_PHASE(dbg, seg, slot)                                                          \
     do {                                                                                  \
         if ((dbg) && lane_id() == 0) (dbg)[(seg) * kPhaseSlots + (slot)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
-#endif
 
 template <int SEG, bool RAW>
 __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
@@ -1921,10 +1670,13 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
     }
     // ---- stored block: [BFINAL|00][LEN][NLEN][data] (+ the empty stored block) ------------
     const uint32_t total = (uint32_t)stored_bytes;
-    const uint32_t nw = (total + 3) / 4;
-#pragma unroll 2
-    for (uint32_t k = lane; k < nw; k += 64) {
-        // output word k = bytes 4k .. 4k + 3; data byte i is output byte 5 + i
+    // 16 output bytes per lane and step, four steps in flight (the copy is latency-bound):
+    // output bytes [16 k, 16 k + 16) are input bytes [16 k - 5, 16 k + 11), five input words
+    // funnelled by the segment's constant misalignment; the first 16 bytes (header) and the
+    // tail go word by word
+    const uint32_t n16 = (total + 15) / 16;
+    uint4* const slot4 = reinterpret_cast<uint4*>(slot);
+    auto word_at = [&](uint32_t k) -> uint32_t {  // output word k = bytes 4k .. 4k + 3
         uint32_t w = 0;
         if (k >= 2 && 4 * k + 3 < 5 + nb) {
             const uint32_t x = 4 * k - 5 + (uint32_t)mis;  // aligned-base byte of the first
@@ -1946,7 +1698,26 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
                 w |= byte << (8 * j);
             }
         }
-        slot[k] = w;
+        return w;
+    };
+#pragma unroll 4
+    for (uint32_t k4 = lane; k4 < n16; k4 += 64) {
+        uint4 o;
+        if (k4 >= 1 && 16 * k4 + 15 < 5 + nb) {
+            const uint32_t x = 16 * k4 - 5 + (uint32_t)mis, i0 = x >> 2, sh = x & 3;
+            const uint32_t a0 = inw[i0], a1 = inw[i0 + 1], a2 = inw[i0 + 2], a3 = inw[i0 + 3];
+            const uint32_t a4 = i0 + 4 < in_words_end ? inw[i0 + 4] : 0u;
+            o.x = __builtin_amdgcn_alignbyte(a1, a0, sh);
+            o.y = __builtin_amdgcn_alignbyte(a2, a1, sh);
+            o.z = __builtin_amdgcn_alignbyte(a3, a2, sh);
+            o.w = __builtin_amdgcn_alignbyte(a4, a3, sh);
+        } else {
+            o.x = word_at(4 * k4);
+            o.y = word_at(4 * k4 + 1);
+            o.z = word_at(4 * k4 + 2);
+            o.w = word_at(4 * k4 + 3);
+        }
+        slot4[k4] = o;
     }
     if (lane == 0) A.sizes[seg] = total;
 }

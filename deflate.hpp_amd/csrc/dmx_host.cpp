@@ -182,13 +182,7 @@ void phase_dump(dmx_ctx* c, const char* kernel, uint64_t nidx, hipStream_t st) {
     }
     if (inf)
         for (int k = 8; k < kPhaseSlots; k++) std::fprintf(f, " x%d=%.1f", k, xcnt[k] ? xsum[k] / xcnt[k] : 0.0);
-    if (!inf && nidx) {  // raw means of slots 4..7 (counters in a DMX_DF_PDIAG build)
-        for (int k = 4; k < 8; k++) {
-            double a = 0;
-            for (uint64_t i = 0; i < nidx; i++) a += (double)h[i * kPhaseSlots + k];
-            if (a / nidx < 1e12) std::fprintf(f, " r%d=%.1f", k, a / nidx);
-        }
-    }
+
     std::fprintf(f, "\n");
     std::fclose(f);
 }
@@ -318,7 +312,10 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     // its predecessor's exact end (FB_V_EXACT repair rounds).
     constexpr uint64_t kStored = 1ull << 62;
     constexpr uint64_t kVirtStep = 1ull << 18, kVirtGap = 4 * kVirtStep;
-    constexpr int kRepairRounds = 8;
+    // A region of fixed-code literals below 144 (8-bit codes only) never re-synchronises: every
+    // virtual unit inside it that missed the token path stays off it, and such a run of units is
+    // repaired one per round, each round one lane-parallel launch (~0.3 ms)
+    constexpr int kRepairRounds = 48;
     const uint64_t nbits = 8ull * n;
     std::vector<uint64_t> starts, vhdr;
     std::vector<uint8_t> strong, vmode;
@@ -369,7 +366,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         const uint64_t w = bounded ? std::min<uint64_t>(stop & FB_STOP_MASK, nbits) - std::min(pos, nbits) + 4096 : 4096 + 65536;
         return (w + 63) & ~63ull;
     };
-    const uint64_t R = std::max<uint64_t>(256, K / 4), Kcap = K + R;  // room for repair units
+    const uint64_t R = std::max<uint64_t>(256, K), Kcap = K + R;  // room for repair units
     std::vector<uint64_t> stops(Kcap), tokoff(Kcap + 1);
     starts.resize(Kcap);
     vhdr.resize(Kcap);

@@ -27,8 +27,3 @@ if [ -n "$AB3" ]; then  # the same at level 3 (256 MiB)
   LIBS="base $AB3 $([ -f ab/libdmx_both.so ] && echo both)" TESTS=0 MIB=256 LEVEL=3 KINDS=${AB3_KINDS:-text,mixed,repeat} bash tools/gpu_ab.sh > gpurun_out/ab3.log 2>&1 || { tail -30 gpurun_out/ab3.log; exit 1; }
   cat gpurun_out/ab3.log
 fi
-if [ -f ab/libdmx_pdiag.so ]; then  # parse-walk counters (slots 4..7: slowest walk, summed walk cycles, steps)
-  rm -f gpurun_out/phases_pdiag.txt
-  DMX_LIB=ab/libdmx_pdiag.so DMX_KINDS=repeat,text timeout -k 10 200 python tools/phases.py gpurun_out/phases_pdiag.txt > /dev/null 2>&1 || true
-  cat gpurun_out/phases_pdiag.txt
-fi
