@@ -92,6 +92,18 @@ constexpr uint32_t DF_L3_RP = DMX_L3_RP;
 #define DMX_DF_SKIP 1
 #endif
 constexpr bool DF_SKIP = DMX_DF_SKIP != 0;
+// the front kernel counts the symbols (the emission kernel skips its histogram pass)
+#ifndef DMX_DF_HIST
+#define DMX_DF_HIST 0
+#endif
+// the emission kernel loads its token words two blocks ahead
+#ifndef DMX_EM_PREF
+#define DMX_EM_PREF 0
+#endif
+// level 2: half-size parse chunks for segments without a run (see the parse walk)
+#ifndef DMX_DF_ADAPT
+#define DMX_DF_ADAPT 0
+#endif
 // token-word count of a segment without any match (k_deflate_emit then reads its input's bytes)
 constexpr uint32_t EM_ALL_LITERALS = 0xFFFFFFFFu;
 
@@ -420,6 +432,7 @@ __device__ __forceinline__ RunPlan plan_run(uint32_t v, uint32_t r) {
 template <int SEG>
 struct DfSmem {
     static constexpr int NWALK = (SEG + DF_CHUNK - 1) / DF_CHUNK;
+    static constexpr int NWALK_MAX = DMX_DF_ADAPT ? (SEG + DF_CHUNK / 2 - 1) / (DF_CHUNK / 2) : NWALK;
     static constexpr int HB = df_hash_bits(SEG);
     static constexpr int HT = 1 << HB;  // entries per hash table
     static constexpr int UW = 2 * HT;
@@ -429,9 +442,10 @@ struct DfSmem {
     alignas(16) uint32_t U[UW];
     uint32_t mmap[SEG / 32];    // "a verified match of >= 3 starts here" (match rounds)
     uint32_t tokmap[SEG / 32];  // token-start bitmap (parse walk; chunks share boundary words)
-    uint16_t lasttok[NWALK + 1];  // last token start of each parse chunk
+    uint16_t lasttok[NWALK_MAX + 1];  // last token start of each parse chunk
     uint32_t scan[4 * DF_NT / 64];
     uint32_t sh[64];  // 44: run candidate, 46: mismatch tag, 48..62: divisor-period tags
+    uint32_t hist[DMX_DF_HIST ? 320 : 1];  // the segment's symbol counts (see deflate_tok_stride)
 };
 
 // Persistent workgroups: the next segment of this workgroup (seg + gridDim.x) is loaded straight
@@ -472,16 +486,18 @@ __device__ __forceinline__ uint32_t next_tok(const uint32_t* tokmap, uint32_t& w
     return p;
 }
 
-template <int SEG>
+// L3: level 3 (chain search, lazy parse) -- a separate instantiation, so the level-2 kernel
+// carries none of that code (the 1024-thread kernel's register allocation and code size)
+template <int SEG, bool L3>
 __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG>& S, uint64_t seg,
                                                 bool& staged) {
-    constexpr int NWALK = DfSmem<SEG>::NWALK;
+    [[maybe_unused]] constexpr int NWALK = DfSmem<SEG>::NWALK;
     constexpr int HT = DfSmem<SEG>::HT;
     constexpr int NMAP = SEG / 32;
     const int t = df_tid();
     const uint64_t base = seg * (uint64_t)SEG;
     const uint32_t nb = (uint32_t)min((uint64_t)SEG, A.n - base);
-    const int level = A.level;
+    constexpr int level = L3 ? 3 : 2;  // (the front kernel runs at levels 2 and 3 only)
     uint8_t* const dbytes = reinterpret_cast<uint8_t*>(S.data32);
     DMX_PHASE(A.dbg, seg, 0);
 
@@ -503,6 +519,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         if (t < NMAP) S.tokmap[t] = 0;
         if (t == 0) S.sh[46] = 0;  // the match rounds' mismatch tag (run continuation)
         if (t >= 48 && t < 63) S.sh[t] = 0;  // its divisor-period tags
+        if (DMX_DF_HIST && t < 320) S.hist[t] = 0;
         if (level >= 2)
             for (int i = t; i < 2 * HT; i += DF_NT) S.U[i] = 0;
     }
@@ -511,6 +528,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
     staged = false;
 
     if (level != 0) {
+        bool any_skip = false;  // (uniform) the run continuation took a round of this segment
         // ---- match candidates: rounds of 2*DF_NT positions, two per thread ---------------
         if (level >= 2) {
             // Table entries carry a fingerprint of the 4-byte key (product bits below the hash
@@ -774,6 +792,7 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
                 else
                     run_rounds(std::integral_constant<uint32_t, 2 * DF_NT>{});
                 if (DF_SKIP && skipped) __syncthreads();  // skipped rounds end without a barrier
+                any_skip = skipped;
             }
             DMX_PHASE(A.dbg, seg, 14);
         }
@@ -867,11 +886,16 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         // ---- parse walk: one DF_CHUNK-byte chunk per quad of lanes (the four walk in step and
         //      share the match-length compares, matchlen4); jumps over literal runs with the
         //      match bitmap, ORs token starts into tokmap (neighbouring chunks share words) -----
-        if (level >= 2 && t < 4 * NWALK) {
+        // DMX_DF_ADAPT: at level 2, a segment without a run (no round taken by the run
+        // continuation: short matches, text-like) is parsed in half-size chunks, twice the
+        // walkers; a segment with one keeps 258-byte chunks, whose matches reach the maximum
+        const uint32_t CH = (DMX_DF_ADAPT && level == 2 && !any_skip) ? (uint32_t)DF_CHUNK / 2 : (uint32_t)DF_CHUNK;
+        const uint32_t nwalk = (nb + CH - 1) / CH;
+        if (level >= 2 && (uint32_t)t < 4 * nwalk) {
             const uint32_t sub = t & 3;
             const bool lead = sub == 0;
-            const uint32_t lo = (t >> 2) * DF_CHUNK;
-            const uint32_t hi = min(lo + DF_CHUNK, nb);
+            const uint32_t lo = (t >> 2) * CH;
+            const uint32_t hi = min(lo + CH, nb);
             auto bits_range = [](uint32_t a, uint32_t b, uint32_t w) -> uint32_t {  // [a, b) in word w
                 const uint32_t e = b - w * 32;
                 return (e >= 32 ? 0xFFFFFFFFu : ((1u << e) - 1u)) & (0xFFFFFFFFu << (a & 31));
@@ -1015,8 +1039,8 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         // edges are independent.
         if (level >= 2) {
             const uint32_t sub = t & 3, c = t >> 2;
-            const uint32_t hb = (c + 1) * DF_CHUNK;  // the edge
-            if (t < 4 * (NWALK - 1) && hb < nb) {
+            const uint32_t hb = (c + 1) * CH;  // the edge
+            if ((uint32_t)t < 4 * (nwalk - 1) && hb < nb) {
                 const uint32_t s0 = S.lasttok[c], d0 = S.cand[s0], L0 = S.cand[s0 + 1];
                 const uint32_t sn = S.lasttok[c + 1];  // the extension ends before it
                 if (d0 != 0 && s0 + L0 == hb && L0 < 258 && sn >= hb + 2) {
@@ -1111,6 +1135,13 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
         const bool all_lit = tr_total == nb;
         if (all_lit) {
             if (t == 0) A.ntok[seg] = EM_ALL_LITERALS;
+            if (DMX_DF_HIST)  // the literal histogram, four bytes per word
+                for (uint32_t i = t; 4 * i < nb; i += DF_NT) {
+                    const uint32_t x = S.data32[i];
+#pragma unroll
+                    for (uint32_t b = 0; b < 4; b++)
+                        if (4 * i + b < nb) atomicAdd(&S.hist[(x >> (8 * b)) & 0xFFu], 1u);
+                }
         } else {
             auto walk = [&](auto emit) {
                 uint32_t w = tr.w, m = tr.m, lit = 0, nl = 0;
@@ -1139,11 +1170,26 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
             const uint32_t woff = block_excl_scan(nw, S.scan, &wtot);
             uint32_t* const dst = A.tok + seg * (uint64_t)A.tok_stride + woff;
             uint32_t j = 0;
-            walk([&](uint32_t v) { dst[j++] = v; });
+            walk([&](uint32_t v) {
+                dst[j++] = v;
+                if (DMX_DF_HIST) {  // the symbol counts the emission kernel codes with
+                    if (v >> 31) {
+                        atomicAdd(&S.hist[len_sym(((v >> 16) & 0xFFu) + 3)], 1u);
+                        atomicAdd(&S.hist[288 + dist_sym((v & 0x7FFFu) + 1)], 1u);
+                    } else {
+                        const uint32_t cnt = (v >> 24) & 3u;
+#pragma unroll
+                        for (uint32_t b = 0; b < 3; b++)
+                            if (b < cnt) atomicAdd(&S.hist[(v >> (8 * b)) & 0xFFu], 1u);
+                    }
+                }
+            });
             if (t == 0) A.ntok[seg] = wtot;
         }
         DMX_PHASE(A.dbg, seg, 11);
         __syncthreads();  // every read of the segment's bytes is done
+        if (DMX_DF_HIST && t < (int)kDeflateHistWords)
+            A.tok[seg * (uint64_t)A.tok_stride + A.tok_stride - kDeflateHistWords + t] = S.hist[2 * t] | (S.hist[2 * t + 1] << 16);
         staged = df_prefetch_next<SEG>(A, seg, S);
         DMX_PHASE(A.dbg, seg, 10);
     }
@@ -1154,22 +1200,23 @@ __device__ __forceinline__ void deflate_segment(const DeflateArgs& A, DfSmem<SEG
 // registers per lane, which amdgpu_waves_per_eu(8) asks for.
 // Persistent workgroups (as many as fit the GPU at once): workgroup b compresses segments
 // b, b + G, b + 2G, ... and loads each next segment while it works on the current one.
-template <int SEG>
+template <int SEG, bool L3>
 __device__ __forceinline__ void deflate_segments(const DeflateArgs& A, DfSmem<SEG>& S) {
     bool staged = false;  // S.data32 already holds the segment's bytes
     for (uint64_t seg = blockIdx.x; seg < A.nseg; seg += gridDim.x) {
-        deflate_segment<SEG>(A, S, seg, staged);
+        deflate_segment<SEG, L3>(A, S, seg, staged);
         __syncthreads();  // the next segment reuses the LDS (and its prefetch has landed)
     }
 }
-template <int SEG>
+template <int SEG, bool L3>
 __global__ __launch_bounds__(DF_NT) void k_deflate_segments(DeflateArgs A) {
     __shared__ DfSmem<SEG> S;
-    deflate_segments<SEG>(A, S);
+    deflate_segments<SEG, L3>(A, S);
 }
+template <bool L3>
 __global__ __launch_bounds__(DF_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_deflate_segments16(DeflateArgs A) {
     __shared__ DfSmem<16384> S;
-    deflate_segments<16384>(A, S);
+    deflate_segments<16384, L3>(A, S);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1475,11 +1522,32 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
 
     if (A.level != 0) {
         // ---- histogram ------------------------------------------------------------------
+        // token words come two blocks ahead (each block's load is a full HBM latency, which the
+        // block's own work does not cover)
+        uint32_t va[4], vb[4];
+        if (DMX_DF_HIST && !RAW) {  // the front kernel's counts
+            const uint32_t* const hs = A.tok + seg * (uint64_t)A.tok_stride + A.tok_stride - kDeflateHistWords;
+            for (int i = lane; i < (int)kDeflateHistWords; i += 64) {
+                const uint32_t x = hs[i];
+                W.freq[2 * i] = x & 0xFFFFu;
+                W.freq[2 * i + 1] = x >> 16;
+            }
+        } else {
         for (int i = lane; i < EM_SYM; i += 64) W.freq[i] = 0;
         wave_sync();
+        if (DMX_EM_PREF) {
+            load4(0, va);
+            if (nblk > 1) load4(1, vb);
+        }
         for (uint32_t blk = 0; blk < nblk; blk++) {
             uint32_t v[4];
-            load4(blk, v);
+            if (DMX_EM_PREF) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) v[j] = va[j], va[j] = vb[j];
+                if (blk + 2 < nblk) load4(blk + 2, vb);
+            } else {
+                load4(blk, v);
+            }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const uint32_t idx = blk * 256 + 4 * lane + j;
@@ -1495,6 +1563,8 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
                 }
             }
         }
+        }
+        wave_sync();
         if (lane == 0) atomicAdd(&W.freq[256], 1u);  // end-of-block
         wave_sync();
         EM_PHASE(A.dbg, seg, 5);
@@ -1618,10 +1688,20 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
             // ---- tokens -------------------------------------------------------------------
             uint32_t cur = 3 + (use_dyn ? hdr_bits : 0u);  // bit position in the window
             uint32_t* dst = slot;                          // next HBM word of the slot
+            if (DMX_EM_PREF) {
+                load4(0, va);
+                if (nblk > 1) load4(1, vb);
+            }
             for (uint32_t blk = 0; blk < nblk; blk++) {
                 uint32_t v[4], nbit[4];
                 uint64_t pat[4];
-                load4(blk, v);
+                if (DMX_EM_PREF) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) v[j] = va[j], va[j] = vb[j];
+                    if (blk + 2 < nblk) load4(blk + 2, vb);
+                } else {
+                    load4(blk, v);
+                }
                 uint32_t mine = 0;
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -1830,17 +1910,21 @@ hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t 
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (seg_bytes == 32768)
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_deflate_segments<32768>, DF_NT, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_deflate_segments<32768, false>, DF_NT, 0);
     else
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_deflate_segments16, DF_NT, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_deflate_segments16<false>, DF_NT, 0);
     const uint64_t fit = (uint64_t)max(ncu, 1) * (uint64_t)max(per, 1);
     const uint32_t grid = (uint32_t)std::min<uint64_t>(A.nseg, fit);  // host min(int, int) would truncate
     if (ev_main0) (void)hipEventRecord(ev_main0, st);
     if (grid && A.level >= 2) {  // match finding + parse -> token words (levels 0-1 have none)
-        if (seg_bytes == 32768)
-            hipLaunchKernelGGL(k_deflate_segments<32768>, dim3(grid), dim3(DF_NT), 0, st, A);
-        else
-            hipLaunchKernelGGL(k_deflate_segments16, dim3(grid), dim3(DF_NT), 0, st, A);
+        const bool l3 = A.level >= 3;
+        if (seg_bytes == 32768) {
+            if (l3) hipLaunchKernelGGL((k_deflate_segments<32768, true>), dim3(grid), dim3(DF_NT), 0, st, A);
+            else hipLaunchKernelGGL((k_deflate_segments<32768, false>), dim3(grid), dim3(DF_NT), 0, st, A);
+        } else {
+            if (l3) hipLaunchKernelGGL(k_deflate_segments16<true>, dim3(grid), dim3(DF_NT), 0, st, A);
+            else hipLaunchKernelGGL(k_deflate_segments16<false>, dim3(grid), dim3(DF_NT), 0, st, A);
+        }
     }
     if (A.nseg) {  // entropy coding and bit packing, one wavefront per segment
         const uint32_t eg = (uint32_t)((A.nseg + EM_NW - 1) / EM_NW);

@@ -26,8 +26,11 @@ struct DeflateArgs {
 
 // Token words per segment of the front kernel: a literal word covers 1-3 input bytes, a match
 // word at least 3, so at most seg / 2 words (one literal between every two 3-byte matches), plus
-// one partial literal word per thread's token range (1024 threads).
-constexpr uint32_t deflate_tok_stride(uint32_t seg) { return seg / 2 + 1024 + 64; }
+// one partial literal word per thread's token range (1024 threads); the last kDeflateHistWords
+// words hold the segment's symbol histogram (320 counts as u16 pairs: lit/len symbols at 0..287,
+// distance symbols at 288..319, end of block not counted), which the emission kernel reads.
+constexpr uint32_t kDeflateHistWords = 160;
+constexpr uint32_t deflate_tok_stride(uint32_t seg) { return seg / 2 + 1024 + 64 + kDeflateHistWords; }
 
 hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t st, hipEvent_t ev0,
                           hipEvent_t ev1);

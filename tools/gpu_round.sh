@@ -20,7 +20,7 @@ fi
 SPECS=${SPECS:-"repeat:2 text:2 random:2"} PH_KINDS=${PH_KINDS:-repeat,text} bash tools/gpu_kstats.sh > gpurun_out/kstats.log 2>&1 || { tail -30 gpurun_out/kstats.log; exit 1; }
 grep -E "^(repeat|text|random|mixed|zeros|bmp) |k_deflate|k_inflate|^deflate|^# " gpurun_out/kstats.log | cut -c1-400
 if [ -n "$AB" ]; then  # A/B of ab/libdmx_<name>.so builds against the in-tree one
-  LIBS="base $AB" TESTS=0 MIB=1024 KINDS=${AB_KINDS:-repeat,text,mixed,bmp} bash tools/gpu_ab.sh > gpurun_out/ab.log 2>&1 || { tail -30 gpurun_out/ab.log; exit 1; }
+  LIBS="base $(ls ab 2>/dev/null | sed -n "s/^libdmx_\(.*\)\.so$/\1/p" | tr "\n" " ")" TESTS=0 MIB=1024 KINDS=${AB_KINDS:-repeat,text,mixed,bmp} bash tools/gpu_ab.sh > gpurun_out/ab.log 2>&1 || { tail -30 gpurun_out/ab.log; exit 1; }
   cat gpurun_out/ab.log
 fi
 if [ -n "$AB3" ]; then  # the same at level 3 (256 MiB)
