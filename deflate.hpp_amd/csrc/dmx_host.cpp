@@ -366,7 +366,10 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         const uint64_t w = bounded ? std::min<uint64_t>(stop & FB_STOP_MASK, nbits) - std::min(pos, nbits) + 4096 : 4096 + 65536;
         return (w + 63) & ~63ull;
     };
-    const uint64_t R = std::max<uint64_t>(256, K), Kcap = K + R;  // room for repair units
+    uint64_t nvirt = 0;
+    for (uint64_t k = 0; k < K; k++) nvirt += vmode[k] == FB_V_VIRTUAL ? 1u : 0u;
+    constexpr uint32_t kPhases = 9;  // exact starts per stray virtual unit (below)
+    const uint64_t R = std::max<uint64_t>(256, K) + kPhases * nvirt, Kcap = K + R;  // repair units
     std::vector<uint64_t> stops(Kcap), tokoff(Kcap + 1);
     starts.resize(Kcap);
     vhdr.resize(Kcap);
@@ -438,6 +441,47 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         return DMX_OK;
     };
     uint64_t rep_used = 0;
+    // Stray virtual units.  In a run of fixed-code literals of one code length (bytes all below
+    // 144: 8-bit codes, or all above: 9 bits) a decode that starts off the token path never gets
+    // back on it, so a virtual unit's warm-up there misses the path for its whole span, and the
+    // chain repairs such a run one unit per round.  A virtual unit whose recorded start is no
+    // decoded unit's end gets exact units at its start bit + 0 .. 8 instead -- the first token
+    // boundary at or past that bit is one of them -- all decoded in one launch, so the walk below
+    // finds every link of the run at once.  (Their token space: a quarter word per bit, plenty
+    // for fixed codes; one that fills up stops softly and is continued by a repair.)
+    // guessed: units whose code state is the gap's first block's (virtual units and these exact
+    // starts) -- its BFINAL bit is a guess, which the walk corrects
+    std::vector<uint8_t> guessed(Kcap, 0);
+    for (uint64_t k = 0; k < K; k++) guessed[k] = vmode[k] == FB_V_VIRTUAL;
+    if (nvirt) {
+        std::vector<uint64_t> ends;
+        ends.reserve(K);
+        for (uint64_t k = 0; k < K; k++)
+            if (!(units[k].flags & SEGF_ERRORS)) ends.push_back(units[k].end);
+        std::sort(ends.begin(), ends.end());
+        const uint64_t k0 = Ku;
+        for (uint64_t j = 0; j < K; j++) {
+            if (vmode[j] != FB_V_VIRTUAL) continue;
+            if (!(units[j].flags & SEGF_ERRORS) && std::binary_search(ends.begin(), ends.end(), units[j].start)) continue;
+            for (uint32_t o = 0; o < kPhases && Ku < Kcap; o++) {
+                const uint64_t e = starts[j] + o;
+                if (e >= nbits) break;
+                starts[Ku] = e;
+                vmode[Ku] = FB_V_EXACT;
+                guessed[Ku] = 1;
+                vhdr[Ku] = vhdr[j];
+                stops[Ku] = stops[j];
+                const uint64_t span = (stops[j] & FB_STOP_MASK) > e ? std::min<uint64_t>(stops[j] & FB_STOP_MASK, nbits) - e : 0;
+                const uint64_t w = std::min<uint64_t>(words_of(e, stops[j]), ((span / 4 + 4096) + 63) & ~63ull);
+                if (rep_used + w > rep_words) break;
+                tokoff[Ku + 1] = tokoff[Ku] + w;
+                rep_used += w;
+                Ku++;
+            }
+        }
+        if (Ku > k0 && (upload(k0, Ku - k0) != DMX_OK || decode(k0, Ku - k0) != DMX_OK)) return DMX_ERR_DEVICE;
+        if (fb_debug) std::fprintf(stderr, "dmx fb: %llu exact starts for stray virtual units\n", (unsigned long long)(Ku - k0));
+    }
     for (int round = 0;; round++) {
         std::vector<std::pair<uint64_t, uint32_t>> by;  // (recorded start, unit) of units decoded without error
         by.reserve(Ku);
@@ -467,7 +511,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
             }
             uint64_t state = u.hdr;
             if (state != FB_AT_HEADER) {
-                const bool own = vmode[k] != FB_V_VIRTUAL || (u.flags & SEGF_CROSSED);
+                const bool own = !guessed[k] || (u.flags & SEGF_CROSSED);
                 if (!own) state = (state & ~FB_STATE_FINAL) | (final_in_force ? FB_STATE_FINAL : 0ull);
                 final_in_force = (state & FB_STATE_FINAL) != 0;
             }
@@ -478,7 +522,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
                 // said not final), and is redone from here with the final state
                 const FbUnit& v = units[it->second];
                 const bool in_final = state != FB_AT_HEADER && (state & FB_STATE_FINAL);
-                if (!(in_final && vmode[it->second] == FB_V_VIRTUAL &&
+                if (!(in_final && guessed[it->second] &&
                       ((v.flags & SEGF_CROSSED) || v.hdr == FB_AT_HEADER))) {
                     k = it->second;
                     continue;
