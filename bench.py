@@ -54,6 +54,16 @@ REF_NOTES = {"text": "reference L2 stream is lossy (SURVEY A-1)",
              "bmp": "reference L2 stream is invalid (SURVEY A-3)"}
 REF_RATIO_L3_TEXT = 2.5741  # reference L3 on the 1 MiB text prefix
 PROFILE_TAG = "r04"  # tools/profile_all.sh writes profiles/<tag>_kstats_*.csv and traffic.json
+
+
+def profile_path(name):
+    """profiles/<tag>_<name>, or the newest earlier round's file of that name when this round has
+    none yet (the record then names the round its evidence comes from)."""
+    for tag in (PROFILE_TAG, "r03"):
+        rel = f"profiles/{tag}_{name}"
+        if os.path.exists(os.path.join(ROOT, rel)):
+            return rel
+    return None
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
 
 
@@ -327,7 +337,7 @@ def corpus_record(run, kind, level, steps):
             "roofline_frac": {"deflate": round(s["frac_def"], 5), "inflate": round(s["frac_inf"], 5)},
             "traffic": {"deflate": traffic_of(f"{kind}:{n}:{level}:", DEF_KERNELS),
                         "inflate": traffic_of(f"{kind}:{n}:{level}:", inf_k)},
-            "profile": f"profiles/{PROFILE_TAG}_kstats_{kind}_L{level}.csv"}
+            "profile": profile_path(f"kstats_{kind}_L{level}.csv")}
 
 
 def c3_record(torch, ctx, dev, stream):
@@ -358,7 +368,7 @@ def c3_record(torch, ctx, dev, stream):
                      "bit_exact": ok}
     res["zlib1"]["traffic"] = traffic_of("c3_zlib1:", ["k_fb_scan", "k_fb_compact", "k_fb_pdecode", "k_fb_units",
                                                        "k_fb_win_init", "k_fb_win_jump", "k_fb_final"])
-    res["zlib1"]["profile"] = f"profiles/{PROFILE_TAG}_kstats_c3_zlib1.csv"
+    res["zlib1"]["profile"] = profile_path("kstats_c3_zlib1.csv")
     return res
 
 
