@@ -9,11 +9,11 @@ if [ -n "$P5PROBE" ]; then
   grep -E "^single|chain breaks|units:|repair" gpurun_out/p5single.log | head -60
   ok_or_fail $rc || exit 1
 fi
-timeout -k 10 600 python -u -m pytest tests/test_gpu_foreign.py -v -s --timeout 300 --timeout-method thread > gpurun_out/p5v.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_path5_foreign.py -v -s --timeout 300 --timeout-method thread > gpurun_out/p5v.log 2>&1; rc=$?
 grep -E "GPU |PASSED|FAILED|passed|failed|Error" gpurun_out/p5v.log | tail -16
 ok_or_fail $rc || exit 1
 if [ "$1" != quick ]; then
-  timeout -k 10 900 python -u -m pytest tests/ -m gpu -q --timeout 300 --timeout-method thread --ignore=tests/test_gpu_foreign.py > gpurun_out/gpu_tests.log 2>&1; rc=$?
+  timeout -k 10 900 python -u -m pytest tests/ -m gpu -q --timeout 300 --timeout-method thread --ignore=tests/test_gpu_path5_foreign.py > gpurun_out/gpu_tests.log 2>&1; rc=$?
   grep -E "FAILED|passed|failed" gpurun_out/gpu_tests.log | tail -12
   ok_or_fail $rc || exit 1
 fi
