@@ -79,3 +79,16 @@ def test_struct_layout_matches_header(tmp_path, cname, pyname):
     body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
     cfields = re.findall(r"\b([a-z_][a-z0-9_]*)\s*;", body)
     assert cfields == fields
+
+
+def test_config_defaults_and_dev_controls():
+    """dmx_config_default: one device, 32 KiB segments, no flags, the developer controls off; the
+    Python mirror maps its developer keywords onto those fields (no device needed)."""
+    import ctypes
+    cfg = dmx.Config()
+    dmx.lib().dmx_config_default(ctypes.byref(cfg))
+    assert (cfg.device, cfg.segment_bytes, cfg.flags, cfg.n_gpus) == (-1, 32768, 0, 1)
+    assert (cfg.dev_inflate_pass, cfg.dev_heavy_bytes) == (0, 0)
+    assert dmx.DMX_CFG_FB_SERIAL == 2 and dmx.DMX_CFG_RFC_STRICT == 1
+    hdr = open(os.path.join(ROOT, "include", "dmx.h")).read()
+    assert re.search(r"#define DMX_CFG_FB_SERIAL 2u", hdr)
