@@ -73,13 +73,15 @@ struct dmx_ctx {
     // block-parallel path (path 5): scan counts / hits / offsets, hit list, unit starts, token
     // offsets and words, unit records, chain (unit index, offset, size), 16-bit image
     DevBuf fbc, fbh, fbo, fbl, fbs, fbt, fbk, fbu, fbch, fbco, fbcs, fbimg, fbstop, fbwin, fbopen, fbp32;
-    DevBuf fbvm, fbvh;  // per-unit start mode and code state (virtual / repair units)
+    DevBuf fbvm, fbvh;  // per-unit start mode and code state (region and repair units)
+    DevBuf fbreg, fbJ, fbvis;  // fixed-code regions: {E, T, first super block} + super-block regions, jumps, visits
     DevBuf ck;  // checksum scratch (checksum.hip) + the 4-byte result at its start
     bool timing = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t ev_df = nullptr;          // end of the last deflate's work (its scratch is reused)
     bool df_pending = false;
     dmx_stats stats{};
+    uint64_t last_end = 0;               // the last inflate: stream byte just past its final block
     std::vector<dmx_ctx*> subs;          // n_gpus > 1: one context per shard / piece
 };
 
@@ -304,88 +306,73 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     }
     // units: bit 0, then every hit (sorted: chunks in order, lanes in order within a chunk);
     // dynamic-header hits are "strong" (practically never false), stored-header hits "weak".
-    // A gap of more than kVirtGap bits between two of them is a run of blocks the scan cannot
-    // split (fixed-code blocks -- zlib's Z_FIXED, the reference's own level-1 chunks -- or one
-    // huge block): virtual units start every kVirtStep bits inside it, each decoded from a
-    // warm-up before its start bit under the code of the gap's first block (FB_V_VIRTUAL).  The
-    // chain walk below verifies every link; a unit whose guess or warm-up failed is redone from
-    // its predecessor's exact end (FB_V_EXACT repair rounds).
+    // A gap of more than kRegionGap bits between two strong starts is a run of blocks the scan
+    // cannot split (fixed-code blocks -- zlib's Z_FIXED, the reference's own level-1/2 chunks --
+    // or one huge block).  Its head unit decodes only a dynamic first block (and what follows
+    // it up to the first far fixed-code header, FB_STOP_REGION); from where it stops, E, to the
+    // next strong start T the region map (k_fb_smap / k_fb_swalk) finds the exact token path,
+    // and one unit per 2^18 bits starts exactly on it.  The chain walk below verifies every link
+    // (end bit and code state); a break gets a repair unit that starts exactly there.
     constexpr uint64_t kStored = 1ull << 62;
-    constexpr uint64_t kVirtStep = 1ull << 18, kVirtGap = 4 * kVirtStep;
-    // A region of fixed-code literals below 144 (8-bit codes only) never re-synchronises: every
-    // virtual unit inside it that missed the token path stays off it, and such a run of units is
-    // repaired one per round, each round one lane-parallel launch (~0.3 ms)
+    const uint64_t kSuper = fb_region_super_bits();
+    const uint64_t kRegionGap = kSuper + kSuper / 2;
     constexpr int kRepairRounds = 48;
     const uint64_t nbits = 8ull * n;
     std::vector<uint64_t> starts, vhdr;
     std::vector<uint8_t> strong, vmode;
-    {
-        std::vector<uint64_t> hs{0};
-        std::vector<uint8_t> hstr{1};
-        for (uint64_t h : hits) {
-            const uint64_t b = h & ~kStored;
-            if (b > hs.back()) {
-                hs.push_back(b);
-                hstr.push_back((h & kStored) ? 0 : 1);
-            }
-        }
-        for (size_t i = 0; i < hs.size(); i++) {
-            starts.push_back(hs[i]);
-            strong.push_back(hstr[i]);
-            vmode.push_back(FB_V_HEADER);
-            vhdr.push_back(0);
-            const uint64_t next = i + 1 < hs.size() ? hs[i + 1] : nbits;
-            if (next - hs[i] > kVirtGap)
-                for (uint64_t b = hs[i] + kVirtStep; b + kVirtStep / 2 < next; b += kVirtStep) {
-                    starts.push_back(b);
-                    strong.push_back(0);
-                    vmode.push_back(FB_V_VIRTUAL);
-                    vhdr.push_back(hs[i]);
-                }
+    starts.push_back(0);
+    strong.push_back(1);
+    for (uint64_t h : hits) {
+        const uint64_t b = h & ~kStored;
+        if (b > starts.back()) {
+            starts.push_back(b);
+            strong.push_back((h & kStored) ? 0 : 1);
         }
     }
     const uint64_t K = starts.size();
-    // stops: a unit stops after passing the next strong start (or on landing on any start); when
-    // the next unit is virtual, at the first token boundary at or past its start bit (soft).
-    // Token words: at most one per bit up to where it can stop, plus room for the block that
-    // crosses that start; a weak unit with a hard stop (a stored block -- two words -- then
-    // possibly fixed-code blocks up to the next dynamic one) gets 64 Ki words, and overflowing
-    // them sends the stream to the serial decoder.  16-B groups.
-    auto next_strong_after = [&](uint64_t pos) -> uint64_t {  // first scanned strong start > pos
-        for (uint64_t k = (uint64_t)(std::upper_bound(starts.begin(), starts.begin() + K, pos) - starts.begin()); k < K; k++)
-            if (strong[k]) return starts[k];
-        return FB_STOP_MASK;
-    };
-    auto stop_of = [&](uint64_t pos, bool weak) -> uint64_t {  // the stop of a unit starting at pos
-        const uint64_t k = (uint64_t)(std::upper_bound(starts.begin(), starts.begin() + K, pos) - starts.begin());
-        const uint64_t st = (k < K && vmode[k] == FB_V_VIRTUAL) ? (starts[k] | FB_STOP_SOFT) : next_strong_after(pos);
-        return st | (weak ? FB_STOP_WEAK : 0ull);
-    };
-    auto words_of = [&](uint64_t pos, uint64_t stop) -> uint64_t {
-        const bool bounded = !(stop & FB_STOP_WEAK) || (stop & FB_STOP_SOFT);
-        const uint64_t w = bounded ? std::min<uint64_t>(stop & FB_STOP_MASK, nbits) - std::min(pos, nbits) + 4096 : 4096 + 65536;
-        return (w + 63) & ~63ull;
-    };
-    uint64_t nvirt = 0;
-    for (uint64_t k = 0; k < K; k++) nvirt += vmode[k] == FB_V_VIRTUAL ? 1u : 0u;
-    constexpr uint32_t kPhases = 9;  // exact starts per stray virtual unit (below)
-    const uint64_t R = std::max<uint64_t>(256, K) + kPhases * nvirt, Kcap = K + R;  // repair units
-    std::vector<uint64_t> stops(Kcap), tokoff(Kcap + 1);
-    starts.resize(Kcap);
-    vhdr.resize(Kcap);
-    vmode.resize(Kcap);
+    std::vector<uint64_t> stops(K);
     {
         uint64_t next_strong = FB_STOP_MASK;
         for (uint64_t k = K; k-- > 0;) {
-            if (k + 1 < K && vmode[k + 1] == FB_V_VIRTUAL) stops[k] = starts[k + 1] | FB_STOP_SOFT;
-            else stops[k] = next_strong;
-            if (vmode[k] == FB_V_HEADER && !strong[k]) stops[k] |= FB_STOP_WEAK;
+            stops[k] = next_strong;
+            if (!strong[k]) stops[k] |= FB_STOP_WEAK;
+            else if (std::min(next_strong, nbits) - starts[k] > kRegionGap) stops[k] |= FB_STOP_REGION;
             if (strong[k]) next_strong = starts[k];
         }
     }
+    // Token words: at most one per bit up to where a unit can stop, plus room for the block
+    // that crosses its stop; a weak unit with a hard stop (a stored block -- two words -- then
+    // possibly fixed-code blocks up to the next dynamic one) gets 64 Ki words; a region head at
+    // most its staged first block.  A unit that fills its space stops softly and a repair unit
+    // continues it.  Inside a fixed-code region a token word covers at least 7 bits (fixed codes
+    // are 7-9 bits, three literals per word), so a third of a word per bit.  16-B groups.
+    auto words_of = [&](uint64_t pos, uint64_t stop) -> uint64_t {
+        const uint64_t s = std::min<uint64_t>(stop & FB_STOP_MASK, nbits), p = std::min(pos, nbits);
+        uint64_t w = 4096 + 65536;
+        if (stop & FB_STOP_REGION) w = std::min<uint64_t>(s - p, 458752 + 65536) + 4096;
+        else if (!(stop & FB_STOP_WEAK)) w = s - p + 4096;
+        return (w + 63) & ~63ull;
+    };
+    auto region_words = [](uint64_t span) -> uint64_t { return ((span / 3 + 4096) + 63) & ~63ull; };
+    // region budget: every long gap could become one region of units, each with a repair
+    uint64_t reg_budget = 0, reg_units_max = 0;
+    for (uint64_t k = 0; k < K; k++)
+        if (stops[k] & FB_STOP_REGION) {
+            const uint64_t span = std::min(stops[k] & FB_STOP_MASK, nbits) - starts[k];
+            const uint64_t nu = span / kSuper + 2;
+            reg_units_max += nu;
+            reg_budget += span / 3 + nu * (4096 + 64);
+        }
+    const uint64_t R = 2 * std::max<uint64_t>(256, K + reg_units_max);  // repair units
+    const uint64_t Kcap = K + reg_units_max + R;
+    std::vector<uint64_t> tokoff(Kcap + 1);
+    starts.resize(Kcap);
+    vhdr.assign(Kcap, 0);
+    vmode.assign(Kcap, FB_V_HEADER);
+    stops.resize(Kcap);
     tokoff[0] = 0;
     for (uint64_t k = 0; k < K; k++) tokoff[k + 1] = tokoff[k] + words_of(starts[k], stops[k]);
-    const uint64_t rep_words = std::min<uint64_t>(tokoff[K] + 4096 * R, 1ull << 28);  // repairs' tokens
+    const uint64_t rep_words = std::min<uint64_t>(tokoff[K] + 2 * reg_budget + 4096 * R, 1ull << 29);
     if (!c->fbs.ensure(Kcap * 8) || !c->fbt.ensure((Kcap + 1) * 8) || !c->fbk.ensure((tokoff[K] + rep_words) * 4) ||
         !c->fbu.ensure(Kcap * sizeof(FbUnit)) || !c->fbstop.ensure(Kcap * 8) || !c->fbvm.ensure(Kcap) ||
         !c->fbvh.ensure(Kcap * 8))
@@ -425,14 +412,116 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
                      "stream-start copy %u\n",
                      (unsigned long long)K, hs[0], hs[1], hs[2], hs[3], hs[4], hs[5], hs[6], hs[7], hs[8], hs[9]);
     }
-    // chain from bit 0: each unit must end exactly where the next one on the chain starts (its
-    // recorded start: a virtual unit's is the token boundary its warm-up found).  Every break --
-    // an end where no decoded unit starts -- gets a repair unit that starts exactly there, in
-    // the code state the unit before it ended in; the walk goes on optimistically past a break
-    // (from the next unit that starts after it), so one round repairs them all.
+    uint64_t Ku = K;
+    uint64_t rep_used = 0;
+    // Sorted list of the starts a repair unit stops at: the scanned ones (a weak start inside a
+    // region is superseded by the region's units) and the region units' (soft: inside a block,
+    // except the region head E, a block header).
+    struct Prim {
+        uint64_t pos;
+        uint8_t kind;  // 0 strong / region head, 1 weak, 2 soft
+    };
+    std::vector<Prim> prim;
+    // ---- fixed-code regions ----
+    {
+        struct Reg {
+            uint64_t E, T, sb0, nsb;
+        };
+        std::vector<Reg> regs;
+        uint64_t nsb = 0;
+        for (uint64_t k = 0; k < K; k++) {
+            if (!(stops[k] & FB_STOP_REGION)) continue;
+            const FbUnit& u = units[k];
+            if ((u.flags & (SEGF_ERRORS | SEGF_FINAL)) || u.hdr != FB_AT_HEADER) continue;
+            const uint64_t T = std::min(stops[k] & FB_STOP_MASK, nbits);
+            if (u.end >= T || T - u.end <= kSuper) continue;  // a repair unit takes the rest
+            const uint64_t m = (T - u.end + kSuper - 1) / kSuper;
+            regs.push_back({u.end, T, nsb, m});
+            nsb += m;
+        }
+        std::vector<uint8_t> in_region(K, 0);
+        if (!regs.empty()) {
+            const uint64_t nreg = regs.size();
+            if (!c->fbreg.ensure(nreg * 24 + nsb * 4) || !c->fbJ.ensure(nsb * (uint64_t)fb_region_nodes() * 4) ||
+                !c->fbvis.ensure((nsb + nreg) * 4))
+                return DMX_OK;
+            std::vector<uint64_t> hreg(3 * nreg);
+            std::vector<uint32_t> sbreg(nsb);
+            for (uint64_t r = 0; r < nreg; r++) {
+                hreg[3 * r] = regs[r].E;
+                hreg[3 * r + 1] = regs[r].T;
+                hreg[3 * r + 2] = regs[r].sb0;
+                for (uint64_t j = 0; j < regs[r].nsb; j++) sbreg[regs[r].sb0 + j] = (uint32_t)r;
+            }
+            uint64_t* dreg = c->fbreg.as<uint64_t>();
+            uint32_t* dsbr = reinterpret_cast<uint32_t*>(dreg + 3 * nreg);
+            uint32_t* dvis = c->fbvis.as<uint32_t>();
+            HIPCHK(hipMemcpyAsync(dreg, hreg.data(), nreg * 24, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(dsbr, sbreg.data(), nsb * 4, hipMemcpyHostToDevice, st));
+            HIPCHK(launch_fb_regions(words, misalign, n, dreg, (uint32_t)nreg, dsbr, nsb, c->fbJ.as<uint32_t>(), dvis,
+                                     dvis + nsb, st));
+            std::vector<uint32_t> vis(nsb + nreg);
+            HIPCHK(hipMemcpyAsync(vis.data(), dvis, (nsb + nreg) * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            const uint64_t ch = fb_region_chunk_bits(), k0 = Ku;
+            for (uint64_t r = 0; r < nreg; r++) {
+                const uint32_t rs = vis[nsb + r];
+                if (fb_debug)
+                    std::fprintf(stderr, "dmx fb: region %llu: bits %llu..%llu, %llu super blocks, walk %s\n",
+                                 (unsigned long long)r, (unsigned long long)regs[r].E, (unsigned long long)regs[r].T,
+                                 (unsigned long long)regs[r].nsb,
+                                 rs == FB_REGION_END ? "end" : rs == FB_REGION_LINK ? "link" : "fail");
+                // no token path through the region: the serial decoder reports what is wrong
+                if (rs != FB_REGION_END && rs != FB_REGION_LINK) return DMX_OK;
+                const uint64_t first = Ku;
+                for (uint64_t j = 0; j < regs[r].nsb; j++) {
+                    const uint32_t v = vis[regs[r].sb0 + j];
+                    if (v == ~0u) continue;
+                    if (Ku >= Kcap) return DMX_OK;
+                    const bool head = Ku == first;
+                    starts[Ku] = regs[r].E + (uint64_t)(v >> 6) * ch + (v & 31u);
+                    vmode[Ku] = head ? FB_V_HEADER : FB_V_EXACT;
+                    vhdr[Ku] = head ? 0 : (FB_STATE_FIXED | ((v >> 5) & 1u ? FB_STATE_FINAL : 0ull));
+                    Ku++;
+                }
+                for (uint64_t k = first; k < Ku; k++) {
+                    stops[k] = k + 1 < Ku ? (starts[k + 1] | FB_STOP_SOFT) : regs[r].T;
+                    const uint64_t w = region_words(std::min(stops[k] & FB_STOP_MASK, nbits) - starts[k]);
+                    if (rep_used + w > rep_words) return DMX_OK;
+                    tokoff[k + 1] = tokoff[k] + w;
+                    rep_used += w;
+                    prim.push_back({starts[k], (uint8_t)(k == first ? 0 : 2)});
+                }
+                // weak starts inside the region: superseded
+                for (uint64_t k = (uint64_t)(std::upper_bound(starts.begin(), starts.begin() + K, regs[r].E) - starts.begin());
+                     k < K && starts[k] < regs[r].T; k++)
+                    in_region[k] = 1;
+            }
+            if (Ku > k0 && (upload(k0, Ku - k0) != DMX_OK || decode(k0, Ku - k0) != DMX_OK)) return DMX_ERR_DEVICE;
+        }
+        for (uint64_t k = 0; k < K; k++)
+            if (!in_region[k]) prim.push_back({starts[k], (uint8_t)(strong[k] ? 0 : 1)});
+        std::sort(prim.begin(), prim.end(), [](const Prim& a, const Prim& b) { return a.pos < b.pos; });
+    }
+    // the stop of a repair unit at pos: a soft stop at the next region unit, else the next
+    // strong start (or region head)
+    auto stop_of = [&](uint64_t pos) -> uint64_t {
+        auto it = std::upper_bound(prim.begin(), prim.end(), pos, [](uint64_t p, const Prim& q) { return p < q.pos; });
+        if (it != prim.end() && it->kind == 2) return it->pos | FB_STOP_SOFT;
+        for (; it != prim.end(); ++it)
+            if (it->kind != 1) return it->pos;
+        return FB_STOP_MASK;
+    };
+    // the code state a unit assumes at its start: FB_AT_HEADER, or the code in force
+    auto expects = [&](uint64_t k) -> uint64_t { return vmode[k] == FB_V_HEADER ? FB_AT_HEADER : vhdr[k]; };
+    // chain from bit 0: each unit must end exactly where the next one on the chain starts, in
+    // the code state that one assumes (a block header, or the code in force and its BFINAL bit).
+    // Every break -- an end where no such unit starts -- gets a repair unit that starts exactly
+    // there in that state; the walk goes on optimistically past a break (from the next unit in
+    // start order), so one round repairs all the breaks it can see.
     std::vector<uint32_t> chain;
     std::vector<uint64_t> coffs, csizes;
-    uint64_t total = 0, Ku = K;
+    uint64_t total = 0;
     auto chain_break = [&](const char* why, uint64_t k) {
         if (fb_debug)
             std::fprintf(stderr, "dmx fb: chain breaks at unit %llu of %llu (%s): start %llu end %llu size %llu flags %u\n",
@@ -440,50 +529,9 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
                          (unsigned long long)units[k].end, (unsigned long long)units[k].size, units[k].flags);
         return DMX_OK;
     };
-    uint64_t rep_used = 0;
-    // Stray virtual units.  In a run of fixed-code literals of one code length (bytes all below
-    // 144: 8-bit codes, or all above: 9 bits) a decode that starts off the token path never gets
-    // back on it, so a virtual unit's warm-up there misses the path for its whole span, and the
-    // chain repairs such a run one unit per round.  A virtual unit whose recorded start is no
-    // decoded unit's end gets exact units at its start bit + 0 .. 8 instead -- the first token
-    // boundary at or past that bit is one of them -- all decoded in one launch, so the walk below
-    // finds every link of the run at once.  (Their token space: a quarter word per bit, plenty
-    // for fixed codes; one that fills up stops softly and is continued by a repair.)
-    // guessed: units whose code state is the gap's first block's (virtual units and these exact
-    // starts) -- its BFINAL bit is a guess, which the walk corrects
-    std::vector<uint8_t> guessed(Kcap, 0);
-    for (uint64_t k = 0; k < K; k++) guessed[k] = vmode[k] == FB_V_VIRTUAL;
-    if (nvirt) {
-        std::vector<uint64_t> ends;
-        ends.reserve(K);
-        for (uint64_t k = 0; k < K; k++)
-            if (!(units[k].flags & SEGF_ERRORS)) ends.push_back(units[k].end);
-        std::sort(ends.begin(), ends.end());
-        const uint64_t k0 = Ku;
-        for (uint64_t j = 0; j < K; j++) {
-            if (vmode[j] != FB_V_VIRTUAL) continue;
-            if (!(units[j].flags & SEGF_ERRORS) && std::binary_search(ends.begin(), ends.end(), units[j].start)) continue;
-            for (uint32_t o = 0; o < kPhases && Ku < Kcap; o++) {
-                const uint64_t e = starts[j] + o;
-                if (e >= nbits) break;
-                starts[Ku] = e;
-                vmode[Ku] = FB_V_EXACT;
-                guessed[Ku] = 1;
-                vhdr[Ku] = vhdr[j];
-                stops[Ku] = stops[j];
-                const uint64_t span = (stops[j] & FB_STOP_MASK) > e ? std::min<uint64_t>(stops[j] & FB_STOP_MASK, nbits) - e : 0;
-                const uint64_t w = std::min<uint64_t>(words_of(e, stops[j]), ((span / 4 + 4096) + 63) & ~63ull);
-                if (rep_used + w > rep_words) break;
-                tokoff[Ku + 1] = tokoff[Ku] + w;
-                rep_used += w;
-                Ku++;
-            }
-        }
-        if (Ku > k0 && (upload(k0, Ku - k0) != DMX_OK || decode(k0, Ku - k0) != DMX_OK)) return DMX_ERR_DEVICE;
-        if (fb_debug) std::fprintf(stderr, "dmx fb: %llu exact starts for stray virtual units\n", (unsigned long long)(Ku - k0));
-    }
+    std::vector<std::pair<uint64_t, uint64_t>> repaired;  // (end bit, state) already given a repair unit
     for (int round = 0;; round++) {
-        std::vector<std::pair<uint64_t, uint32_t>> by;  // (recorded start, unit) of units decoded without error
+        std::vector<std::pair<uint64_t, uint32_t>> by;  // (start, unit) of units decoded without error
         by.reserve(Ku);
         for (uint64_t k = 0; k < Ku; k++)
             if (!(units[k].flags & SEGF_ERRORS)) by.emplace_back(units[k].start, (uint32_t)k);
@@ -496,9 +544,6 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         bool fin = false;
         if (units[0].flags & SEGF_ERRORS) return chain_break("unit error", 0);
         uint64_t k = 0;
-        // the BFINAL bit of the block in force where the walk stands: a virtual unit that passed
-        // no block header only guessed it (not final), its predecessor's reading holds
-        bool final_in_force = false;
         for (;;) {
             const FbUnit& u = units[k];
             chain.push_back((uint32_t)k);
@@ -509,31 +554,21 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
                 fin = true;
                 break;
             }
-            uint64_t state = u.hdr;
-            if (state != FB_AT_HEADER) {
-                const bool own = !guessed[k] || (u.flags & SEGF_CROSSED);
-                if (!own) state = (state & ~FB_STATE_FINAL) | (final_in_force ? FB_STATE_FINAL : 0ull);
-                final_in_force = (state & FB_STATE_FINAL) != 0;
-            }
-            auto it = std::lower_bound(by.begin(), by.end(), std::make_pair(u.end, 0u));
-            if (it != by.end() && it->first == u.end && it->second != k) {
-                // inside a final block a virtual unit is right only up to a soft stop: one that
-                // passed a header or ended at one read past the final end of block (its guess
-                // said not final), and is redone from here with the final state
-                const FbUnit& v = units[it->second];
-                const bool in_final = state != FB_AT_HEADER && (state & FB_STATE_FINAL);
-                if (!(in_final && guessed[it->second] &&
-                      ((v.flags & SEGF_CROSSED) || v.hdr == FB_AT_HEADER))) {
-                    k = it->second;
-                    continue;
-                }
+            const uint64_t state = u.hdr;
+            // (several units may start there in that state -- a scanned one, a region unit, a
+            // repair: all decode the same tokens, the one that reaches farthest is taken)
+            uint64_t best = ~0ull;
+            for (auto it = std::lower_bound(by.begin(), by.end(), std::make_pair(u.end, 0u));
+                 it != by.end() && it->first == u.end; ++it)
+                if (it->second != k && expects(it->second) == state &&
+                    (best == ~0ull || units[it->second].end >= units[best].end))
+                    best = it->second;
+            if (best != ~0ull) {
+                k = best;
+                continue;
             }
             breaks.emplace_back(u.end, state);
-            // (optimistic: on with the unit after this one in start order, even one that starts
-            // before the break -- a virtual unit whose warm-up missed the token path records a
-            // start off it, but it re-synchronises within its span, so its end is on the path:
-            // the break there gets its repair in this same round, and a run of such units costs
-            // one round instead of one round each)
+            // (optimistic: on with the unit after this one in start order)
             auto self = std::lower_bound(by.begin(), by.end(), std::make_pair(u.start, (uint32_t)k));
             if (self == by.end() || self->second != k || ++self == by.end()) break;
             k = self->second;
@@ -541,20 +576,28 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         if (fin && breaks.empty()) break;
         if (breaks.empty() || round == kRepairRounds || Ku + breaks.size() > Kcap)
             return chain_break(fin ? "repairs exhausted" : "no final block", chain.back());
+        std::sort(breaks.begin(), breaks.end());
+        breaks.erase(std::unique(breaks.begin(), breaks.end()), breaks.end());
         // repair units, appended at [Ku, Ku + breaks)
         const uint64_t k0 = Ku;
         for (const auto& br : breaks) {
+            // a repair that was already made there failed: the serial decoder reports why
+            if (std::binary_search(repaired.begin(), repaired.end(), br))
+                return chain_break("repair failed", chain.back());
             const uint64_t e = br.first;
             starts[Ku] = e;
             vmode[Ku] = br.second == FB_AT_HEADER ? FB_V_HEADER : FB_V_EXACT;
             vhdr[Ku] = br.second == FB_AT_HEADER ? 0 : br.second;
-            stops[Ku] = stop_of(e, false);
-            const uint64_t w = words_of(e, stops[Ku]);
+            stops[Ku] = stop_of(e);
+            const uint64_t w = (stops[Ku] & FB_STOP_SOFT) ? region_words((stops[Ku] & FB_STOP_MASK) - std::min(e, nbits))
+                                                          : words_of(e, stops[Ku]);
             if (rep_used + w > rep_words) return chain_break("repair token space", chain.back());
             tokoff[Ku + 1] = tokoff[Ku] + w;
             rep_used += w;
             Ku++;
         }
+        repaired.insert(repaired.end(), breaks.begin(), breaks.end());
+        std::sort(repaired.begin(), repaired.end());
         if (upload(k0, Ku - k0) != DMX_OK || decode(k0, Ku - k0) != DMX_OK) return DMX_ERR_DEVICE;
         if (fb_debug)
             std::fprintf(stderr, "dmx fb: repair round %d: %llu units\n", round, (unsigned long long)(Ku - k0));
@@ -602,6 +645,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         return DMX_OK;
     }
     c->stats.segments = nch;
+    c->last_end = (units[chain.back()].end + 7) / 8;
     if (dev_out) *dev_out = out;
     return DMX_OK;
 }
@@ -722,7 +766,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     if (!parallel_ok) np = 0;
     // no marker in a large stream: not libdmx's segment layout, the block-parallel path next
     if (ncand == 1 && n > 65536 && path_env == -1) np = 0;
-    if (path_env == 5) np = 0;
+    if (path_env == 5 || path_env == 7) np = 0;  // 7: the serial decoder alone
     // the plan's passes into A.out / A.cap; returns the last validation result
     auto run_plan = [&](InflateResult& r) -> int {
         r.status = 2;
@@ -785,6 +829,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     c->stats.in_bytes = n;
     if (r.status == 0) {
         end_timing(c, st);
+        c->last_end = r.end_byte;
         c->stats.path = lead_mode == 4 ? 4 : lead_mode >= 2 ? 3 : lead_mode;
         c->stats.out_bytes = r.total;
         *total_out = r.total;
@@ -866,6 +911,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
             if (c->timing) (void)hipEventRecord(c->ev[2], st);
             HIPCHK(hipStreamSynchronize(st));
             end_timing(c, st);
+            c->last_end = h[chain.back()].end_byte;
             c->stats.path = 4;
             c->stats.out_bytes = tot;
             *total_out = tot;
@@ -887,26 +933,39 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
             return rc;
         }
     }
-    // serial path: size pass, then write pass
+    // serial path: one pass into the caller's buffer, or into c->out sized generously (bytes
+    // past the capacity are counted, not written); a second pass only when that did not fit
     c->stats.path = 2;
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
-    HIPCHK(launch_inflate_serial(A, 1, &ds->res, st));
-    HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (r.status != 0) return r.status;
-    *total_out = r.total;
     if (!fixed_out) {
-        if (!c->out.ensure(r.total ? r.total : 1)) return DMX_ERR_NOMEM;
+        size_t freeb = 0, totb = 0;
+        if (hipMemGetInfo(&freeb, &totb) != hipSuccess) freeb = 0;
+        const uint64_t guess = std::min<uint64_t>(64ull * n + (16ull << 20), freeb / 4);
+        if (c->out.cap < guess && !c->out.ensure(guess)) (void)c->out.ensure(1);
         A.out = c->out.as<uint8_t>();
-        A.cap = c->out.cap;
-    } else if (r.total > cap) {
-        return DMX_ERR_CAPACITY;
+        A.cap = c->out.p ? c->out.cap : 0;
+    } else {
+        A.out = fixed_out;
+        A.cap = cap;
     }
     HIPCHK(launch_inflate_serial(A, 0, &ds->res, st));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (r.status != 0) return r.status;
+    if (r.total > A.cap) {
+        if (fixed_out) return DMX_ERR_CAPACITY;
+        if (!c->out.ensure(r.total)) return DMX_ERR_NOMEM;
+        A.out = c->out.as<uint8_t>();
+        A.cap = c->out.cap;
+        HIPCHK(launch_inflate_serial(A, 0, &ds->res, st));
+        if (c->timing) (void)hipEventRecord(c->ev[2], st);
+        HIPCHK(hipMemcpyAsync(&r, &ds->res, sizeof r, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
     end_timing(c, st);
+    *total_out = r.total;
+    c->last_end = r.end_byte;
     c->stats.out_bytes = r.total;
     if (dev_out) *dev_out = A.out;
     return r.status;
@@ -1119,8 +1178,12 @@ int inflate_multi(dmx_ctx* c, const uint8_t* in, size_t n, uint8_t* out, size_t 
             rc[g] = DMX_ERR_DEVICE;
             return;
         }
+        s->last_end = 0;
         rc[g] = inflate_device_locked(s, s->in.as<uint8_t>(), m + (closes ? 2 : 0), nullptr, 0, &len[g], &dev[g],
                                       s->stream, g ? DMX_IFLAG_PIECE : 0u);
+        // a piece must end at its appended empty final block: a BFINAL block before it (two
+        // streams concatenated: the reference stops at the first) would drop the piece's rest
+        if (rc[g] == DMX_OK && closes && s->last_end != m + 2) rc[g] = DMX_ERR_DATA;
     });
     for (size_t g = 0; g < G; g++)
         if (rc[g] != DMX_OK) return 1;
@@ -1240,6 +1303,7 @@ void dmx_destroy(dmx_ctx* c) {
                       &c->tiles, &c->tileoffs, &c->recs, &c->status, &c->dbg, &c->ltok,
                       &c->ltokoff, &c->lntok, &c->lcaps, &c->lheavy, &c->rtmp, &c->rchain, &c->fbc, &c->fbh, &c->fbo, &c->fbl,
                       &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg, &c->fbstop, &c->fbwin, &c->fbopen, &c->fbp32, &c->fbvm, &c->fbvh,
+                      &c->fbreg, &c->fbJ, &c->fbvis,
                       &c->ck})
         b->release();
     for (auto& e : c->ev)

@@ -91,6 +91,7 @@ struct InflateResult {
     int32_t status;   // fast path: 0 ok, 1 re-run with look-back, 2 serial; serial: 0 / DMX_ERR_*
     uint32_t fin_index;
     uint64_t exotic;  // candidates flagged SEGF_EXOTIC by the pass
+    uint64_t end_byte;  // status 0: the stream byte just past the final block (relative to the stream)
 };
 
 hipError_t launch_marker_count(const uint32_t* in_words, uint64_t misalign, uint64_t n,
@@ -141,7 +142,10 @@ struct FbUnit {         // per-unit record written by k_fb_pdecode / k_fb_decode
 constexpr uint64_t FB_STOP_WEAK = 1ull << 63;  // a stored-header (weak) unit
 constexpr uint64_t FB_STOP_SOFT = 1ull << 62;  // the next unit starts inside a block: end at the
                                                // first token boundary at or past the stop
-constexpr uint64_t FB_STOP_MASK = FB_STOP_SOFT - 1;
+constexpr uint64_t FB_STOP_REGION = 1ull << 61;  // the head of a long gap between dynamic-header
+                                                 // starts: a first block that is not dynamic ends
+                                                 // the unit at once (the region map decodes the run)
+constexpr uint64_t FB_STOP_MASK = FB_STOP_REGION - 1;
 // A code state (FbUnit.hdr, the per-unit vhdr): the stream bit of the dynamic block header whose
 // code is in force, or FB_STATE_FIXED for the fixed code; FB_STATE_FINAL: that block has BFINAL.
 constexpr uint64_t FB_STATE_FIXED = 1ull << 62;
@@ -171,6 +175,17 @@ hipError_t launch_fb_compact(const uint32_t* counts, const uint64_t* offs, const
                              uint64_t nchunks, uint64_t* list, hipStream_t st);
 // hits carry bit 62 for a stored-block header; stops[u] = the next dynamic-header start after u
 // units [u0, u0 + count) of the nunits listed; vmode / vhdr as above
+// fixed-code regions (k_fb_smap + k_fb_swalk): reg = nreg x {E, T, first super block}, sbreg =
+// the region of each of the nsb super blocks, J = nsb * fb_region_nodes() words, visit = nsb
+// words (the node the path enters each super block at, ~0 = none: region chunk << 6 | f << 5 |
+// offset, chunks of fb_region_chunk_bits()), rstat = nreg words (FB_REGION_END / _LINK / other)
+constexpr uint32_t FB_REGION_END = 0x80000001u, FB_REGION_LINK = 0x80000002u;
+uint64_t fb_region_super_bits();
+uint64_t fb_region_chunk_bits();
+uint32_t fb_region_nodes();
+hipError_t launch_fb_regions(const uint32_t* in_words, uint64_t misalign, uint64_t n, const uint64_t* reg,
+                             uint32_t nreg, const uint32_t* sbreg, uint64_t nsb, uint32_t* J, uint32_t* visit,
+                             uint32_t* rstat, hipStream_t st);
 hipError_t launch_fb_decode(const uint32_t* in_words, uint64_t misalign, uint64_t n,
                             const uint64_t* starts, const uint64_t* stops, const uint8_t* vmode,
                             const uint64_t* vhdr, uint64_t nunits, uint64_t u0, uint64_t count,

@@ -393,99 +393,6 @@ struct TokSink {
 };
 
 
-// Wave-uniform bit reader over a sliding LDS ring of the stream (k_fb_decode).  BitIn reads
-// through the scalar cache, and scalar loads share lgkmcnt with LDS, so every table lookup
-// waited for the next stream word (~1000 cycles per symbol on C3).  Here the wave copies the
-// stream into a ring of FB_RW words ahead of the reader, FB_RC words at a time, so every bit
-// read is an LDS read.  Invariant after seek / refill: words [wi - 1, wi + FB_AHEAD) are in
-// the ring (fast_header reads up to ~140 words past its start).  All lanes call every method
-// together (the decoder state is wave-uniform).
-constexpr uint32_t FB_RW = 1024, FB_RC = 512, FB_AHEAD = 320;
-struct RingIn {
-    const uint32_t* w;
-    uint64_t nwords, end_bytes, end_bits;
-    uint32_t* ring;
-    uint64_t rb;    // ring holds words [rb, rb + FB_RW) at ring[i % FB_RW]
-    uint64_t pos;   // bits consumed, relative to the aligned base
-    uint64_t buf;   // LSB = next bit
-    uint32_t cnt;   // valid bits in buf
-    uint64_t wi;    // next word to shift into buf
-
-    __device__ void init(const uint32_t* words, uint64_t misalign, uint64_t n, uint32_t* lds) {
-        w = words;
-        end_bytes = misalign + n;
-        end_bits = end_bytes * 8;
-        nwords = (end_bytes + 3) / 4;
-        ring = lds;
-        rb = ~0ull >> 1;
-    }
-    __device__ void fill(uint64_t from, uint64_t to) {  // words [from, to), masked at the end
-        for (uint64_t i = from + lane_id(); i < to; i += 64) {
-            uint32_t v = 0;
-            if (i < nwords) {
-                v = w[i];
-                const uint64_t lim = end_bytes - 4 * i;
-                if (lim < 4) v &= (1u << (8 * lim)) - 1u;
-            }
-            ring[i % FB_RW] = v;
-        }
-        wave_sync();
-    }
-    __device__ uint32_t word(uint64_t i) const { return ring[i % FB_RW]; }
-    __device__ void refill() {
-        if (cnt <= 32) {
-            if (wi + FB_AHEAD >= rb + FB_RW) {  // slide: the oldest FB_RC words make room
-                fill(rb + FB_RW, rb + FB_RW + FB_RC);
-                rb += FB_RC;
-            }
-            buf |= (uint64_t)word(wi) << cnt;
-            cnt += 32;
-            wi++;
-        }
-    }
-    __device__ void seek(uint64_t bitpos) {
-        pos = bitpos;
-        const uint64_t i = bitpos >> 5;
-        if (i < rb || i + 1 + FB_AHEAD >= rb + FB_RW) {
-            rb = i;
-            fill(i, i + FB_RW);
-        }
-        buf = (uint64_t)(word(i) >> (bitpos & 31));
-        cnt = 32 - (uint32_t)(bitpos & 31);
-        wi = i + 1;
-        refill();
-    }
-    __device__ void ensure(uint32_t k) {  // k <= 33
-        if (cnt < k) refill();
-    }
-    __device__ uint32_t peek(uint32_t k) const { return (uint32_t)buf & ((1u << k) - 1u); }
-    __device__ void consume(uint32_t k) {
-        buf >>= k;
-        cnt -= k;
-        pos += k;
-    }
-    __device__ uint32_t bits(uint32_t k) {  // k <= 16
-        ensure(k);
-        const uint32_t v = peek(k);
-        consume(k);
-        return v;
-    }
-    __device__ void align() {
-        ensure(8);
-        consume((8 - (uint32_t)(pos & 7)) & 7);
-    }
-    __device__ bool over() const { return pos > end_bits; }
-    __device__ uint32_t window32() {
-        ensure(32);
-        return (uint32_t)buf;
-    }
-    __device__ uint64_t abspos() const { return pos; }
-};
-struct RingWords {
-    const uint32_t* ring;
-    __device__ uint32_t word(uint64_t i) const { return ring[i % FB_RW]; }
-};
-__device__ __forceinline__ RingWords reader_words(const RingIn& br) { return RingWords{br.ring}; }
 
 struct FbDecodeArgs {
     const uint32_t* in_words;
@@ -530,6 +437,7 @@ __device__ __attribute__((noinline)) void fb_serial(const FbDecodeArgs& A, uint6
     // by fixed ones -- zlib's small blocks -- needs the weak unit to carry on through them.)
     const bool weak = (A.stops[u] & FB_STOP_WEAK) != 0;
     const bool soft = (A.stops[u] & FB_STOP_SOFT) != 0;
+    const bool region_head = (A.stops[u] & FB_STOP_REGION) != 0;
     const uint64_t stop = A.stops[u] & FB_STOP_MASK;
     uint64_t jn = 0;  // first listed unit start above the unit's start (repair units are
     {                 // appended after the sorted list: search it)
@@ -540,8 +448,8 @@ __device__ __attribute__((noinline)) void fb_serial(const FbDecodeArgs& A, uint6
             else hi = mid;
         }
     }
-    uint64_t end_at = 0;  // stream bit of the first block the unit leaves undecoded (weak units,
-                          // a far fixed block), else 0
+    uint64_t end_at = 0;  // (end_set) aligned-image bit of the first block the unit leaves
+    bool end_set = false; // undecoded: weak units, a far fixed block, a region head's run
     const uint64_t base = A.misalign * 8;  // stream bit 0 in the aligned image
     const uint64_t soft_abs = soft ? base + stop : ~0ull;
     RingIn br;
@@ -595,12 +503,10 @@ __device__ __attribute__((noinline)) void fb_serial(const FbDecodeArgs& A, uint6
         const uint32_t btype = br.bits(2);
         if (br.over()) { err = SEGF_OVERREAD; break; }
         if (!f) crossed = true;
-        if (weak && btype == 2) {
+        if ((weak && btype == 2) || (f && region_head && btype != 2) ||
+            (!f && btype == 1 && stop - (hpos - base) > FB_SER_FIXED_MAX)) {  // a far fixed run
             end_at = hpos;
-            break;
-        }
-        if (!f && btype == 1 && stop - (hpos - base) > FB_SER_FIXED_MAX) {  // a far fixed run
-            end_at = hpos;
+            end_set = true;
             break;
         }
         if (btype == 0) {
@@ -644,7 +550,7 @@ __device__ __attribute__((noinline)) void fb_serial(const FbDecodeArgs& A, uint6
     if (lane_id() == 0) {
         FbUnit r;
         r.start = start;
-        r.end = (end_at ? end_at : br.abspos()) - base;
+        r.end = (end_set ? end_at : br.abspos()) - base;
         r.size = sk.pos;
         r.ntok = sk.n;
         r.hdr = midend ? state : FB_AT_HEADER;
@@ -657,8 +563,7 @@ __device__ __attribute__((noinline)) void fb_serial(const FbDecodeArgs& A, uint6
 __global__ __launch_bounds__(64) void k_fb_decode(FbDecodeArgs A) {
     __shared__ Tables T;
     __shared__ uint32_t ring[FB_RW];
-    const uint64_t u = A.u0 + blockIdx.x;
-    if (u >= A.nunits) return;
+    const uint64_t u = A.u0 + blockIdx.x;  // (the grid is the launch's unit count)
     const uint8_t vm = A.vmode[u];
     if (vm == FB_V_VIRTUAL) {  // a guessed start: only the lane-parallel decoder's warm-up finds
         if (threadIdx.x == 0) { // the token boundary near it (the chain repairs around it)
@@ -792,6 +697,9 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             S.hecap = hecap;
         }
         if (vm == FB_V_VIRTUAL && kind != 0) kind = 3;  // no serial decode from a guessed start
+        // a region head whose first block is not dynamic: the unit is empty, the region map
+        // takes the run of blocks from its header on
+        if ((A.stops[u] & FB_STOP_REGION) && vm == FB_V_HEADER && btype != 2) kind = 5;
         S.kind = kind;
         S.err = SEGF_ERR_DATA;
         S.btype = btype;
@@ -1102,10 +1010,10 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
         break;
     }
     const uint32_t kind = S.kind;
-    if (A.stats && t == 0) atomicAdd(&A.stats[weak ? 3 : kind == 3 ? 0 : kind], 1u);
+    if (A.stats && t == 0 && kind != 5) atomicAdd(&A.stats[weak ? 3 : kind == 3 ? 0 : kind], 1u);
     // a virtual unit starts at the token boundary its warm-up found
     const uint64_t rstart = vm == FB_V_VIRTUAL && kind != 3 ? S.ws * 32 + S.hs + S.vs0 - base : start;
-    if (kind == 0 || kind == 3) {
+    if (kind == 0 || kind == 3 || kind == 5) {
         if (t == 0) {
             FbUnit rec;
             rec.start = rstart;
@@ -1113,7 +1021,9 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             rec.size = kind == 0 ? S.bytes : 0;
             rec.ntok = kind == 0 ? S.words : 0;
             rec.hdr = kind == 0 && S.midend ? S.vstate : FB_AT_HEADER;
-            rec.flags = kind == 3 ? S.err : ((S.bfinal && !S.midend) ? SEGF_FINAL : 0u) | (S.crossed ? SEGF_CROSSED : 0u);
+            rec.flags = kind == 3 ? S.err
+                        : kind == 5 ? 0u
+                                    : ((S.bfinal && !S.midend) ? SEGF_FINAL : 0u) | (S.crossed ? SEGF_CROSSED : 0u);
             A.units[u] = rec;
         }
     } else if (wave == 0) {
@@ -1620,6 +1530,254 @@ __global__ __launch_bounds__(256) void k_fb_final(const uint16_t* img, const uin
             out[x] = v < 0x8000u ? (uint8_t)v : (b <= uoff ? out[uoff - b] : (uint8_t)0);
         }
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// Fixed-code regions: exact token boundaries without scanned block starts.
+//
+// A run of fixed-code blocks (zlib's Z_FIXED, the reference's own level-1/2 fixed chunks,
+// realDecompress's prebuilt trees, inflate.hpp:280-283, 310-312) or one huge block has no
+// dynamic header for the scan to find, and a decode that starts off the token path inside it
+// need not get back on it: in literal runs of one code length (8-bit codes for bytes < 144)
+// every misaligned start stays misaligned.  Guessing starts and repairing them round by round
+// therefore does not converge.  Instead the region [E, T) -- from the block header E where the
+// unit before it stopped, to the next dynamic-header start T -- is cut into chunks of FBS_CH
+// bits, and for every chunk c and entry offset e < 32 (a fixed-code token is at most 31 bits:
+// 8-bit length code + 5 extra + 5-bit distance code + 13 extra, so the token path enters every
+// chunk within its first 31 bits) one lane decodes from bit c * FBS_CH + e to the first token
+// boundary at or past the next chunk: a function from entries to entries.  The true path is
+// that function's orbit from E.
+//
+// Node = (chunk, f, e): f is the BFINAL bit of the fixed block in force.  A lane starting at e
+// does not know f; f only matters at the first end of block it meets, so one lane yields both
+// nodes' results: with f = 1 the first end of block ends the stream, with f = 0 the next header
+// is read.  End of block + the following headers are one token: stored blocks are skipped
+// (the lane continues from the chunk their data ends in), BTYPE 3 blocks are empty (the
+// reference has no case for them, inflate.hpp:292), a dynamic header ends the lane (a link
+// when it is T, else no path), so every boundary is inside a fixed block.
+//
+// A node's result (32 bits): a next node (region chunk << 6 | f << 5 | e, bit 31 clear) or a
+// terminal FBS_END (the final block ended), FBS_LINK (the dynamic header at T follows), FBS_FAIL
+// (no valid path: past T, an over-read).  Chunk 0's node 0 is the region head: the block header
+// at E (its other nodes are unreachable).
+//
+//   k_fb_smap   one workgroup per super block of FBS_K chunks (2^18 bits, staged in LDS): the
+//               chunk map, then pointer jumping in LDS so that every node of the super block
+//               maps to the first node of its path past the super block (or a terminal).
+//   k_fb_swalk  one lane per region walks those jumps from the head: one dependent read per
+//               super block; the node where the path enters each super block is recorded.
+// The host starts one unit per visited super block at that node (FB_V_EXACT, fixed code, f),
+// each ending softly at the next one's start: exact starts, so every link holds.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t FBS_CH = 4096;             // bits per chunk
+constexpr uint32_t FBS_K = 64;                // chunks per super block
+constexpr uint32_t FBS_SB = FBS_CH * FBS_K;   // 2^18 bits
+constexpr uint32_t FBS_NODES = FBS_K * 64;    // nodes per super block
+constexpr int FBS_NT = 256;
+constexpr uint32_t FBS_STG = FBS_SB / 32 + 128;  // staged words: one before the super block, 4 KiB bits after
+constexpr uint32_t FBS_TERM = 0x80000000u;
+constexpr uint32_t FBS_END = FB_REGION_END, FBS_LINK = FB_REGION_LINK, FBS_FAIL = FBS_TERM | 3u;
+
+struct FbsSmem {
+    uint32_t stg[FBS_STG + 2];
+    uint32_t lut[512];          // fixed lit/len code by the next 9 stream bits (lit_entry format)
+    uint32_t J[FBS_NODES];
+};
+
+// 32 bits at stream bit p: from the staged words when they hold them, else from HBM (masked at
+// the stream end; a stored block's data can carry a lane far past the staging)
+struct FbsBits {
+    const uint32_t* stg;
+    uint64_t a0;        // aligned-image bit of stg[0]
+    const uint32_t* w;  // aligned image
+    uint64_t base, nwords, end_bytes;
+    __device__ uint32_t word(uint64_t i) const {
+        if (i >= nwords) return 0u;
+        const uint32_t v = w[i];
+        const uint64_t lim = end_bytes - 4 * i;
+        return lim >= 4 ? v : v & ((1u << (8 * lim)) - 1u);
+    }
+    __device__ uint32_t peek(uint64_t p) const {
+        const uint64_t a = base + p;
+        const uint64_t rel = a - a0;
+        if (a >= a0 && rel < (uint64_t)(FBS_STG - 1) * 32) {
+            const uint32_t i = (uint32_t)(rel >> 5);
+            return __builtin_amdgcn_alignbit(stg[i + 1], stg[i], (uint32_t)(rel & 31));
+        }
+        const uint64_t i = a >> 5;
+        return __builtin_amdgcn_alignbit(word(i + 1), word(i), (uint32_t)(a & 31));
+    }
+};
+
+// One lane: the token path from stream bit p (hstate: p is the region head's block header)
+// to the first fixed-code token boundary at or past the next chunk (chunk grid from E).
+// *r0 / *r1: the result for entry f = 0 / f = 1.
+__device__ void fbs_lane(const FbsBits& B, const uint32_t* lut, uint64_t p, bool hstate, uint64_t E,
+                         uint64_t T, uint64_t nbits, uint32_t* r0, uint32_t* r1) {
+    uint64_t target = p - ((p - E) % FBS_CH) + FBS_CH;
+    bool eob_seen = false;  // an end of block met with f unknown: the f = 1 entry ended there
+    bool hdr = hstate;      // a header is next
+    uint32_t fcur = 0;      // BFINAL of the last header read (valid once one was read)
+    bool hdr_read = false;
+    uint32_t res = 0;
+    for (;;) {
+        if (hdr) {
+            // block headers up to the next fixed block (stored data skipped, BTYPE 3 empty)
+            if (p >= T || p + 3 > nbits) { res = (p == T && T < nbits) ? FBS_LINK : FBS_FAIL; break; }
+            const uint32_t h = B.peek(p) & 7u;
+            const uint32_t bfinal = h & 1u, btype = h >> 1;
+            if (btype == 2) { res = FBS_FAIL; break; }  // a dynamic header before T: not scanned
+            p += 3;
+            hdr_read = true;
+            if (btype == 1) {
+                fcur = bfinal;
+                hdr = false;
+                continue;
+            }
+            if (btype == 0) {
+                p = (p + 7) & ~7ull;
+                if (p + 32 > nbits) { res = FBS_FAIL; break; }
+                const uint32_t len = B.peek(p) & 0xFFFFu;  // NLEN unchecked (inflate.hpp:293-303)
+                p += 32 + 8ull * len;
+                if (p > nbits) { res = FBS_FAIL; break; }
+            }
+            if (bfinal) { res = FBS_END; break; }
+            continue;
+        }
+        // a fixed-code token boundary
+        if (p >= T) { res = FBS_FAIL; break; }
+        if (p >= target) {
+            const uint64_t rel = p - E;
+            const uint64_t cc = rel / FBS_CH;
+            const uint32_t off = (uint32_t)(rel % FBS_CH);
+            if (off < 32) {
+                res = (uint32_t)(cc << 6) | (off & 31u);
+                break;
+            }
+            target = E + (cc + 1) * FBS_CH;  // a stored block's data ended deep inside a chunk
+        }
+        const uint32_t v = B.peek(p);
+        const uint32_t e = lut[v & 511u];
+        const uint32_t cl = e & 15u, ty = (e >> 4) & 3u;
+        if (ty == 0) {
+            p += cl;
+        } else if (ty == 2) {
+            const uint32_t ex = (e >> 6) & 15u;
+            p += cl + ex;
+            const uint32_t ds = __builtin_bitreverse32(B.peek(p)) >> 27;  // 5-bit distance code
+            p += 5 + (ds < 30 ? dist_extra(ds) : 0u);
+        } else {  // end of block
+            p += 7;
+            if (!hdr_read) eob_seen = true;
+            else if (fcur) { res = FBS_END; break; }
+            hdr = true;
+        }
+        if (p > nbits) { res = FBS_FAIL; break; }
+    }
+    if (!(res & FBS_TERM)) {
+        *r0 = res | ((hdr_read ? fcur : 0u) << 5);
+        *r1 = eob_seen ? FBS_END : (res | (1u << 5));
+    } else {
+        *r0 = res;
+        *r1 = eob_seen ? FBS_END : res;
+    }
+}
+
+struct FbsArgs {
+    const uint32_t* in_words;
+    uint64_t misalign, n;
+    const uint64_t* reg;    // per region: E, T, first super block (3 words)
+    const uint32_t* sbreg;  // region of each super block
+    uint32_t* J;            // FBS_NODES per super block
+    uint32_t* visit;        // per super block: the node the path enters it at (~0: none)
+    uint32_t* rstat;        // per region: the walk's terminal
+    uint32_t nreg;
+};
+
+__global__ __launch_bounds__(FBS_NT) void k_fb_smap(FbsArgs A) {
+    __shared__ __attribute__((aligned(16))) FbsSmem S;
+    const uint32_t t = threadIdx.x;
+    const uint64_t sb = blockIdx.x;
+    const uint32_t r = A.sbreg[sb];
+    const uint64_t E = A.reg[3 * r], T = A.reg[3 * r + 1], lsb = sb - A.reg[3 * r + 2];
+    const uint64_t base = A.misalign * 8;
+    const uint64_t end_bytes = A.misalign + A.n, nwords = (end_bytes + 3) / 4, nbits = 8 * A.n;
+    const uint64_t b0 = E + lsb * FBS_SB;  // first bit of the super block
+    const uint64_t w0 = ((base + b0) >> 5) - ((base + b0) >= 32 ? 1 : 0);
+    FbsBits B{S.stg, w0 * 32, A.in_words, base, nwords, end_bytes};
+    for (uint32_t i = t; i < FBS_STG + 2; i += FBS_NT) S.stg[i] = B.word(w0 + i);
+    for (uint32_t v = t; v < 512; v += FBS_NT) {
+        // the fixed lit/len code (RFC 1951 3.2.6) by the next 9 stream bits, MSB-first code x
+        const uint32_t x = __builtin_bitreverse32(v) >> 23;
+        uint32_t sym, len;
+        if ((x >> 2) < 0x18) sym = 256 + (x >> 2), len = 7;
+        else if ((x >> 1) >= 0x30 && (x >> 1) <= 0xBF) sym = (x >> 1) - 0x30, len = 8;
+        else if ((x >> 1) >= 0xC0 && (x >> 1) <= 0xC7) sym = 280 + (x >> 1) - 0xC0, len = 8;
+        else sym = 144 + x - 0x190, len = 9;
+        S.lut[v] = lit_entry(sym, len);
+    }
+    __syncthreads();
+    // the chunk map: 32 lanes per chunk, entry e = lane & 31
+    const uint32_t e = t & 31;
+    for (uint32_t lc = t >> 5; lc < FBS_K; lc += FBS_NT / 32) {
+        const uint64_t cc = lsb * FBS_K + lc;
+        const uint64_t p = E + cc * FBS_CH + e;
+        uint32_t r0 = FBS_FAIL, r1 = FBS_FAIL;
+        if (cc == 0) {
+            if (e == 0) fbs_lane(B, S.lut, p, true, E, T, nbits, &r0, &r1);
+            r1 = FBS_FAIL;
+        } else if (p < T) {
+            fbs_lane(B, S.lut, p, false, E, T, nbits, &r0, &r1);
+        }
+        S.J[lc * 64 + e] = r0;
+        S.J[lc * 64 + 32 + e] = r1;
+    }
+    __syncthreads();
+    // pointer jumping inside the super block: a path has at most one node per chunk
+    const uint32_t lo = (uint32_t)(lsb * FBS_K);  // region chunk of local chunk 0
+    for (int round = 0; round < 7; round++) {
+        for (uint32_t i = t; i < FBS_NODES; i += FBS_NT) {
+            uint32_t v = S.J[i];
+            if (v & FBS_TERM) continue;
+            const uint32_t c = v >> 6;
+            if (c - lo < FBS_K) S.J[i] = S.J[(c - lo) * 64 + (v & 63u)];
+        }
+        __syncthreads();
+    }
+    uint32_t* Jg = A.J + sb * FBS_NODES;
+    for (uint32_t i = t; i < FBS_NODES; i += FBS_NT) Jg[i] = S.J[i];
+}
+
+__global__ __launch_bounds__(64) void k_fb_swalk(FbsArgs A) {
+    const uint32_t r = blockIdx.x;
+    if (threadIdx.x != 0 || r >= A.nreg) return;
+    const uint64_t sb0 = A.reg[3 * r + 2];
+    uint32_t node = 0;  // the head: chunk 0, node 0
+    A.visit[sb0] = 0;
+    for (;;) {
+        const uint32_t v = A.J[(sb0 + (node >> 6) / FBS_K) * FBS_NODES + ((node >> 6) % FBS_K) * 64 + (node & 63u)];
+        if (v & FBS_TERM) {
+            A.rstat[r] = v;
+            return;
+        }
+        A.visit[sb0 + (v >> 6) / FBS_K] = v;
+        node = v;
+    }
+}
+
+uint64_t fb_region_super_bits() { return FBS_SB; }
+uint64_t fb_region_chunk_bits() { return FBS_CH; }
+uint32_t fb_region_nodes() { return FBS_NODES; }
+
+hipError_t launch_fb_regions(const uint32_t* in_words, uint64_t misalign, uint64_t n, const uint64_t* reg,
+                             uint32_t nreg, const uint32_t* sbreg, uint64_t nsb, uint32_t* J, uint32_t* visit,
+                             uint32_t* rstat, hipStream_t st) {
+    if (!nreg || !nsb) return hipSuccess;
+    const FbsArgs A{in_words, misalign, n, reg, sbreg, J, visit, rstat, nreg};
+    (void)hipMemsetAsync(visit, 0xFF, nsb * 4, st);
+    hipLaunchKernelGGL(k_fb_smap, dim3((uint32_t)nsb), dim3(FBS_NT), 0, st, A);
+    hipLaunchKernelGGL(k_fb_swalk, dim3(nreg), dim3(64), 0, st, A);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------

@@ -553,6 +553,103 @@ __device__ uint32_t fast_header(const Src& src, uint64_t* pos_io, uint64_t end_b
     return 0;
 }
 
+// Wave-uniform bit reader over a sliding LDS ring of the stream (fb_serial, k_inflate_serial).  BitIn reads
+// through the scalar cache, and scalar loads share lgkmcnt with LDS, so every table lookup
+// waited for the next stream word (~1000 cycles per symbol on C3).  Here the wave copies the
+// stream into a ring of FB_RW words ahead of the reader, FB_RC words at a time, so every bit
+// read is an LDS read.  Invariant after seek / refill: words [wi - 1, wi + FB_AHEAD) are in
+// the ring (fast_header reads up to ~140 words past its start).  All lanes call every method
+// together (the decoder state is wave-uniform).
+constexpr uint32_t FB_RW = 1024, FB_RC = 512, FB_AHEAD = 320;
+struct RingIn {
+    const uint32_t* w;
+    uint64_t nwords, end_bytes, end_bits;
+    uint32_t* ring;
+    uint64_t rb;    // ring holds words [rb, rb + FB_RW) at ring[i % FB_RW]
+    uint64_t pos;   // bits consumed, relative to the aligned base
+    uint64_t buf;   // LSB = next bit
+    uint32_t cnt;   // valid bits in buf
+    uint64_t wi;    // next word to shift into buf
+
+    __device__ void init(const uint32_t* words, uint64_t misalign, uint64_t n, uint32_t* lds) {
+        w = words;
+        end_bytes = misalign + n;
+        end_bits = end_bytes * 8;
+        nwords = (end_bytes + 3) / 4;
+        ring = lds;
+        rb = ~0ull >> 1;
+    }
+    __device__ void fill(uint64_t from, uint64_t to) {  // words [from, to), masked at the end
+        for (uint64_t i = from + lane_id(); i < to; i += 64) {
+            uint32_t v = 0;
+            if (i < nwords) {
+                v = w[i];
+                const uint64_t lim = end_bytes - 4 * i;
+                if (lim < 4) v &= (1u << (8 * lim)) - 1u;
+            }
+            ring[i % FB_RW] = v;
+        }
+        wave_sync();
+    }
+    __device__ uint32_t word(uint64_t i) const { return ring[i % FB_RW]; }
+    __device__ void refill() {
+        if (cnt <= 32) {
+            if (wi + FB_AHEAD >= rb + FB_RW) {  // slide: the oldest FB_RC words make room
+                fill(rb + FB_RW, rb + FB_RW + FB_RC);
+                rb += FB_RC;
+            }
+            buf |= (uint64_t)word(wi) << cnt;
+            cnt += 32;
+            wi++;
+        }
+    }
+    __device__ void seek(uint64_t bitpos) {
+        pos = bitpos;
+        const uint64_t i = bitpos >> 5;
+        if (i < rb || i + 1 + FB_AHEAD >= rb + FB_RW) {
+            rb = i;
+            fill(i, i + FB_RW);
+        }
+        buf = (uint64_t)(word(i) >> (bitpos & 31));
+        cnt = 32 - (uint32_t)(bitpos & 31);
+        wi = i + 1;
+        refill();
+    }
+    __device__ void ensure(uint32_t k) {  // k <= 33
+        if (cnt < k) refill();
+    }
+    __device__ uint32_t peek(uint32_t k) const { return (uint32_t)buf & ((1u << k) - 1u); }
+    __device__ void consume(uint32_t k) {
+        buf >>= k;
+        cnt -= k;
+        pos += k;
+    }
+    __device__ uint32_t bits(uint32_t k) {  // k <= 16
+        ensure(k);
+        const uint32_t v = peek(k);
+        consume(k);
+        return v;
+    }
+    __device__ void align() {
+        ensure(8);
+        consume((8 - (uint32_t)(pos & 7)) & 7);
+    }
+    __device__ bool over() const { return pos > end_bits; }
+    __device__ uint32_t window32() {
+        ensure(32);
+        return (uint32_t)buf;
+    }
+    __device__ uint64_t abspos() const { return pos; }
+    __device__ uint8_t byte_at(uint64_t b) const {  // b relative to the aligned base (stored data)
+        return (uint8_t)(w[b >> 2] >> ((b & 3) * 8));
+    }
+};
+struct RingWords {
+    const uint32_t* ring;
+    __device__ uint32_t word(uint64_t i) const { return ring[i % FB_RW]; }
+};
+__device__ __forceinline__ RingWords reader_words(const RingIn& br) { return RingWords{br.ring}; }
+
 // ---------------------------------------------------------------------------------------
 // lane-parallel token decoding over LDS-staged words (k_inflate_pj, k_fb_pdecode): every lane
 // decodes its own bit range with 32-bit tables of PJ_LL / PJ_LD primary bits

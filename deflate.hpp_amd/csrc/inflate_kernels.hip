@@ -61,63 +61,6 @@ struct SegSink {
     }
 };
 
-// output sink of the serial path: 64 KiB LDS ring window + the output in HBM
-struct RingSink {
-    uint8_t* ring;
-    uint64_t pos;
-    uint8_t* out;
-    uint64_t cap;
-    bool count_only;
-    uint32_t err;
-    bool piece;  // a reference before the first byte is an error (DMX_IFLAG_PIECE)
-    __device__ bool full() const { return false; }
-    __device__ bool literal(uint32_t b) {
-        if (!count_only) {
-            if (lane_id() == 0) {
-                ring[pos & 0xFFFF] = (uint8_t)b;
-                if (pos < cap) out[pos] = (uint8_t)b;
-            }
-        }
-        pos++;
-        return true;
-    }
-    __device__ bool copy(uint32_t L, uint32_t dist) {
-        if (L == 0 || dist == 0) return true;
-        if (dist > pos) {
-            if (!piece) return true;  // reference: nothing to copy (inflate.hpp:268-270)
-            err |= SEGF_XREF;
-            return false;
-        }
-        if (!count_only) {
-            const uint32_t lane = lane_id();
-            const uint64_t src = pos - dist;
-            uint32_t r = dist >= L ? lane : (dist >= 64 ? lane : lane % dist);
-            const uint32_t step = dist >= L ? 64 : (dist >= 64 ? 64 : 64 % dist);
-            const bool wrap = dist < L;
-            for (uint32_t i = lane; i < L; i += 64) {
-                const uint8_t v = ring[(src + r) & 0xFFFF];
-                ring[(pos + i) & 0xFFFF] = v;
-                if (pos + i < cap) out[pos + i] = v;
-                r += step;
-                if (wrap && r >= dist) r -= dist;
-            }
-        }
-        pos += L;
-        return true;
-    }
-    template <class BR>
-    __device__ bool stored(const BR& br, uint64_t b0, uint32_t len) {
-        if (!count_only) {
-            for (uint32_t i = lane_id(); i < len; i += 64) {
-                const uint8_t v = br.byte_at(b0 + i);
-                ring[(pos + i) & 0xFFFF] = v;
-                if (pos + i < cap) out[pos + i] = v;
-            }
-        }
-        pos += len;
-        return true;
-    }
-};
 
 // ---------------------------------------------------------------------------------------
 // marker scan: candidates = {0} U {p : 4 <= p < n, in[p-4..p) == 00 00 FF FF}
@@ -981,6 +924,7 @@ __global__ void k_inflate_validate(InflateArgs A, const ValidateWords* W, Inflat
         } else {
             res->status = 0;
             res->total = A.recs[k].offset + A.recs[k].out_size;
+            res->end_byte = A.recs[k].end_byte;
         }
     } else {
         res->total = 0;
@@ -989,26 +933,97 @@ __global__ void k_inflate_validate(InflateArgs A, const ValidateWords* W, Inflat
 }
 
 // ---------------------------------------------------------------------------------------
-// serial path: the whole stream by one wavefront (sizes first, then bytes)
+// serial path: the whole stream by one wavefront, realDecompress (inflate.hpp:277-322) with
+// the reference's error semantics.  The stream comes through an LDS ring (RingIn: every bit
+// read is an LDS read; the scalar-cache reader waited ~1000 cycles per symbol), the output
+// through a 64 KiB LDS ring that holds the 32 KiB window and is written to HBM by the whole
+// wave in pieces of >= 32 KiB (instead of one single-byte global store per literal).  Bytes
+// past `cap` are counted, not written: the host re-runs with a larger buffer only when the
+// output did not fit.
 // ---------------------------------------------------------------------------------------
+struct FlushSink {
+    uint8_t* ring;   // 64 KiB
+    uint64_t pos;    // output bytes so far
+    uint64_t flushed;  // bytes [0, flushed) are in `out`
+    uint8_t* out;
+    uint64_t cap;
+    uint32_t err;
+    bool piece;  // a reference before the first byte is an error (DMX_IFLAG_PIECE)
+    __device__ bool full() const { return false; }
+    __device__ void flush() {  // [flushed, pos) ring -> out (at most 64 KiB, held by the ring)
+        const uint64_t hi = pos < cap ? pos : cap;
+        for (uint64_t i = flushed + lane_id(); i < hi; i += 64) out[i] = ring[i & 0xFFFF];
+        flushed = pos;
+    }
+    __device__ void grown() {
+        if (pos - flushed >= 32768) flush();
+    }
+    __device__ bool literal(uint32_t b) {
+        if (lane_id() == 0) ring[pos & 0xFFFF] = (uint8_t)b;
+        pos++;
+        grown();
+        return true;
+    }
+    __device__ bool copy(uint32_t L, uint32_t dist) {
+        if (L == 0 || dist == 0) return true;
+        if (dist > pos) {
+            if (!piece) return true;  // reference: nothing to copy (inflate.hpp:268-270)
+            err |= SEGF_XREF;
+            return false;
+        }
+        wave_sync();
+        const uint32_t lane = lane_id();
+        const uint64_t src = pos - dist;
+        if (dist >= L || dist >= 64) {  // each group of 64 reads only bytes written before it
+            for (uint32_t i = lane; i < L; i += 64) {
+                ring[(pos + i) & 0xFFFF] = ring[(src + i) & 0xFFFF];
+                wave_sync();
+            }
+        } else {  // periodic: byte i repeats byte i mod dist
+            for (uint32_t i = lane; i < L; i += 64) ring[(pos + i) & 0xFFFF] = ring[(src + i % dist) & 0xFFFF];
+        }
+        wave_sync();
+        pos += L;
+        grown();
+        return true;
+    }
+    template <class BR>
+    __device__ bool stored(const BR& br, uint64_t b0, uint32_t len) {
+        flush();
+        wave_sync();
+        for (uint32_t i = lane_id(); i < len; i += 64) {
+            const uint8_t v = br.byte_at(b0 + i);
+            ring[(pos + i) & 0xFFFF] = v;
+            if (pos + i < cap) out[pos + i] = v;
+        }
+        wave_sync();
+        pos += len;
+        flushed = pos;
+        return true;
+    }
+};
+
 __global__ __launch_bounds__(IF_NT) void k_inflate_serial(InflateArgs A, int count_only,
                                                           InflateResult* res) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[65536];
+    __shared__ uint32_t inring[FB_RW];
     __shared__ Tables T;
     if (threadIdx.x == 0) T.fixed_loaded = 0;
     __syncthreads();
-    BitIn br;
-    br.init(A.in_words, A.misalign, A.n);
+    RingIn br;
+    br.init(A.in_words, A.misalign, A.n, inring);
     br.seek(A.misalign * 8);
-    RingSink sk{ring, 0, A.out, A.cap, count_only != 0, 0, (A.flags & DMX_IFLAG_PIECE) != 0};
+    FlushSink sk{ring, 0, 0, A.out, count_only ? 0 : A.cap, 0, (A.flags & DMX_IFLAG_PIECE) != 0};
     uint64_t end_byte = 0;
     bool fin = false;
     const uint32_t err =
         inflate_blocks(br, T, sk, (A.flags & DMX_CFG_RFC_STRICT) != 0, false, &end_byte, &fin);
+    sk.flush();
     if (threadIdx.x == 0) {
         res->total = sk.pos;
         res->status = err == 0 ? 0 : (err & SEGF_OVERREAD) ? DMX_ERR_OVERREAD : DMX_ERR_DATA;
         res->fin_index = 0;
+        res->end_byte = fin ? end_byte - A.misalign : 0;
     }
 }
 

@@ -11,9 +11,10 @@ torch.distributed (RCCL over xGMI on MI355X nodes, gloo for the CPU tests):
      collective),
   2. rank 0 receives every shard at its prefix offset (batched P2P), others send.
 
-deflate_gather() pipelines this: the shard is compressed in sub-shards, and each sub-shard's
-bytes go to rank 0 (into a staging slot) while the next one compresses; rank 0 compresses its
-own shard straight into the output and packs the other ranks' slots behind it at the end.
+deflate_gather() pipelines this: ranks 1.. compress their shard in sub-shards on a side stream,
+and each sub-shard's bytes go to rank 0 while the next one compresses; rank 0 compresses its own
+shard straight into the output (one non-blocking call) and packs the other ranks' sub-shards
+behind it at the end.
 """
 import torch
 import torch.distributed as dist
@@ -75,19 +76,65 @@ def gather_stream(local, clen, out=None):
     return total
 
 
+class _Lens:
+    """Per-step compressed lengths that stay on the device while the next step compresses; each
+    is read on the host one step later through a pinned copy and an event on the compression
+    stream (never an .item() that would wait for the work behind it).  CPU tensors (the gloo
+    tests) are read directly."""
+
+    def __init__(self, count, dev):
+        self.dev = dev
+        self.d = torch.zeros(max(1, count), dtype=torch.int64, device=dev)
+        self.cuda = dev.type == "cuda"
+        self.h = torch.zeros(max(1, count), dtype=torch.int64, pin_memory=self.cuda)
+        self.ev = [None] * max(1, count)
+        self.stream = torch.cuda.Stream(dev) if self.cuda else None
+
+    def ptr(self, k):
+        return self.d.data_ptr() + 8 * k
+
+    def issued(self, k):  # after step k's compression was enqueued on self.stream
+        if self.cuda:
+            with torch.cuda.stream(self.stream):
+                self.h[k].copy_(self.d[k], non_blocking=True)
+                self.ev[k] = torch.cuda.Event()
+                self.ev[k].record(self.stream)
+
+    def read(self, k):  # the host value of step k; torch's stream then also waits for step k
+        if not self.cuda:
+            return int(self.d[k])
+        self.ev[k].synchronize()
+        torch.cuda.current_stream(self.dev).wait_event(self.ev[k])
+        return int(self.h[k])
+
+
+def _deflate(ctx, lens, k, src, n, level, dst, cap, not_final):
+    """Enqueue one device deflate (length into lens step k): dmx's non-blocking call on the
+    compression stream, or -- a codec without it (the CPU stand-in) -- the blocking one."""
+    if hasattr(ctx, "deflate_device_async"):
+        ctx.deflate_device_async(src, n, level, dst, cap, lens.ptr(k),
+                                 stream=lens.stream.cuda_stream if lens.cuda else None, not_final=not_final)
+    else:
+        lens.d[k] = ctx.deflate_device(src, n, level, dst, cap, not_final=not_final)
+    lens.issued(k)
+
+
 def deflate_gather(ctx, d_in, n, level, out=None, sub=4, align=32768):
     """Compress this rank's device-resident shard d_in[:n] and gather every rank's stream on
     rank 0, the transfers pipelined behind the compression.
 
-    The shard is cut into `sub` sub-shards (multiples of `align`), each compressed NOT_FINAL
-    except the last rank's last NON-EMPTY one, which carries BFINAL (a last rank with no bytes
-    emits the empty final block 03 00, so the gathered stream always ends in BFINAL).  After
-    sub-shard k every rank r >= 1 sends its length and then its bytes to rank 0 (asynchronous
-    P2P) and goes on compressing k + 1.  Rank 0 compresses its own shard straight into `out`
-    (its bytes open the stream), posts the length receives of step k before compressing k + 1
-    and reads them only after it (one step of lag: rank 0's compression never waits for the
-    other ranks), then posts the payload receives into a per-rank staging buffer of the shard
-    bound; at the end it packs ranks 1.. behind its own bytes (rank order, then k).
+    Ranks r >= 1 cut the shard into `sub` sub-shards (multiples of `align`), each compressed
+    NOT_FINAL except the last rank's last NON-EMPTY one, which carries BFINAL (a last rank with
+    no bytes emits the empty final block 03 00, so the gathered stream always ends in BFINAL).
+    Sub-shard k is enqueued on a side stream; then the length of k - 1 is read (it finished
+    while k runs) and its length and bytes go to rank 0 by P2P.  Rank 0 compresses its whole
+    shard with one non-blocking call straight into `out` (its bytes open the stream) and, while
+    that runs, receives the other ranks' sub-shards: each length first, then the bytes into a
+    buffer of exactly that size (staging = the compressed bytes of ranks 1.., not a worst-case
+    bound per rank and step).  The stream is rank-major (rank r's input shard follows rank
+    r - 1's), and rank r's offset is known only once every rank before it has finished, so
+    rank 0 packs the received sub-shards behind its own bytes at the end: that copy of
+    (world - 1) / world of the stream is inherent to the byte order.
     ctx: dmx.Context on this rank's GPU.  Returns (total stream bytes, this rank's bytes) on
     every rank; raises ValueError on every rank when rank 0's out is too small.
     """
@@ -95,90 +142,94 @@ def deflate_gather(ctx, d_in, n, level, out=None, sub=4, align=32768):
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = d_in.device
     last = rank == world - 1
-    cuts = [min(n, -(-(n * k // sub) // align) * align) for k in range(sub + 1)]
-    cuts[-1] = n
-    nonempty = [k for k in range(sub) if cuts[k + 1] > cuts[k]]
-    fin_k = (nonempty[-1] if nonempty else -1) if last else None
-    slot = dmx.deflate_bound(max([1] + [b - a for a, b in zip(cuts, cuts[1:])])) + 64
     cap0 = out.numel() if (rank == 0 and out is not None) else -1
-    direct = rank == 0 and cap0 >= sub * slot  # rank 0 compresses into out (room for any result)
-    stage = None if direct else torch.empty(sub * slot, dtype=torch.uint8, device=dev)
-    lens = [0] * sub
-    rlens = [[0] * sub for _ in range(world)]
-    rstage = [None] * world
     if rank == 0:
-        for r in range(1, world):
-            rstage[r] = torch.empty(sub * slot, dtype=torch.uint8, device=dev)
-    pend, keep = [], []
-    lag = None  # rank 0: (k, length tensors) whose payload receives are still to be posted
-
-    def post_payloads(k, got):  # the payload receives of step k (its lengths have arrived)
-        ops = []
-        for r in range(1, world):
-            Lr = int(got[r].item())
-            rlens[r][k] = Lr
-            if Lr:
-                ops.append(dist.P2POp(dist.irecv, rstage[r][k * slot: k * slot + Lr], r))
-        return ops
-
-    o0 = 0
-    for k in range(sub):
-        a, b = cuts[k], cuts[k + 1]
-        L = 0
-        if b > a or k == fin_k or (fin_k == -1 and k == sub - 1):
-            final = k == fin_k or (fin_k == -1 and k == sub - 1)
-            if direct:
-                dst, cap = out.data_ptr() + o0, slot
-            else:
-                dst, cap = stage.data_ptr() + k * slot, slot
-            L = ctx.deflate_device(d_in.data_ptr() + a, b - a, level, dst, cap, not_final=not final)
-        lens[k] = L
-        if direct:
-            o0 += L
-        if world == 1:
-            continue
-        if rank == 0:
-            # receives are posted in the order each rank sends (length k, payload k, length
-            # k + 1, ...): P2P matching per peer is in posting order (RCCL, gloo)
+        # rank 0: one call; BFINAL only when it is also the last rank
+        lens = _Lens(1, dev)
+        need = dmx.deflate_bound(max(1, n)) + 64
+        direct = cap0 >= need
+        stage = None if direct else torch.empty(need, dtype=torch.uint8, device=dev)
+        dst = out.data_ptr() if direct else stage.data_ptr()
+        own = n > 0 or world == 1  # (an empty first shard adds no bytes; alone it is 03 00)
+        if own:
+            _deflate(ctx, lens, 0, d_in.data_ptr(), n, level, dst, need, world > 1)
+        rbufs = [[None] * sub for _ in range(world)]
+        lag = None  # (k, length tensors, requests) of the step whose payload receives are pending
+        for k in range(sub if world > 1 else 0):
             got = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
             ops = []
-            if lag is not None:
+            if lag is not None:  # receives in each sender's order: length k-1, bytes k-1, length k
                 for q in lag[2]:
                     q.wait()
-                ops = post_payloads(lag[0], lag[1])
+                for r in range(1, world):
+                    L = int(lag[1][r].item())
+                    if L:
+                        rbufs[r][lag[0]] = torch.empty(L, dtype=torch.uint8, device=dev)
+                        ops.append(dist.P2POp(dist.irecv, rbufs[r][lag[0]], r))
             ops += [dist.P2POp(dist.irecv, got[r], r) for r in range(1, world)]
-            reqs = dist.batch_isend_irecv(ops)
-            lag = (k, got, reqs)
-        else:
+            lag = (k, got, dist.batch_isend_irecv(ops))
+        pend = []
+        if lag is not None:
+            for q in lag[2]:
+                q.wait()
+            ops = []
+            for r in range(1, world):
+                L = int(lag[1][r].item())
+                if L:
+                    rbufs[r][lag[0]] = torch.empty(L, dtype=torch.uint8, device=dev)
+                    ops.append(dist.P2POp(dist.irecv, rbufs[r][lag[0]], r))
+            if ops:
+                pend = dist.batch_isend_irecv(ops)
+        for q in pend:
+            q.wait()
+        mine = lens.read(0) if own else 0
+    else:
+        cuts = [min(n, -(-(n * k // sub) // align) * align) for k in range(sub + 1)]
+        cuts[-1] = n
+        nonempty = [k for k in range(sub) if cuts[k + 1] > cuts[k]]
+        fin_k = (nonempty[-1] if nonempty else sub - 1) if last else None
+        slot = dmx.deflate_bound(max([1] + [b - a for a, b in zip(cuts, cuts[1:])])) + 64
+        stage = torch.empty(sub * slot, dtype=torch.uint8, device=dev)
+        lens = _Lens(sub, dev)
+        emitted = [False] * sub
+        pend, keep = [], []
+
+        def send(j):  # step j's length, then its bytes
+            L = lens.read(j) if emitted[j] else 0
             lt = torch.tensor([L], dtype=torch.int64, device=dev)
             keep.append(lt)
             ops = [dist.P2POp(dist.isend, lt, 0)]
             if L:
-                ops.append(dist.P2POp(dist.isend, stage[k * slot: k * slot + L], 0))
-            pend += dist.batch_isend_irecv(ops)
-    if lag is not None:
-        for q in lag[2]:
+                ops.append(dist.P2POp(dist.isend, stage[j * slot: j * slot + L], 0))
+            pend.extend(dist.batch_isend_irecv(ops))
+            return L
+
+        mine = 0
+        for k in range(sub):
+            a, b = cuts[k], cuts[k + 1]
+            if b > a or k == fin_k:
+                _deflate(ctx, lens, k, d_in.data_ptr() + a, b - a, level, stage.data_ptr() + k * slot, slot,
+                         k != fin_k)
+                emitted[k] = True
+            if k:
+                mine += send(k - 1)
+        mine += send(sub - 1)
+        for q in pend:
             q.wait()
-        ops = post_payloads(lag[0], lag[1])
-        if ops:
-            pend += dist.batch_isend_irecv(ops)
-    for q in pend:
-        q.wait()
-    mine = sum(lens)
     st = _all_gather_ints([mine, cap0], dev) if world > 1 else [[mine, cap0]]
     total = sum(x[0] for x in st)
     if total and st[0][1] < total:
         raise ValueError("rank 0 needs an output buffer of at least the total stream size")
     if rank == 0:
-        rlens[0] = lens
-        rstage[0] = stage
-        o = o0 if direct else 0
-        for r in range(1 if direct else 0, world):
+        o = mine
+        if not direct and mine:
+            out[:mine].copy_(stage[:mine])
+        for r in range(1, world):
             for k in range(sub):
-                L = rlens[r][k]
-                if L:
-                    out[o: o + L].copy_(rstage[r][k * slot: k * slot + L])
-                    o += L
+                t = rbufs[r][k]
+                if t is not None:
+                    out[o: o + t.numel()].copy_(t)
+                    o += t.numel()
     return total, mine
 
 

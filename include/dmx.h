@@ -58,7 +58,8 @@ typedef struct dmx_config {
                                segments would be inflated too, where one device stops.          */
     /* developer controls for A/B runs; dmx_config_default sets both to 0 = the product plan */
     uint32_t dev_inflate_pass; /* k + 1 forces inflate pass k of the segmented plan
-                                  (0 wave, 1 workgroup, 2 look-back, 4 lanes, 5 block-parallel) */
+                                  (0 wave, 1 workgroup, 2 look-back, 4 lanes, 5 block-parallel,
+                                  7 the serial decoder alone) */
     uint32_t dev_heavy_bytes;  /* lane decoder: candidates spanning more compressed bytes go to
                                   the workgroup decoder; 0 = the built-in 2048 and CU rule      */
 } dmx_config;

@@ -22,8 +22,9 @@ def zfixed(data, level=6):
     return zlib_raw(data, level, 8, zlib.Z_FIXED)
 
 
-def single_fixed_block(data, final=True):
-    """One fixed-Huffman block holding every input byte as a literal, then end of block."""
+def single_fixed_block(data, final=True, close=False):
+    """One fixed-Huffman block holding every input byte as a literal, then end of block.
+    close (with final=False): an empty final fixed block follows in the same bit stream."""
     a = np.frombuffer(bytes(data), dtype=np.uint8).astype(np.uint32)
     code = np.where(a < 144, 0x30 + a, 0x190 + a - 144)  # fixed literal codes, MSB first
     ln = np.where(a < 144, 8, 9)
@@ -33,5 +34,8 @@ def single_fixed_block(data, final=True):
     body = bits[valid]  # row-major: each symbol's bits in sending order
     head = np.array([1 if final else 0, 1, 0], dtype=np.uint8)  # BFINAL, BTYPE = 01 (LSB first)
     eob = np.zeros(7, dtype=np.uint8)  # symbol 256: seven zero bits
-    allbits = np.concatenate([head, body, eob])
+    tail = [head, body, eob]
+    if close and not final:
+        tail += [np.array([1, 1, 0], dtype=np.uint8), eob]
+    allbits = np.concatenate(tail)
     return np.packbits(allbits, bitorder="little").tobytes()

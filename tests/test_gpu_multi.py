@@ -57,3 +57,20 @@ def test_deflate_device_async_leaves_length_on_device(ctx):
     ctx.deflate_device_async(d_in.data_ptr(), len(data), 2, a.data_ptr(), 1000, d_len.data_ptr(), stream=st)
     torch.cuda.synchronize()
     assert int(d_len[0]) == la > 1000
+
+
+def test_n_gpus_concatenated_streams_match_one_device(ctx, oracle):
+    """Two libdmx streams back to back: the reference stops at the first BFINAL block, so the
+    split decode must give exactly the one-device result (a piece that ends at an
+    early BFINAL no longer passes as complete; the stream falls back to one device)."""
+    a = dmx.corpus("mixed", 6 << 20, offset=7)
+    b = dmx.corpus("text", 6 << 20, offset=99)
+    s = ctx.compress(a, 2) + ctx.compress(b, 2)
+    want = oracle.inflate(s)
+    assert want == a
+    assert ctx.decompress(s) == want
+    multi = dmx.Context(n_gpus=2)
+    try:
+        assert multi.decompress(s) == want
+    finally:
+        multi.close()

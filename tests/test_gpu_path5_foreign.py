@@ -16,13 +16,13 @@ from oracle_bind import Reference
 pytestmark = pytest.mark.gpu
 
 
-def _gpu_inflate(ctx, s, n):
+def _gpu_inflate(ctx, s, n, reps=3):
     import torch
     d_in = torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda()
     d_o = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     ctx.set_timing(True)
     best = 1e30
-    for _ in range(3):
+    for _ in range(reps):
         olen = ctx.inflate_device(d_in.data_ptr(), len(s), d_o.data_ptr(), n + 64)
         best = min(best, ctx.stats().ms_device_total)
     path = ctx.stats().path
@@ -49,6 +49,7 @@ CASES = {
     "zlib1_zeros_256MiB": lambda: (dmx.corpus("zeros", 256 << 20), None),
     "single_block_16MiB": lambda: (dmx.corpus("mixed", 16 << 20), None),
     "zfixed_mixed_32MiB": lambda: (dmx.corpus("mixed", 32 << 20), None),
+    "single_block_open_8MiB": lambda: (dmx.corpus("text", 8 << 20), None),
 }
 
 
@@ -57,6 +58,8 @@ def _stream(name, data):
         return streams.zfixed(data)
     if name.startswith("zlib1"):
         return streams.zlib_raw(data, 1)
+    if "open" in name:  # a non-final block, then an empty final fixed block
+        return streams.single_fixed_block(data, final=False, close=True)
     return streams.single_fixed_block(data)
 
 
@@ -121,4 +124,21 @@ def test_path5_dynamic_then_fixed_run(ctx, oracle, final_fixed):
     assert b"\x00\x00\xff\xff" not in s[len(s1) - 16: len(s1) + 16]
     out, path, ms = _gpu_inflate(ctx, s, len(want))
     assert out == want == oracle.inflate(s)
+    assert path == 5
+
+
+@pytest.mark.parametrize("name", ["single_block_2MiB", "zfixed_mixed_4MiB", "zfixed_text_2MiB"])
+def test_path5_regions_serial_units(oracle, name):
+    """The same shapes with DMX_CFG_FB_SERIAL (every unit decoded by one wavefront, the serial
+    replay and window hand-off): the A/B reference of the lane-parallel unit decoder."""
+    kind, mib = {"single_block_2MiB": ("mixed", 2), "zfixed_mixed_4MiB": ("mixed", 4),
+                 "zfixed_text_2MiB": ("text", 2)}[name]
+    data = dmx.corpus(kind, mib << 20)
+    s = streams.single_fixed_block(data) if name.startswith("single") else streams.zfixed(data)
+    c = dmx.Context(fb_serial=True)
+    try:
+        out, path, ms = _gpu_inflate(c, s, len(data), reps=1)
+    finally:
+        c.close()
+    assert out == data == oracle.inflate(s)
     assert path == 5

@@ -288,7 +288,17 @@ class _HostDeflate:
         return len(s)
 
 
-def _deflate_gather_worker(rank, world, port, total, sub, cuts, q):
+class _HostDeflateAsync(_HostDeflate):
+    """The same with dmx.Context.deflate_device_async's interface: the length goes to an 8-byte
+    buffer (here a host int64), as the GPU path of shard.deflate_gather uses it."""
+
+    def deflate_device_async(self, d_in, n, level, d_out, cap, d_len, stream=None, not_final=False):
+        import ctypes
+        ctypes.c_int64.from_address(d_len).value = self.deflate_device(d_in, n, level, d_out, cap, not_final)
+
+
+def _deflate_gather_worker(rank, world, port, total, sub, cuts, *rest):
+    codec, q = rest if len(rest) == 2 else ("sync", rest[0])
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -297,9 +307,19 @@ def _deflate_gather_worker(rank, world, port, total, sub, cuts, q):
     b, e = (cuts[rank], cuts[rank + 1]) if cuts else shard.shard_range(total, rank, world, SEG)
     d_in = torch.frombuffer(bytearray(data[b:e] or b"\0"), dtype=torch.uint8)
     out = torch.empty(2 * total + 4096, dtype=torch.uint8) if rank == 0 else None
-    n, mine = shard.deflate_gather(_HostDeflate(), d_in, e - b, 0, out=out, sub=sub)
+    c = _HostDeflateAsync() if codec == "async" else _HostDeflate()
+    n, mine = shard.deflate_gather(c, d_in, e - b, 0, out=out, sub=sub)
     q.put((rank, bytes(out[:n].numpy()) if rank == 0 else mine))
     dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,sub", [(2, 3), (3, 4)])
+def test_deflate_gather_pipelined_async_codec(oracle, world, sub):
+    """The codec's non-blocking deflate (lengths left in device buffers, read one step late)."""
+    import dmx
+    total = 11 * SEG + 777
+    res = _run(_deflate_gather_worker, world, total, sub, None, "async", all_ranks=True)
+    assert oracle.inflate(res[0]) == dmx.corpus("mixed", total)
 
 
 @pytest.mark.parametrize("world,sub", [(2, 3), (3, 4)])

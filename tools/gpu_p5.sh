@@ -1,17 +1,13 @@
-# path-5 checks + timings (developer script): tests, probe, rocprof kernel stats of C3 and more
-set -e
-mkdir -p gpurun_out && cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread -k "${SEL:-path5 or foreign or c3 or quirk or zlib}" > gpurun_out/t5.log 2>&1 || { tail -30 gpurun_out/t5.log; exit 1; }
-tail -2 gpurun_out/t5.log
-DMX_FB_DEBUG=${FBDBG:-} timeout -k 10 200 python tools/foreign_probe.py ${SPECS:-bmp:0:1 text:256:1 text:1024:1 mixed:256:6} > gpurun_out/fp.log 2>&1
-grep -v "^W\|^E" gpurun_out/fp.log
-rm -rf gpurun_out/p5prof
-for sp in ${PROF:-bmp:0:1 mixed:256:6}; do
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/p5prof/$sp --output-format csv -- python3 tools/foreign_probe.py $sp > /dev/null 2>&1
-  python3 - "$sp" <<'PY'
-import csv, glob, sys
-f = glob.glob(f"gpurun_out/p5prof/{sys.argv[1]}/**/*kernel_stats.csv", recursive=True)[0]
-for r in csv.DictReader(open(f)):
-    print(f"{sys.argv[1]:14s} {r['Name'][:40]:40s} {r['Calls']:>4s} {float(r['AverageNs'])/1e3:10.1f} us")
-PY
-done
+# Path-5 check on the GPU: the region probe (DMX_FB_DEBUG), then the third-party-stream file,
+# then (unless quick) the whole GPU suite.  usage: bash tools/gpu_p5.sh [quick]
+mkdir -p gpurun_out
+timeout -k 10 300 python -u tools/p5single.py 4 16 > gpurun_out/p5single.log 2>&1 || { tail -40 gpurun_out/p5single.log; exit 1; }
+grep -E "^single|chain breaks|units:|repair|region" gpurun_out/p5single.log | head -40
+timeout -k 10 600 python -u -m pytest tests/test_gpu_path5_foreign.py tests/test_gpu_serial.py -v -s --timeout 300 --timeout-method thread > gpurun_out/p5v.log 2>&1; rc=$?
+grep -E "GPU |PASSED|FAILED|passed|failed|Error" gpurun_out/p5v.log | tail -24
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 1
+if [ "$1" != quick ]; then
+  timeout -k 10 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread --ignore=tests/test_gpu_path5_foreign.py --ignore=tests/test_gpu_serial.py > gpurun_out/gpu_tests.log 2>&1; rc=$?
+  grep -E "FAILED|passed|failed" gpurun_out/gpu_tests.log | tail -12
+  [ $rc -eq 0 ] || exit 1
+fi

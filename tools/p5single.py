@@ -13,9 +13,9 @@ ctx = dmx.Context()
 for mib in [int(x) for x in (sys.argv[1:] or ["1", "4", "16"])]:
     data = dmx.corpus("mixed", mib << 20)
     for final in (True, False):
-        s = streams.single_fixed_block(data, final=final)
-        if not final:
-            s = s + bytes([0x03, 0x00])  # an empty final fixed block after it
+        # (not final: an empty final fixed block follows in the same bit stream; appended at a
+        # byte boundary instead, the pad bits would read as a stored header: no final block)
+        s = streams.single_fixed_block(data, final=final, close=True)
         out = ctx.decompress(s)
         print(f"single {mib} MiB final={final}: path {ctx.stats().path} ok {out == data}", flush=True)
         sys.stderr.flush()
