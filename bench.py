@@ -53,28 +53,35 @@ REF_NOTES = {"text": "reference L2 stream is lossy (SURVEY A-1)",
              "mixed": "reference L2 stream is invalid (SURVEY A-3)",
              "bmp": "reference L2 stream is invalid (SURVEY A-3)"}
 REF_RATIO_L3_TEXT = 2.5741  # reference L3 on the 1 MiB text prefix
-PROFILE_TAG = "r04"  # tools/profile_all.sh writes profiles/<tag>_kstats_*.csv and traffic.json
+PROFILE_TAG = "r05"  # tools/profile_all.sh writes profiles/<tag>_kstats_*.csv and traffic.json
 
 
 def profile_path(name):
-    """profiles/<tag>_<name>, or the newest earlier round's file of that name when this round has
-    none yet (the record then names the round its evidence comes from)."""
-    for tag in (PROFILE_TAG, "r03"):
-        rel = f"profiles/{tag}_{name}"
-        if os.path.exists(os.path.join(ROOT, rel)):
-            return rel
-    return None
+    """profiles/<tag>_<name> of THIS round's kernels, or None: an earlier round's profile
+    describes other kernels and is never cited."""
+    rel = f"profiles/{PROFILE_TAG}_{name}"
+    return rel if os.path.exists(os.path.join(ROOT, rel)) else None
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def traffic_entry(tj, key):
+    """HBM bytes per launch under key, only when measured this round (traffic.py records the
+    round tag with every entry); None otherwise."""
+    d = tj.get(key + ":detail")
+    if key not in tj or not isinstance(d, dict) or d.get("round") != PROFILE_TAG:
+        return None
+    return tj[key]
 
 
 def traffic_of(key_prefix, kernels):
     """HBM bytes per launch from profiles/traffic.json (tools/profile_all.sh) for each kernel
-    that has an entry under key_prefix + kernel; None when none has."""
+    that has an entry of this round under key_prefix + kernel; None when none has."""
     try:
         tj = json.load(open(TRAFFIC_JSON))
     except Exception:
         return None
-    got = {k: tj[key_prefix + k] for k in kernels if key_prefix + k in tj}
+    got = {k: traffic_entry(tj, key_prefix + k) for k in kernels}
+    got = {k: v for k, v in got.items() if v is not None}
     return got or None
 
 
@@ -469,7 +476,7 @@ def main():
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
-            parts = [tj.get(f"{a.corpus}:{n}:{a.level}:{k}") for k in dom.split("+")]
+            parts = [traffic_entry(tj, f"{a.corpus}:{n}:{a.level}:{k}") for k in dom.split("+")]
             traffic = sum(parts) if all(x is not None for x in parts) else None
         except Exception:
             traffic = None

@@ -937,6 +937,8 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     // past the capacity are counted, not written); a second pass only when that did not fit
     c->stats.path = 2;
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
+    uint64_t dummy_dbg = 0;
+    A.dbg = (c->diag & DIAG_FB) ? &dummy_dbg : nullptr;  // (a flag for the kernel: count phases)
     if (!fixed_out) {
         size_t freeb = 0, totb = 0;
         if (hipMemGetInfo(&freeb, &totb) != hipSuccess) freeb = 0;
@@ -964,6 +966,10 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
         HIPCHK(hipStreamSynchronize(st));
     }
     end_timing(c, st);
+    if (c->diag & DIAG_FB)
+        std::fprintf(stderr, "dmx serial: cycles decode %llu walk %llu offsets %llu writes %llu flush %llu, steps %llu\n",
+                     (unsigned long long)r.cycles[0], (unsigned long long)r.cycles[1], (unsigned long long)r.cycles[2],
+                     (unsigned long long)r.cycles[3], (unsigned long long)r.cycles[4], (unsigned long long)r.cycles[5]);
     *total_out = r.total;
     c->last_end = r.end_byte;
     c->stats.out_bytes = r.total;
@@ -1256,6 +1262,9 @@ int dmx_create(dmx_ctx** out, const dmx_config* cfg) {
     int dev = cfg->device;
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return DMX_ERR_DEVICE;
     if (dev >= ndev || !is_gfx950(dev)) return DMX_ERR_DEVICE;
+    // n_gpus: at most 8 shards per visible device (a stale or garbage value -- a caller built
+    // against an older dmx_config -- would otherwise create contexts without bound)
+    if (cfg->n_gpus > 8u * (uint32_t)ndev) return DMX_ERR_ARG;
     DeviceGuard dg(dev);
     if (!dg.ok) return DMX_ERR_DEVICE;
     dmx_ctx* c = new (std::nothrow) dmx_ctx();

@@ -92,6 +92,8 @@ struct InflateResult {
     uint32_t fin_index;
     uint64_t exotic;  // candidates flagged SEGF_EXOTIC by the pass
     uint64_t end_byte;  // status 0: the stream byte just past the final block (relative to the stream)
+    uint64_t cycles[6];  // serial decoder (DMX_FB_DEBUG): s_memtime per phase -- decode, walk,
+                         // offsets, literals + copies, flush + refill, steps
 };
 
 hipError_t launch_marker_count(const uint32_t* in_words, uint64_t misalign, uint64_t n,

@@ -181,7 +181,8 @@ __device__ void build_tree(const uint8_t* lens, int nsym, uint16_t* sorted, Tree
 
 // the reference's lookup rule for key (k, x): the last-inserted code c in [lo_k, hi_k] with
 // c == x (mod 2^k) (common.hpp:95-100 overwrites on collision); for prefix codes c == x.
-__device__ __forceinline__ bool key_hit(const TreeMeta& m, uint32_t k, uint32_t x, uint32_t* c) {
+template <class Meta>  // (TreeMeta in any address space)
+__device__ __forceinline__ bool key_hit(const Meta& m, uint32_t k, uint32_t x, uint32_t* c) {
     if (!m.cnt[k] || x > m.hi[k]) return false;
     const uint32_t cm = x + (((m.hi[k] - x) >> k) << k);
     if (cm < m.lo[k]) return false;
@@ -249,7 +250,8 @@ __device__ void fill_prelut(uint16_t* lut, const TreeMeta& m, const uint16_t* so
 }
 
 // codes longer than the primary table: test lengths kfrom..15 in order
-__device__ __forceinline__ bool slow_decode(const TreeMeta& m, const uint16_t* sorted,
+template <class Meta, class Sorted>  // (LDS tables through a flat or an LDS pointer)
+__device__ __forceinline__ bool slow_decode(const Meta& m, const Sorted* sorted,
                                             uint32_t peek15, int kfrom, uint32_t* sym,
                                             uint32_t* len) {
     const uint32_t v = bitrev(peek15, 15);
@@ -831,6 +833,13 @@ __device__ uint32_t decode_huffman(BR& br, const Tables& T, Sink& sk, uint64_t s
     }
 }
 
+// One Huffman-coded block of inflate_blocks: the generic decoder; a sink with its own block
+// decoder (the serial path's FlushSink) provides an overload that ADL finds at instantiation.
+template <class BR, class Sink>
+__device__ __forceinline__ uint32_t decode_block(BR& br, const Tables& T, Sink& sk) {
+    return decode_huffman(br, T, sk);
+}
+
 // realDecompress (inflate.hpp:277-322).  With stop_at_marker the segment ends at an empty,
 // non-final stored block whose NLEN is FFFF (the "00 00 FF FF" the scanner keyed on).
 template <class BR, class Sink>
@@ -862,7 +871,7 @@ __device__ uint32_t inflate_blocks(BR& br, Tables& T, Sink& sk, bool rfc, bool s
                 load_fixed(T);
                 T.fixed_loaded = 1;
             }
-            const uint32_t err = decode_huffman(br, T, sk);
+            const uint32_t err = decode_block(br, T, sk);
             if (err) return err;
         } else if (btype == 2) {
             T.fixed_loaded = 0;
@@ -873,7 +882,7 @@ __device__ uint32_t inflate_blocks(BR& br, Tables& T, Sink& sk, bool rfc, bool s
             if (hdr_cycles) *hdr_cycles += __builtin_amdgcn_s_memtime() - h0;
             if (err) return err;
             br.seek(hp);
-            err = decode_huffman(br, T, sk);
+            err = decode_block(br, T, sk);
             if (err) return err;
         }  // btype 3: no-op block (inflate.hpp:292 has no case 3)
         if (bfinal) {

@@ -949,6 +949,7 @@ struct FlushSink {
     uint64_t cap;
     uint32_t err;
     bool piece;  // a reference before the first byte is an error (DMX_IFLAG_PIECE)
+    uint64_t* cyc;  // optional phase counters (sk_loop)
     __device__ bool full() const { return false; }
     __device__ void flush() {  // [flushed, pos) ring -> out (at most 64 KiB, held by the ring)
         const uint64_t hi = pos < cap ? pos : cap;
@@ -1003,6 +1004,256 @@ struct FlushSink {
     }
 };
 
+// A whole Huffman block for the serial path, 64 bit offsets at a time (the way fast_header reads
+// code lengths): lane i decodes the token -- literal, length + distance, end of block -- that
+// would start at bit p + i; the chain of true token starts from p is walked with v_readlane (a
+// few scalar instructions per token instead of a dependent table lookup); the chain's output
+// offsets come from one wave scan, its literals are written by one LDS store, its matches are
+// copied in order.  Semantics of decode_huffman (inflate.hpp:226-275): length symbols 286+ and
+// distance symbols 30+ copy nothing, a distance reaching before the stream start copies nothing
+// (an error in piece mode), a token ending past the stream is an over-read.
+constexpr uint32_t SK_LIT = 0, SK_MATCH = 1, SK_EOB = 2, SK_BAD = 3;
+__device__ __forceinline__ void sk_ring_copy(uint8_t* ring, uint64_t dst, uint32_t d, uint32_t L) {
+    const uint32_t lane = lane_id();
+    const uint64_t src = dst - d;
+    if (d >= L || d >= 64) {  // each group of 64 reads only bytes written before it
+        for (uint32_t i = lane; i < L; i += 64) {
+            ring[(dst + i) & 0xFFFF] = ring[(src + i) & 0xFFFF];
+            wave_sync();
+        }
+    } else {  // periodic: byte i repeats byte i mod d
+        for (uint32_t i = lane; i < L; i += 64) ring[(dst + i) & 0xFFFF] = ring[(src + i % d) & 0xFFFF];
+    }
+    wave_sync();
+}
+
+typedef __attribute__((address_space(3))) uint32_t LdsU32;
+typedef __attribute__((address_space(3))) uint8_t LdsU8;
+typedef __attribute__((address_space(3))) const Tables LdsTables;
+typedef __attribute__((address_space(1))) uint8_t GlbU8;
+typedef __attribute__((address_space(1))) const uint32_t GlbU32;
+
+// the token that would start at bit b: info = length in bits | kind << 8; *L = literal byte or
+// match length, *d = distance (0: symbols 286+ / 30+, no copy)
+__device__ __forceinline__ uint32_t sk_token(const LdsU32* ring, const LdsTables* T, uint64_t b, uint32_t* L,
+                                             uint32_t* d) {
+    const uint32_t wi = (uint32_t)(b >> 5);
+    const uint32_t sh = (uint32_t)(b & 31);
+    const uint32_t x0 = ring[wi % FB_RW], x1 = ring[(wi + 1) % FB_RW], x2 = ring[(wi + 2) % FB_RW];
+    const uint32_t v = __builtin_amdgcn_alignbit(x1, x0, sh);
+    const uint64_t W = (uint64_t)v | ((uint64_t)__builtin_amdgcn_alignbit(x2, x1, sh) << 32);
+    uint32_t e = T->llut[v & ((1u << LUT_L) - 1)];
+    if (!e) {
+        uint32_t sym, len;
+        e = slow_decode(T->lm, T->lsorted, v & 0x7FFF, LUT_L + 1, &sym, &len) ? lit_entry(sym, len) : 0u;
+    }
+    *L = 0;
+    *d = 0;
+    if (!e) return SK_BAD << 8;
+    const uint32_t cl = e & 15, ty = (e >> 4) & 3;
+    if (ty == 0) {
+        *L = e >> 16;
+        return cl | (SK_LIT << 8);
+    }
+    if (ty == 1) return cl | (SK_EOB << 8);
+    const uint32_t ex = (e >> 6) & 15;
+    *L = (e >> 16) + ((v >> cl) & ((1u << ex) - 1u));
+    const uint32_t q = cl + ex;
+    const uint32_t dv = (uint32_t)(W >> q);
+    uint32_t de = T->dlut[dv & ((1u << LUT_D) - 1)];
+    if (!de) {
+        uint32_t ds, dl;
+        de = slow_decode(T->dm, T->dsorted, dv & 0x7FFF, LUT_D + 1, &ds, &dl) ? dist_entry(ds, dl) : 0u;
+    }
+    if (!de) return SK_BAD << 8;
+    const uint32_t dl = de & 15, dx = (de >> 6) & 15;
+    *d = (de >> 16) + ((dv >> dl) & ((1u << dx) - 1u));
+    return (q + dl + dx) | (SK_MATCH << 8);
+}
+
+__device__ __forceinline__ void sk_copy(LdsU8* ring, uint64_t dst, uint32_t d, uint32_t L) {
+    const uint32_t lane = lane_id();
+    const uint64_t src = dst - d;
+    if (d >= L || d >= 64) {  // each group of 64 reads only bytes written before it
+        for (uint32_t i = lane; i < L; i += 64) {
+            ring[(dst + i) & 0xFFFF] = ring[(src + i) & 0xFFFF];
+            wave_sync();
+        }
+    } else {  // periodic: byte i repeats byte i mod d
+        for (uint32_t i = lane; i < L; i += 64) ring[(dst + i) & 0xFFFF] = ring[(src + i % d) & 0xFFFF];
+    }
+    wave_sync();
+}
+
+struct SkState {
+    uint64_t p, rb, pos, flushed;
+    uint32_t err;
+    uint64_t* cyc;  // optional phase counters (6)
+};
+
+// the block loop proper, out of line (its own register allocation) with explicit LDS / global
+// pointers (a flat pointer would send every ring and table read through the flat path)
+__device__ __attribute__((noinline)) SkState sk_loop(GlbU32* w, uint64_t nwords, uint64_t end_bytes, LdsU32* ring,
+                                                     const LdsTables* T, LdsU8* oring, GlbU8* out, uint64_t cap,
+                                                     SkState S, bool piece) {
+    const uint32_t lane = lane_id();
+    const uint64_t endb = end_bytes * 8;
+    uint64_t p = S.p, rb = S.rb, pos = S.pos, flushed = S.flushed;
+    uint64_t* const cyc = S.cyc;
+    uint64_t tc = cyc ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int k) {
+        if (cyc) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            cyc[k] += t1 - tc;
+            tc = t1;
+        }
+    };
+    auto flush = [&]() {
+        const uint64_t hi = pos < cap ? pos : cap;
+        for (uint64_t i = flushed + lane; i < hi; i += 64) out[i] = oring[i & 0xFFFF];
+        flushed = pos;
+    };
+    for (;;) {
+        // ring: words [p / 32, p / 32 + 7) (a token at p + 127 ends within 48 bits)
+        const uint64_t w0 = p >> 5;
+        if (w0 < rb || w0 + 10 >= rb + FB_RW) {
+            rb = w0;
+            for (uint64_t i = w0 + lane; i < w0 + FB_RW; i += 64) {
+                uint32_t v = 0;
+                if (i < nwords) {
+                    v = w[i];
+                    const uint64_t lim = end_bytes - 4 * i;
+                    if (lim < 4) v &= (1u << (8 * lim)) - 1u;
+                }
+                ring[i % FB_RW] = v;
+            }
+            wave_sync();
+        }
+        stamp(4);
+        uint32_t La, da, Lb, db;
+        const uint32_t ia = sk_token(ring, T, p + lane, &La, &da);       // offsets 0..63
+        const uint32_t ib = sk_token(ring, T, p + 64 + lane, &Lb, &db);  // offsets 64..127
+        if (cyc) __builtin_amdgcn_s_waitcnt(0);
+        stamp(0);
+        // the chain of true token starts in [0, 128)
+        uint64_t Ma = 0, Mb = 0;
+        uint32_t q = 0, stopk = SK_LIT;
+        while (q < 128) {
+            uint32_t t;
+            if (q < 64) {
+                Ma |= 1ull << q;
+                t = (uint32_t)__builtin_amdgcn_readlane((int)ia, (int)q);
+            } else {
+                Mb |= 1ull << (q - 64);
+                t = (uint32_t)__builtin_amdgcn_readlane((int)ib, (int)(q - 64));
+            }
+            q += t & 255;
+            if ((t >> 8) >= SK_EOB) {
+                stopk = t >> 8;
+                break;
+            }
+        }
+        stamp(1);
+        const bool ona = (Ma >> lane) & 1ull, onb = (Mb >> lane) & 1ull;
+        const uint32_t ka = ia >> 8, kb = ib >> 8;
+        // over-read: a chain token ending past the stream (the reference throws there)
+        if (__ballot((ona && ka != SK_BAD && p + lane + (ia & 255) > endb) ||
+                     (onb && kb != SK_BAD && p + 64 + lane + (ib & 255) > endb))) {
+            S.err = SEGF_OVERREAD;
+            break;
+        }
+        // output offsets: literals count one (mbcnt), matches their length (a scalar loop over
+        // the few match lanes)
+        const bool la = ona && ka == SK_LIT, lb = onb && kb == SK_LIT;
+        bool ma = ona && ka == SK_MATCH && La && da, mb = onb && kb == SK_MATCH && Lb && db;
+        const uint64_t mla = __ballot(la), mlb = __ballot(lb);
+        uint32_t offa = __builtin_amdgcn_mbcnt_hi((uint32_t)(mla >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mla, 0u));
+        uint32_t offb = __builtin_amdgcn_mbcnt_hi((uint32_t)(mlb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mlb, 0u));
+        uint32_t tot = (uint32_t)__popcll(mla);
+        bool xref = false;
+        for (uint64_t m = __ballot(ma); m; m &= m - 1) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(m);
+            const uint32_t Lk = (uint32_t)__builtin_amdgcn_readlane((int)La, (int)k);
+            const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)da, (int)k);
+            const uint32_t ok = (uint32_t)__builtin_amdgcn_readlane((int)offa, (int)k);
+            if ((uint64_t)dk > pos + ok) {  // before the stream start: the reference copies nothing
+                xref = true;
+                if (lane == k) ma = false;
+                continue;
+            }
+            if (lane > k) offa += Lk;
+            tot += Lk;
+        }
+        offb += tot;
+        tot += (uint32_t)__popcll(mlb);
+        for (uint64_t m = __ballot(mb); m; m &= m - 1) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(m);
+            const uint32_t Lk = (uint32_t)__builtin_amdgcn_readlane((int)Lb, (int)k);
+            const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)db, (int)k);
+            const uint32_t ok = (uint32_t)__builtin_amdgcn_readlane((int)offb, (int)k);
+            if ((uint64_t)dk > pos + ok) {
+                xref = true;
+                if (lane == k) mb = false;
+                continue;
+            }
+            if (lane > k) offb += Lk;
+            tot += Lk;
+        }
+        if (xref && piece) {  // a piece of a larger stream: a reference before it is an error
+            S.err = SEGF_XREF;
+            break;
+        }
+        stamp(2);
+        if (la) oring[(pos + offa) & 0xFFFF] = (uint8_t)La;
+        if (lb) oring[(pos + offb) & 0xFFFF] = (uint8_t)Lb;
+        wave_sync();
+        for (uint64_t m = __ballot(ma); m; m &= m - 1) {
+            const int k = __builtin_ctzll(m);
+            sk_copy(oring, pos + (uint32_t)__builtin_amdgcn_readlane((int)offa, k),
+                    (uint32_t)__builtin_amdgcn_readlane((int)da, k), (uint32_t)__builtin_amdgcn_readlane((int)La, k));
+        }
+        for (uint64_t m = __ballot(mb); m; m &= m - 1) {
+            const int k = __builtin_ctzll(m);
+            sk_copy(oring, pos + (uint32_t)__builtin_amdgcn_readlane((int)offb, k),
+                    (uint32_t)__builtin_amdgcn_readlane((int)db, k), (uint32_t)__builtin_amdgcn_readlane((int)Lb, k));
+        }
+        if (cyc) __builtin_amdgcn_s_waitcnt(0);
+        stamp(3);
+        pos += tot;
+        if (pos - flushed >= 32768) flush();
+        if (cyc) cyc[5]++;
+        p += q;
+        if (stopk == SK_BAD) {
+            S.err = SEGF_ERR_DATA;
+            break;
+        }
+        if (stopk == SK_EOB) {
+            S.err = 0;
+            break;
+        }
+    }
+    S.p = p;
+    S.rb = rb;
+    S.pos = pos;
+    S.flushed = flushed;
+    return S;
+}
+
+__device__ uint32_t decode_block(RingIn& br, const Tables& T, FlushSink& sk) {
+    SkState S{br.abspos(), br.rb, sk.pos, sk.flushed, 0, sk.cyc};
+    S = sk_loop((GlbU32*)br.w, br.nwords, br.end_bytes, (LdsU32*)br.ring, (const LdsTables*)&T, (LdsU8*)sk.ring,
+                (GlbU8*)sk.out, sk.cap, S, sk.piece);
+    br.rb = S.rb;
+    sk.pos = S.pos;
+    sk.flushed = S.flushed;
+    if (S.err) {
+        sk.err |= S.err == SEGF_XREF ? SEGF_XREF : 0u;
+        return S.err;
+    }
+    br.seek(S.p);
+    return 0;
+}
+
 __global__ __launch_bounds__(IF_NT) void k_inflate_serial(InflateArgs A, int count_only,
                                                           InflateResult* res) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[65536];
@@ -1013,7 +1264,11 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_serial(InflateArgs A, int cou
     RingIn br;
     br.init(A.in_words, A.misalign, A.n, inring);
     br.seek(A.misalign * 8);
-    FlushSink sk{ring, 0, 0, A.out, count_only ? 0 : A.cap, 0, (A.flags & DMX_IFLAG_PIECE) != 0};
+    __shared__ uint64_t cyc[6];
+    if (threadIdx.x < 6) cyc[threadIdx.x] = 0;
+    __syncthreads();
+    FlushSink sk{ring, 0, 0, A.out, count_only ? 0 : A.cap, 0, (A.flags & DMX_IFLAG_PIECE) != 0,
+                 A.dbg ? cyc : nullptr};
     uint64_t end_byte = 0;
     bool fin = false;
     const uint32_t err =
@@ -1025,6 +1280,7 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_serial(InflateArgs A, int cou
         res->fin_index = 0;
         res->end_byte = fin ? end_byte - A.misalign : 0;
     }
+    if (threadIdx.x < 6) res->cycles[threadIdx.x] = cyc[threadIdx.x];
 }
 
 // ---------------------------------------------------------------------------------------

@@ -46,7 +46,8 @@ typedef struct dmx_config {
                                dmx_inflate, dmx_inflate_alloc, hence deflate::compress and
                                inflate::decompress) splits each large call over N devices,
                                `device`, device + 1, ... (mod the visible count: fewer GPUs than N
-                               run several shards each).  Deflate: contiguous segment-aligned
+                               run several shards each; more than 8 per visible GPU is
+                               DMX_ERR_ARG).  Deflate: contiguous segment-aligned
                                shards, NOT_FINAL except the last -- segments are independent
                                (deflate.hpp:689-697), so the bytes equal the one-device stream.
                                Inflate: cuts at segment starts proven by a piece-mode decode

@@ -74,3 +74,11 @@ def test_n_gpus_concatenated_streams_match_one_device(ctx, oracle):
         assert multi.decompress(s) == want
     finally:
         multi.close()
+
+
+def test_n_gpus_bound():
+    """A garbage n_gpus (e.g. from a caller built against another dmx_config layout) is
+    DMX_ERR_ARG, not thousands of sub-contexts."""
+    with pytest.raises(dmx.DmxError) as e:
+        dmx.Context(n_gpus=1 << 20)
+    assert e.value.code == dmx.DMX_ERR_ARG

@@ -9,10 +9,11 @@
 # which gpurun merges back), then here `bash tools/profile_all.sh collect r03` (profiles/).
 set -e
 mode=${1:-run}
-tag=${2:-r03}
+tag=${2:-r05}
 P=gpurun_out/prof_all
 SPECS=${SPECS:-"repeat:2 text:2 mixed:2 random:2 zeros:2 bmp:2 text:3"}
 N=1073741824
+export DMX_ROUND=$tag
 if [ "$mode" = collect ]; then
   for spec in $SPECS; do
     c=${spec%%:*}; l=${spec#*:}
