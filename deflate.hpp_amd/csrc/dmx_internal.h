@@ -131,8 +131,8 @@ hipError_t launch_inflate_validate(const InflateArgs& A, ValidateWords* W, Infla
 
 // block-parallel inflate of arbitrary streams (inflate_blocks.hip, path 5)
 struct FbUnit {         // per-unit record written by k_fb_pdecode / k_fb_decode
-    uint64_t start;     // stream bit of the unit's first token (a block header, or for a virtual
-                        // unit the token boundary its warm-up found)
+    uint64_t start;     // stream bit of the unit's first token (a block header, or a token
+                        // boundary inside a block: region and repair units)
     uint64_t end;       // stream bit where it stopped: past its last block, or (soft stop) the
                         // first token boundary at or past its stop
     uint64_t size;      // output bytes
@@ -157,13 +157,11 @@ constexpr uint64_t FB_AT_HEADER = ~0ull;       // the unit ended at a block head
 // how a unit starts (vmode)
 enum : uint8_t {
     FB_V_HEADER = 0,   // at a block header (bit 0, a scanned dynamic or stored header)
-    FB_V_VIRTUAL = 1,  // near its start bit inside a long run of blocks: warm-up decode from
-                       // before it, under the code of vhdr's block (a guess the chain verifies)
     FB_V_EXACT = 2,    // exactly at its start bit inside a block whose code is vhdr (a repair)
 };
 constexpr uint32_t SEGF_SOFT = 1u << 30;  // internal: decode_huffman reached the soft stop
 // FbUnit flag (not an error): the unit's decode passed at least one block header after its
-// start, so the BFINAL bit of its end state is its own reading, not a virtual unit's guess
+// start (diagnostics)
 constexpr uint32_t SEGF_CROSSED = 1u << 29;
 constexpr uint32_t SEGF_ERRORS = ~(SEGF_FINAL | SEGF_CROSSED);
 uint64_t fb_scan_chunks(uint64_t n);

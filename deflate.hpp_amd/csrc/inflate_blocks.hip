@@ -400,7 +400,7 @@ struct FbDecodeArgs {
     const uint64_t* starts;
     const uint64_t* stops;   // FB_STOP_* flags
     const uint8_t* vmode;    // FB_V_*
-    const uint64_t* vhdr;    // code state of FB_V_VIRTUAL / FB_V_EXACT units
+    const uint64_t* vhdr;    // code state of FB_V_EXACT units
     uint64_t nunits;
     uint64_t u0;             // this launch decodes units u0 + blockIdx.x
     const uint64_t* tokoff;
@@ -565,13 +565,6 @@ __global__ __launch_bounds__(64) void k_fb_decode(FbDecodeArgs A) {
     __shared__ uint32_t ring[FB_RW];
     const uint64_t u = A.u0 + blockIdx.x;  // (the grid is the launch's unit count)
     const uint8_t vm = A.vmode[u];
-    if (vm == FB_V_VIRTUAL) {  // a guessed start: only the lane-parallel decoder's warm-up finds
-        if (threadIdx.x == 0) { // the token boundary near it (the chain repairs around it)
-            FbUnit r{A.starts[u], A.starts[u], 0, FB_AT_HEADER, 0, SEGF_ERR_DATA};
-            A.units[u] = r;
-        }
-        return;
-    }
     fb_serial(A, u, T, ring, A.starts[u], 0, 0, true, vm == FB_V_EXACT ? A.vhdr[u] : FB_AT_HEADER);
 }
 
@@ -618,7 +611,6 @@ struct FbpSmem {
     uint32_t kind;            // 0 parallel, 1 serial from the unit start, 2 serial continuation,
                               // 3 an error the serial decoder would report (S.err), 4 again
     uint32_t btype, bfinal, hs, nst, words, bytes, err;
-    uint32_t vs0;             // FB_V_VIRTUAL: the first token boundary the warm-up found
     uint32_t midend;          // the unit stopped inside a block (soft stop)
     uint32_t crossed;         // the settled path passed a fixed-block header (TK_NOP)
     uint64_t ws, he, hecap, endbit;
@@ -677,7 +669,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             btype = (h >> 1) & 3;
             bfinal = h & 1;
             state = (btype == 1 ? FB_STATE_FIXED : start) | (bfinal ? FB_STATE_FINAL : 0ull);
-        } else {  // inside a block: the code of vhdr's block (a virtual unit's is a guess)
+        } else {  // inside a block (FB_V_EXACT): the code of vhdr's block
             const uint64_t vh = A.vhdr[u];
             const uint32_t h = (vh & FB_STATE_FIXED) ? 2u : hdr3(base + (vh & FB_STATE_POS));
             btype = ((h >> 1) & 3) == 2 ? 2u : 1u;  // a stored or fixed first block: fixed blocks follow
@@ -686,8 +678,8 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
         }
         // The block run must end by he: first the stop (the next unit start), then -- if no end of
         // block comes before a hard stop: a false header hit inside the block -- as far as the
-        // staging reaches.  Staged: as many words as fit (a virtual unit's from its warm-up on).
-        const uint64_t ws = (vm == FB_V_VIRTUAL ? b - FBP_WARM - 64 : b) >> 5;
+        // staging reaches.  Staged: as many words as fit.
+        const uint64_t ws = b >> 5;
         const uint64_t hecap = min(nbits, (ws + FBP_IN - 16) * 32 - base);
         if (!weak && (btype == 1 || btype == 2) && start + (vm == FB_V_HEADER ? 3 : 0) < hecap) {
             kind = 0;
@@ -696,7 +688,6 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             S.he = min(stop, hecap);
             S.hecap = hecap;
         }
-        if (vm == FB_V_VIRTUAL && kind != 0) kind = 3;  // no serial decode from a guessed start
         // a region head whose first block is not dynamic: the unit is empty, the region map
         // takes the run of blocks from its header on
         if ((A.stops[u] & FB_STOP_REGION) && vm == FB_V_HEADER && btype != 2) kind = 5;
@@ -705,7 +696,6 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
         S.btype = btype;
         S.bfinal = bfinal;
         S.vstate = state;
-        S.vs0 = 0;
         S.midend = 0;
         S.crossed = 0;
     }
@@ -744,7 +734,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
                     S.kind = 3;
                     S.err = err;
                 } else if (base + S.hecap - ws * 32 <= hs) {
-                    S.kind = vm == FB_V_VIRTUAL ? 3u : 1u;
+                    S.kind = 1u;
                     if (A.stats) atomicAdd(&A.stats[4], 1u);
                 } else if (base + S.he - ws * 32 <= hs) {
                     S.he = S.hecap;  // the stop lies inside the header
@@ -783,10 +773,9 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
         __syncthreads();
         // ---- 2. warm-up, first pass ----
         uint32_t s0 = sp;
-        if ((r > 0 || vm == FB_V_VIRTUAL) && r < nl) {
-            // (a virtual unit's range 0 warms up before the unit's start bit, inside the staging)
+        if (r > 0 && r < nl) {
             int32_t p = (int32_t)sp - (int32_t)FBP_WARM;
-            if (vm != FB_V_VIRTUAL && p < 0) p = 0;
+            if (p < 0) p = 0;
             uint32_t pa = (uint32_t)((int32_t)hs + p);
             bool ok = true;
             while (p < (int32_t)sp) {
@@ -797,7 +786,6 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             }
             if (ok && p < (int32_t)sp1) s0 = (uint32_t)p;
         }
-        if (r == 0) S.vs0 = s0;
         uint32_t e1, st1 = 0, w1 = 0, b1 = 0;
         {
             uint32_t p = s0, pa = hs + s0, pn = 0;
@@ -862,7 +850,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
         }
         // ---- 4. the block's end; recount ranges that moved ----
         if (t == 0 && !settled) {
-            S.kind = vm == FB_V_VIRTUAL ? 3u : 1u;
+            S.kind = 1u;
             if (A.stats) atomicAdd(&A.stats[5], 1u);
         } else if (t == 0 && te >= (uint32_t)FBP_NT) {
             if (soft && S.he == stop) {
@@ -872,7 +860,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
                 S.endbit = S.ws * 32 + hs + S.endp[nl - 1] - base;
             } else {
                 // no end of block before he: again up to the staging's end, else serially
-                S.kind = S.he < S.hecap ? 4u : (vm == FB_V_VIRTUAL ? 3u : 1u);
+                S.kind = S.he < S.hecap ? 4u : (1u);
                 if (S.kind == 4) S.he = S.hecap;
                 if (A.stats) atomicAdd(&A.stats[6], 1u);
             }
@@ -945,7 +933,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             S.words = tw;
             S.bytes = tb;
             if (tw > cap) {
-                S.kind = vm == FB_V_VIRTUAL ? 3u : 1u;
+                S.kind = 1u;
                 if (A.stats) atomicAdd(&A.stats[8], 1u);
             }
         }
@@ -984,7 +972,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             }
             if (pn) tk[nw++] = (pn << 24) | pend;
             if (drop) {
-                S.kind = vm == FB_V_VIRTUAL ? 3u : 1u;
+                S.kind = 1u;
                 if (A.stats) atomicAdd(&A.stats[9], 1u);
             }
         }
@@ -1011,8 +999,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
     }
     const uint32_t kind = S.kind;
     if (A.stats && t == 0 && kind != 5) atomicAdd(&A.stats[weak ? 3 : kind == 3 ? 0 : kind], 1u);
-    // a virtual unit starts at the token boundary its warm-up found
-    const uint64_t rstart = vm == FB_V_VIRTUAL && kind != 3 ? S.ws * 32 + S.hs + S.vs0 - base : start;
+    const uint64_t rstart = start;
     if (kind == 0 || kind == 3 || kind == 5) {
         if (t == 0) {
             FbUnit rec;
