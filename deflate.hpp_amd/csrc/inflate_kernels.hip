@@ -950,6 +950,7 @@ struct FlushSink {
     uint32_t err;
     bool piece;  // a reference before the first byte is an error (DMX_IFLAG_PIECE)
     uint64_t* cyc;  // optional phase counters (sk_loop)
+    uint8_t* flag;  // 128 zeroed bytes of LDS (sk_loop's chain marks)
     __device__ bool full() const { return false; }
     __device__ void flush() {  // [flushed, pos) ring -> out (at most 64 KiB, held by the ring)
         const uint64_t hi = pos < cap ? pos : cap;
@@ -1034,46 +1035,46 @@ typedef __attribute__((address_space(1))) uint8_t GlbU8;
 typedef __attribute__((address_space(1))) const uint32_t GlbU32;
 
 // the token that would start at bit b: info = length in bits | kind << 8; *L = literal byte or
-// match length, *d = distance (0: symbols 286+ / 30+, no copy)
-__device__ __forceinline__ uint32_t sk_token(const LdsU32* ring, const LdsTables* T, uint64_t b, uint32_t* L,
+// match length, *d = distance (0: symbols 286+ / 30+, no copy).  Branch-free: every lane reads
+// both tables; codes longer than the primary tables take one wave-uniform branch (rare).
+__device__ __noinline__ void sk_slow_lit(const LdsTables* T, uint32_t v, uint32_t* e) {
+    uint32_t sym, len;
+    *e = slow_decode(T->lm, T->lsorted, v & 0x7FFF, LUT_L + 1, &sym, &len) ? lit_entry(sym, len) : 0u;
+}
+__device__ __noinline__ void sk_slow_dist(const LdsTables* T, uint32_t dv, uint32_t* de) {
+    uint32_t ds, dl;
+    *de = slow_decode(T->dm, T->dsorted, dv & 0x7FFF, LUT_D + 1, &ds, &dl) ? dist_entry(ds, dl) : 0u;
+}
+__device__ __forceinline__ uint32_t sk_token(const LdsU32* ring, const LdsTables* T, uint32_t b, uint32_t* L,
                                              uint32_t* d) {
-    const uint32_t wi = (uint32_t)(b >> 5);
-    const uint32_t sh = (uint32_t)(b & 31);
+    const uint32_t wi = b >> 5, sh = b & 31;
     const uint32_t x0 = ring[wi % FB_RW], x1 = ring[(wi + 1) % FB_RW], x2 = ring[(wi + 2) % FB_RW];
     const uint32_t v = __builtin_amdgcn_alignbit(x1, x0, sh);
     const uint64_t W = (uint64_t)v | ((uint64_t)__builtin_amdgcn_alignbit(x2, x1, sh) << 32);
     uint32_t e = T->llut[v & ((1u << LUT_L) - 1)];
-    if (!e) {
-        uint32_t sym, len;
-        e = slow_decode(T->lm, T->lsorted, v & 0x7FFF, LUT_L + 1, &sym, &len) ? lit_entry(sym, len) : 0u;
+    if (__ballot(e == 0)) {
+        if (!e) sk_slow_lit(T, v, &e);
     }
-    *L = 0;
-    *d = 0;
-    if (!e) return SK_BAD << 8;
-    const uint32_t cl = e & 15, ty = (e >> 4) & 3;
-    if (ty == 0) {
-        *L = e >> 16;
-        return cl | (SK_LIT << 8);
-    }
-    if (ty == 1) return cl | (SK_EOB << 8);
-    const uint32_t ex = (e >> 6) & 15;
-    *L = (e >> 16) + ((v >> cl) & ((1u << ex) - 1u));
+    const uint32_t cl = e & 15, ty = (e >> 4) & 3, ex = (e >> 6) & 15;
     const uint32_t q = cl + ex;
     const uint32_t dv = (uint32_t)(W >> q);
     uint32_t de = T->dlut[dv & ((1u << LUT_D) - 1)];
-    if (!de) {
-        uint32_t ds, dl;
-        de = slow_decode(T->dm, T->dsorted, dv & 0x7FFF, LUT_D + 1, &ds, &dl) ? dist_entry(ds, dl) : 0u;
+    const bool ism = ty == 2;
+    if (__ballot(ism && de == 0)) {
+        if (ism && !de) sk_slow_dist(T, dv, &de);
     }
-    if (!de) return SK_BAD << 8;
     const uint32_t dl = de & 15, dx = (de >> 6) & 15;
-    *d = (de >> 16) + ((dv >> dl) & ((1u << dx) - 1u));
-    return (q + dl + dx) | (SK_MATCH << 8);
+    const uint32_t lenv = (e >> 16) + ((v >> cl) & ((1u << ex) - 1u));  // literal byte or match length
+    *L = ty == 1 ? 0u : lenv;
+    *d = ism ? (de >> 16) + ((dv >> dl) & ((1u << dx) - 1u)) : 0u;
+    const uint32_t kind = !e || (ism && !de) ? SK_BAD : ty == 0 ? SK_LIT : ty == 1 ? SK_EOB : SK_MATCH;
+    const uint32_t tl = ism ? q + dl + dx : cl;
+    return tl | (kind << 8);
 }
 
-__device__ __forceinline__ void sk_copy(LdsU8* ring, uint64_t dst, uint32_t d, uint32_t L) {
+__device__ __forceinline__ void sk_copy(LdsU8* ring, uint32_t dst, uint32_t d, uint32_t L) {
     const uint32_t lane = lane_id();
-    const uint64_t src = dst - d;
+    const uint32_t src = dst - d;  // (ring positions: the low 16 bits matter)
     if (d >= L || d >= 64) {  // each group of 64 reads only bytes written before it
         for (uint32_t i = lane; i < L; i += 64) {
             ring[(dst + i) & 0xFFFF] = ring[(src + i) & 0xFFFF];
@@ -1095,16 +1096,18 @@ struct SkState {
 // pointers (a flat pointer would send every ring and table read through the flat path)
 __device__ __attribute__((noinline)) SkState sk_loop(GlbU32* w, uint64_t nwords, uint64_t end_bytes, LdsU32* ring,
                                                      const LdsTables* T, LdsU8* oring, GlbU8* out, uint64_t cap,
-                                                     SkState S, bool piece) {
+                                                     SkState S, bool piece, LdsU8* flag) {
     const uint32_t lane = lane_id();
     const uint64_t endb = end_bytes * 8;
     uint64_t p = S.p, rb = S.rb, pos = S.pos, flushed = S.flushed;
     uint64_t* const cyc = S.cyc;
-    uint64_t tc = cyc ? __builtin_amdgcn_s_memtime() : 0;
+    const bool timed = cyc != nullptr;
+    uint64_t tc = timed ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t cy[6] = {0, 0, 0, 0, 0, 0};  // (registers: a memory update per stamp would skew them)
     auto stamp = [&](int k) {
-        if (cyc) {
+        if (timed) {
             const uint64_t t1 = __builtin_amdgcn_s_memtime();
-            cyc[k] += t1 - tc;
+            cy[k] += t1 - tc;
             tc = t1;
         }
     };
@@ -1131,33 +1134,72 @@ __device__ __attribute__((noinline)) SkState sk_loop(GlbU32* w, uint64_t nwords,
         }
         stamp(4);
         uint32_t La, da, Lb, db;
-        const uint32_t ia = sk_token(ring, T, p + lane, &La, &da);       // offsets 0..63
-        const uint32_t ib = sk_token(ring, T, p + 64 + lane, &Lb, &db);  // offsets 64..127
-        if (cyc) __builtin_amdgcn_s_waitcnt(0);
+        const uint32_t ia = sk_token(ring, T, (uint32_t)p + lane, &La, &da);       // offsets 0..63
+        const uint32_t ib = sk_token(ring, T, (uint32_t)p + 64 + lane, &Lb, &db);  // offsets 64..127
+        if (timed) __builtin_amdgcn_s_waitcnt(0);
         stamp(0);
-        // the chain of true token starts in [0, 128)
-        uint64_t Ma = 0, Mb = 0;
-        uint32_t q = 0, stopk = SK_LIT;
+        // The chain of true token starts in [0, 128), walked four tokens per step.  N1(o) = the
+        // position after the token at offset o (a token that ends the block -- end of block, no
+        // code -- steps by 128 + its length, past the window); N2 = N1(N1), N3 = N1(N2), N4 =
+        // N2(N2), gathered across lanes with ds_bpermute (a position >= 128 stays where it is).
+        // The scalar loop follows N4 from 0 and records the entries e it visits; the chain is
+        // {e, N1(e), N2(e), N3(e)}, marked in parallel through an LDS flag per offset.
+        const uint32_t n1a = min(lane + (ia & 255) + ((ia >> 8) >= SK_EOB ? 128u : 0u), 255u);
+        const uint32_t n1b = min(64 + lane + (ib & 255) + ((ib >> 8) >= SK_EOB ? 128u : 0u), 255u);
+        auto gather = [](uint32_t xa, uint32_t xb, uint32_t idx) -> uint32_t {  // X[idx], idx < 128
+            const int sel = (int)((idx & 63) << 2);
+            const uint32_t va = (uint32_t)__builtin_amdgcn_ds_bpermute(sel, (int)xa);
+            const uint32_t vb = (uint32_t)__builtin_amdgcn_ds_bpermute(sel, (int)xb);
+            return idx < 64 ? va : idx < 128 ? vb : idx;
+        };
+        const uint32_t n2a = gather(n1a, n1b, n1a), n2b = gather(n1a, n1b, n1b);
+        const uint32_t n3a = gather(n1a, n1b, n2a), n3b = gather(n1a, n1b, n2b);
+        const uint32_t n4a = gather(n2a, n2b, n2a), n4b = gather(n2a, n2b, n2b);
+        uint64_t Ea = 0, Eb = 0;
+        uint32_t q = 0;
+        do {
+            Ea |= 1ull << q;
+            q = (uint32_t)__builtin_amdgcn_readlane((int)n4a, (int)q);
+        } while (q < 64);
         while (q < 128) {
-            uint32_t t;
-            if (q < 64) {
-                Ma |= 1ull << q;
-                t = (uint32_t)__builtin_amdgcn_readlane((int)ia, (int)q);
-            } else {
-                Mb |= 1ull << (q - 64);
-                t = (uint32_t)__builtin_amdgcn_readlane((int)ib, (int)(q - 64));
-            }
-            q += t & 255;
+            Eb |= 1ull << (q - 64);
+            q = (uint32_t)__builtin_amdgcn_readlane((int)n4b, (int)(q - 64));
+        }
+        const bool ea = (Ea >> lane) & 1ull, eb = (Eb >> lane) & 1ull;
+        if (ea) {
+            flag[lane] = 1;
+            if (n1a < 128) flag[n1a] = 1;
+            if (n2a < 128) flag[n2a] = 1;
+            if (n3a < 128) flag[n3a] = 1;
+        }
+        if (eb) {
+            flag[64 + lane] = 1;
+            if (n1b < 128) flag[n1b] = 1;
+            if (n2b < 128) flag[n2b] = 1;
+            if (n3b < 128) flag[n3b] = 1;
+        }
+        wave_sync();
+        const uint64_t Ma = __ballot(flag[lane] != 0), Mb = __ballot(flag[64 + lane] != 0);
+        flag[lane] = 0;
+        flag[64 + lane] = 0;
+        // a token that ends the block: the last chain member, if its kind says so
+        uint32_t stopk = SK_LIT;
+        {
+            const uint32_t last = Mb ? 127u - (uint32_t)__clzll(Mb) : 63u - (uint32_t)__clzll(Ma);
+            const uint32_t t = last < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)ia, (int)last)
+                                         : (uint32_t)__builtin_amdgcn_readlane((int)ib, (int)(last - 64));
             if ((t >> 8) >= SK_EOB) {
                 stopk = t >> 8;
-                break;
+                q = last + (t & 255);
             }
         }
         stamp(1);
         const bool ona = (Ma >> lane) & 1ull, onb = (Mb >> lane) & 1ull;
         const uint32_t ka = ia >> 8, kb = ib >> 8;
-        // over-read: a chain token ending past the stream (the reference throws there)
-        if (__ballot((ona && ka != SK_BAD && p + lane + (ia & 255) > endb) ||
+        // over-read: a chain token ending past the stream (the reference throws there); a token
+        // ends within 48 bits of its start, so only the stream's last window can
+        if (p + 128 + 48 > endb &&
+            __ballot((ona && ka != SK_BAD && p + lane + (ia & 255) > endb) ||
                      (onb && kb != SK_BAD && p + 64 + lane + (ib & 255) > endb))) {
             S.err = SEGF_OVERREAD;
             break;
@@ -1171,15 +1213,19 @@ __device__ __attribute__((noinline)) SkState sk_loop(GlbU32* w, uint64_t nwords,
         uint32_t offb = __builtin_amdgcn_mbcnt_hi((uint32_t)(mlb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mlb, 0u));
         uint32_t tot = (uint32_t)__popcll(mla);
         bool xref = false;
+        // (a distance reaches before the stream start only within its first 32 KiB)
+        const bool early = pos < 32768;
         for (uint64_t m = __ballot(ma); m; m &= m - 1) {
             const uint32_t k = (uint32_t)__builtin_ctzll(m);
             const uint32_t Lk = (uint32_t)__builtin_amdgcn_readlane((int)La, (int)k);
-            const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)da, (int)k);
-            const uint32_t ok = (uint32_t)__builtin_amdgcn_readlane((int)offa, (int)k);
-            if ((uint64_t)dk > pos + ok) {  // before the stream start: the reference copies nothing
-                xref = true;
-                if (lane == k) ma = false;
-                continue;
+            if (early) {
+                const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)da, (int)k);
+                const uint32_t ok = (uint32_t)__builtin_amdgcn_readlane((int)offa, (int)k);
+                if ((uint64_t)dk > pos + ok) {  // before the stream start: the reference copies nothing
+                    xref = true;
+                    if (lane == k) ma = false;
+                    continue;
+                }
             }
             if (lane > k) offa += Lk;
             tot += Lk;
@@ -1189,12 +1235,14 @@ __device__ __attribute__((noinline)) SkState sk_loop(GlbU32* w, uint64_t nwords,
         for (uint64_t m = __ballot(mb); m; m &= m - 1) {
             const uint32_t k = (uint32_t)__builtin_ctzll(m);
             const uint32_t Lk = (uint32_t)__builtin_amdgcn_readlane((int)Lb, (int)k);
-            const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)db, (int)k);
-            const uint32_t ok = (uint32_t)__builtin_amdgcn_readlane((int)offb, (int)k);
-            if ((uint64_t)dk > pos + ok) {
-                xref = true;
-                if (lane == k) mb = false;
-                continue;
+            if (early) {
+                const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)db, (int)k);
+                const uint32_t ok = (uint32_t)__builtin_amdgcn_readlane((int)offb, (int)k);
+                if ((uint64_t)dk > pos + ok) {
+                    xref = true;
+                    if (lane == k) mb = false;
+                    continue;
+                }
             }
             if (lane > k) offb += Lk;
             tot += Lk;
@@ -1204,24 +1252,25 @@ __device__ __attribute__((noinline)) SkState sk_loop(GlbU32* w, uint64_t nwords,
             break;
         }
         stamp(2);
-        if (la) oring[(pos + offa) & 0xFFFF] = (uint8_t)La;
-        if (lb) oring[(pos + offb) & 0xFFFF] = (uint8_t)Lb;
+        const uint32_t pos32 = (uint32_t)pos;
+        if (la) oring[(pos32 + offa) & 0xFFFF] = (uint8_t)La;
+        if (lb) oring[(pos32 + offb) & 0xFFFF] = (uint8_t)Lb;
         wave_sync();
         for (uint64_t m = __ballot(ma); m; m &= m - 1) {
             const int k = __builtin_ctzll(m);
-            sk_copy(oring, pos + (uint32_t)__builtin_amdgcn_readlane((int)offa, k),
+            sk_copy(oring, pos32 + (uint32_t)__builtin_amdgcn_readlane((int)offa, k),
                     (uint32_t)__builtin_amdgcn_readlane((int)da, k), (uint32_t)__builtin_amdgcn_readlane((int)La, k));
         }
         for (uint64_t m = __ballot(mb); m; m &= m - 1) {
             const int k = __builtin_ctzll(m);
-            sk_copy(oring, pos + (uint32_t)__builtin_amdgcn_readlane((int)offb, k),
+            sk_copy(oring, pos32 + (uint32_t)__builtin_amdgcn_readlane((int)offb, k),
                     (uint32_t)__builtin_amdgcn_readlane((int)db, k), (uint32_t)__builtin_amdgcn_readlane((int)Lb, k));
         }
-        if (cyc) __builtin_amdgcn_s_waitcnt(0);
+        if (timed) __builtin_amdgcn_s_waitcnt(0);
         stamp(3);
         pos += tot;
         if (pos - flushed >= 32768) flush();
-        if (cyc) cyc[5]++;
+        cy[5]++;
         p += q;
         if (stopk == SK_BAD) {
             S.err = SEGF_ERR_DATA;
@@ -1232,6 +1281,8 @@ __device__ __attribute__((noinline)) SkState sk_loop(GlbU32* w, uint64_t nwords,
             break;
         }
     }
+    if (timed && lane_id() == 0)
+        for (int k = 0; k < 6; k++) cyc[k] += cy[k];
     S.p = p;
     S.rb = rb;
     S.pos = pos;
@@ -1242,7 +1293,7 @@ __device__ __attribute__((noinline)) SkState sk_loop(GlbU32* w, uint64_t nwords,
 __device__ uint32_t decode_block(RingIn& br, const Tables& T, FlushSink& sk) {
     SkState S{br.abspos(), br.rb, sk.pos, sk.flushed, 0, sk.cyc};
     S = sk_loop((GlbU32*)br.w, br.nwords, br.end_bytes, (LdsU32*)br.ring, (const LdsTables*)&T, (LdsU8*)sk.ring,
-                (GlbU8*)sk.out, sk.cap, S, sk.piece);
+                (GlbU8*)sk.out, sk.cap, S, sk.piece, (LdsU8*)sk.flag);
     br.rb = S.rb;
     sk.pos = S.pos;
     sk.flushed = S.flushed;
@@ -1265,10 +1316,13 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_serial(InflateArgs A, int cou
     br.init(A.in_words, A.misalign, A.n, inring);
     br.seek(A.misalign * 8);
     __shared__ uint64_t cyc[6];
+    __shared__ uint8_t flag[128];
     if (threadIdx.x < 6) cyc[threadIdx.x] = 0;
+    flag[threadIdx.x] = 0;
+    flag[64 + threadIdx.x] = 0;
     __syncthreads();
     FlushSink sk{ring, 0, 0, A.out, count_only ? 0 : A.cap, 0, (A.flags & DMX_IFLAG_PIECE) != 0,
-                 A.dbg ? cyc : nullptr};
+                 A.dbg ? cyc : nullptr, flag};
     uint64_t end_byte = 0;
     bool fin = false;
     const uint32_t err =
