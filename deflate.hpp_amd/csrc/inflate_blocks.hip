@@ -37,7 +37,6 @@
 // serial decoder instead, so results and error codes stay the reference's.
 #include "inflate_common.h"
 
-#include <hip/hip_cooperative_groups.h>
 
 namespace dmx {
 
@@ -1459,28 +1458,6 @@ __global__ __launch_bounds__(256) void k_fb_win_jump(uint32_t* W, uint64_t nent,
     if (__ballot(left) && lane_id() == 0) atomicOr(&open[round], 1u);
 }
 
-// All rounds in one cooperative launch (every workgroup resident, a grid barrier between
-// rounds): the separate launches cost ~18 us each on C3 (10 rounds), most of it launch and drain
-// for rounds with little left.  The host falls back to one launch per round when the cooperative
-// launch is refused.
-__global__ __launch_bounds__(256) void k_fb_win_jump_all(uint32_t* W, uint64_t nent, uint32_t* open, int rounds) {
-    cooperative_groups::grid_group grid = cooperative_groups::this_grid();
-    for (int r = 0; r < rounds; r++) {
-        bool left = false;
-        for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nent; i += (uint64_t)gridDim.x * 256) {
-            uint32_t v = W[i];
-            if (v & FB_WLIT) continue;
-#pragma unroll 1
-            for (int h = 0; h < FB_HOPS && !(v & FB_WLIT); h++) v = W[v];
-            W[i] = v;
-            left |= !(v & FB_WLIT);
-        }
-        if (__ballot(left) && lane_id() == 0) atomicOr(&open[r], 1u);
-        grid.sync();
-        if (__hip_atomic_load(&open[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) break;  // (grid-uniform)
-    }
-}
-
 // ---------------------------------------------------------------------------------------
 // k_fb_final: every entry (W != nullptr) or every entry before its unit's tail (after
 // k_fb_tails).  One workgroup per FB_FIN_SPAN entries; the unit of the span's first entry is
@@ -1825,29 +1802,12 @@ hipError_t launch_fb_resolve(const uint8_t* stream, const uint64_t* starts, cons
                            img, offs, sizes, win);
         const uint32_t rounds = fb_window_rounds(nchain);
         (void)hipMemsetAsync(open, 0, rounds * 4, st);
-        // one grid-striding wave of workgroups: a round with nothing left returns in microseconds
+        // one grid-striding wave of workgroups per round: a round with nothing left returns in
+        // microseconds.  (Round 4 ran all rounds in one cooperative launch with a grid barrier
+        // between them: on C3 that took 0.36 ms against ~0.2 ms for the separate launches.)
         const uint32_t g = (uint32_t)std::min<uint64_t>((nent + 255) / 256, 1024);
-        static const uint32_t coop_max = [] {  // workgroups that fit the device at once
-            int dev = 0, per_cu = 0, ncu = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fb_win_jump_all, 256, 0) != hipSuccess ||
-                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                return 0u;
-            return (uint32_t)std::max(0, per_cu * ncu);
-        }();
-        const uint32_t gc = std::min(g, coop_max);
-        bool done = false;
-        if (gc) {
-            int rr = (int)rounds;
-            uint64_t ne = nent;
-            void* args[] = {&win, &ne, &open, &rr};
-            done = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_fb_win_jump_all), dim3(gc), dim3(256),
-                                              args, 0, st) == hipSuccess;
-            if (!done) (void)hipGetLastError();
-        }
-        if (!done)
-            for (uint32_t r = 0; r < rounds; r++)
-                hipLaunchKernelGGL(k_fb_win_jump, dim3(g), dim3(256), 0, st, win, nent, open, (int)r);
+        for (uint32_t r = 0; r < rounds; r++)
+            hipLaunchKernelGGL(k_fb_win_jump, dim3(g), dim3(256), 0, st, win, nent, open, (int)r);
     } else {
         hipLaunchKernelGGL(k_fb_tails, dim3(1), dim3(FB_TNT), 0, st, img, offs, sizes, nchain, out);
     }
