@@ -18,13 +18,14 @@ if [ "$mode" = collect ]; then
   for spec in $SPECS; do
     c=${spec%%:*}; l=${spec#*:}
     [ -d $P/s_$c$l ] || continue
-    cp $(find $P/s_$c$l -name "*kernel_stats.csv" | head -1) profiles/${tag}_kstats_${c}_L$l.csv
+    # (the newest run's file: gpurun merges every box's results into the local gpurun_out/)
+    cp $(ls -t $(find $P/s_$c$l -name "*kernel_stats.csv") | head -1) profiles/${tag}_kstats_${c}_L$l.csv
     for k in k_deflate_segments k_deflate_emit k_inflate_lanes k_inflate_resolve k_inflate_pj_list; do
       python3 tools/traffic.py $P/f_$c$l $P/w_$c$l $c:$N:$l:$k $k profiles/traffic.json || true
     done
   done
   if [ -d $P/s_c3 ]; then
-    cp $(find $P/s_c3 -name "*kernel_stats.csv" | head -1) profiles/${tag}_kstats_c3_zlib1.csv
+    cp $(ls -t $(find $P/s_c3 -name "*kernel_stats.csv") | head -1) profiles/${tag}_kstats_c3_zlib1.csv
     for k in k_fb_scan k_fb_compact k_fb_pdecode k_fb_units k_fb_win_init k_fb_win_jump k_fb_final \
              k_marker_count k_marker_write k_scan_sizes; do
       python3 tools/traffic.py $P/f_c3 $P/w_c3 c3_zlib1:$k $k profiles/traffic.json || true

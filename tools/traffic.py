@@ -12,9 +12,16 @@ import os
 import sys
 
 
+def newest(root, pattern):
+    """The newest run's file under root (gpurun merges each box's results into the local
+    gpurun_out/, so older runs' files can sit beside it: they describe other kernels)."""
+    files = glob.glob(os.path.join(root, "**", pattern), recursive=True)
+    return [max(files, key=os.path.getmtime)] if files else []
+
+
 def per_dispatch(root, counter, sub):
     vals = {}
-    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+    for f in newest(root, "*counter_collection.csv"):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if row["Counter_Name"] != counter or sub not in row.get("Kernel_Name", ""):
