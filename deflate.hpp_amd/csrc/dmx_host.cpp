@@ -72,8 +72,9 @@ struct dmx_ctx {
     int ncu = 0;                         // compute units (mode 6 grid)
     // block-parallel path (path 5): scan counts / hits / offsets, hit list, unit starts, token
     // offsets and words, unit records, chain (unit index, offset, size), 16-bit image
-    DevBuf fbc, fbh, fbo, fbl, fbs, fbt, fbk, fbu, fbch, fbco, fbcs, fbimg, fbstop, fbwin, fbopen, fbp32;
+    DevBuf fbc, fbh, fbo, fbl, fbs, fbt, fbk, fbu, fbch, fbco, fbcs, fbimg, fbstop, fbwin, fbopen;
     DevBuf fbvm, fbvh;  // per-unit start mode and code state (region and repair units)
+    DevBuf fbph;  // DMX_FB_DEBUG: k_fb_units phase cycles
     DevBuf fbreg, fbJ, fbvis;  // fixed-code regions: {E, T, first super block} + super-block regions, jumps, visits
     DevBuf ck;  // checksum scratch (checksum.hip) + the 4-byte result at its start
     bool timing = false;
@@ -299,8 +300,8 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     std::vector<uint64_t> hits(nhits);
     if (nhits) {
         if (!c->fbl.ensure(nhits * 8)) return DMX_OK;
-        HIPCHK(launch_fb_compact(c->fbc.as<uint32_t>(), c->fbo.as<uint64_t>(), c->fbh.as<uint64_t>(), nc,
-                                 c->fbl.as<uint64_t>(), st));
+        HIPCHK(launch_fb_compact(words, misalign, n, c->fbc.as<uint32_t>(), c->fbo.as<uint64_t>(),
+                                 c->fbh.as<uint64_t>(), nc, c->fbl.as<uint64_t>(), nhits, st));
         HIPCHK(hipMemcpyAsync(hits.data(), c->fbl.p, nhits * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
     }
@@ -323,6 +324,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     starts.push_back(0);
     strong.push_back(1);
     for (uint64_t h : hits) {
+        if (h & FB_HIT_REJECT) continue;
         const uint64_t b = h & ~kStored;
         if (b > starts.back()) {
             starts.push_back(b);
@@ -388,9 +390,9 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     if (upload(0, K) != DMX_OK) return DMX_ERR_DEVICE;
     const bool fb_debug = (c->diag & DIAG_FB) != 0;  // developer aid: unit outcomes, chain breaks
     uint32_t* dstats = nullptr;
-    if (fb_debug && c->fbopen.ensure(64)) {
+    if (fb_debug && c->fbopen.ensure(256)) {
         dstats = c->fbopen.as<uint32_t>();
-        HIPCHK(hipMemsetAsync(dstats, 0, 40, st));
+        HIPCHK(hipMemsetAsync(dstats, 0, 256, st));
     }
     std::vector<FbUnit> units(Kcap);
     auto decode = [&](uint64_t u0, uint64_t cnt) -> int {
@@ -404,9 +406,14 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     };
     if (decode(0, K) != DMX_OK) return DMX_ERR_DEVICE;
     if (dstats) {
-        uint32_t hs[10];
-        HIPCHK(hipMemcpyAsync(hs, dstats, 40, hipMemcpyDeviceToHost, st));
+        uint32_t hs[16];
+        unsigned long long ph[8];
+        HIPCHK(hipMemcpyAsync(hs, dstats, 64, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(ph, dstats + 16, 64, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        std::fprintf(stderr, "dmx fb: pdecode cycles per unit: stage %llu, header %llu, tables %llu, first pass %llu, "
+                     "settle %llu, recount %llu, scans %llu, words %llu\n",
+                     ph[0] / K, ph[1] / K, ph[2] / K, ph[3] / K, ph[4] / K, ph[5] / K, ph[6] / K, ph[7] / K);
         std::fprintf(stderr, "dmx fb: %llu units: %u lane-parallel, %u serial, %u serial after a parallel block, %u weak; "
                      "serial because: header %u, unsettled %u, no end of block %u, bad end %u, capacity %u, "
                      "stream-start copy %u\n",
@@ -628,13 +635,22 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         win = c->fbwin.as<uint32_t>();
         open = c->fbopen.as<uint32_t>();
     }
-    // the workgroup replay needs a 32-bit image of the output
-    uint32_t* p32 = nullptr;
-    if (!fb_serial_only(c) && c->fbp32.ensure(total * 4 + 16)) p32 = c->fbp32.as<uint32_t>();
+    unsigned long long* uph = nullptr;
+    if ((c->diag & DIAG_FB) && c->fbph.ensure(64)) {
+        uph = c->fbph.as<unsigned long long>();
+        HIPCHK(hipMemsetAsync(uph, 0, 64, st));
+    }
     HIPCHK(launch_fb_resolve(d_in, c->fbs.as<uint64_t>(), c->fbch.as<uint32_t>(), c->fbco.as<uint64_t>(),
                              c->fbcs.as<uint64_t>(), nch, c->fbt.as<uint64_t>(), c->fbk.as<uint32_t>(),
                              c->fbu.as<FbUnit>(), c->fbimg.as<uint16_t>(), total, out, &ds->fb_err, win, open,
-                             p32, st));
+                             !fb_serial_only(c), uph, st));
+    if (uph) {
+        unsigned long long ph[5];
+        HIPCHK(hipMemcpyAsync(ph, uph, sizeof(ph), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        std::fprintf(stderr, "dmx fb: k_fb_units cycles per unit: batches %llu, expansion %llu, jumping %llu (%llu rounds "
+                     "in all), write-out %llu\n", ph[0] / nch, ph[1] / nch, ph[2] / nch, ph[4], ph[3] / nch);
+    }
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     uint32_t ferr = 0;
     HIPCHK(hipMemcpyAsync(&ferr, &ds->fb_err, 4, hipMemcpyDeviceToHost, st));
@@ -1311,8 +1327,8 @@ void dmx_destroy(dmx_ctx* c) {
     for (DevBuf* b : {&c->in, &c->out, &c->slots, &c->sizes, &c->offs, &c->scal, &c->cands,
                       &c->tiles, &c->tileoffs, &c->recs, &c->status, &c->dbg, &c->ltok,
                       &c->ltokoff, &c->lntok, &c->lcaps, &c->lheavy, &c->rtmp, &c->rchain, &c->fbc, &c->fbh, &c->fbo, &c->fbl,
-                      &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg, &c->fbstop, &c->fbwin, &c->fbopen, &c->fbp32, &c->fbvm, &c->fbvh,
-                      &c->fbreg, &c->fbJ, &c->fbvis,
+                      &c->fbs, &c->fbt, &c->fbk, &c->fbu, &c->fbch, &c->fbco, &c->fbcs, &c->fbimg, &c->fbstop, &c->fbwin, &c->fbopen, &c->fbvm, &c->fbvh,
+                      &c->fbreg, &c->fbJ, &c->fbvis, &c->fbph,
                       &c->ck})
         b->release();
     for (auto& e : c->ev)

@@ -171,8 +171,12 @@ uint32_t fb_hits_per_chunk();
 hipError_t launch_fb_scan(const uint32_t* in_words, uint64_t misalign, uint64_t n,
                           uint32_t* counts, uint64_t* hits, uint64_t* offs, uint64_t* nhits,
                           hipStream_t st);
-hipError_t launch_fb_compact(const uint32_t* counts, const uint64_t* offs, const uint64_t* hits,
-                             uint64_t nchunks, uint64_t* list, hipStream_t st);
+// compacts the scan's candidates into one sorted list of count entries and runs the full header
+// test on them (k_fb_check): a candidate that fails it gets FB_HIT_REJECT
+constexpr uint64_t FB_HIT_REJECT = 1ull << 63;
+hipError_t launch_fb_compact(const uint32_t* in_words, uint64_t misalign, uint64_t n, const uint32_t* counts,
+                             const uint64_t* offs, const uint64_t* hits, uint64_t nchunks, uint64_t* list,
+                             uint64_t count, hipStream_t st);
 // hits carry bit 62 for a stored-block header; stops[u] = the next dynamic-header start after u
 // units [u0, u0 + count) of the nunits listed; vmode / vhdr as above
 // fixed-code regions (k_fb_smap + k_fb_swalk): reg = nreg x {E, T, first super block}, sbreg =
@@ -194,7 +198,7 @@ hipError_t launch_fb_decode(const uint32_t* in_words, uint64_t misalign, uint64_
 // replay + window hand-off + final resolve; *err (zeroed by the caller) becomes nonzero when a
 // copy reaches before the stream start.  win (fb_window_entries(nchain) words, 0 = not
 // available) and open (fb_window_rounds(nchain) words): the parallel hand-off; win == nullptr:
-// the serial one (k_fb_tails).  p32 (total words, or nullptr): the workgroup replay k_fb_units,
+// the serial one (k_fb_tails).  workgroup: the workgroup replay k_fb_units (pieces in LDS),
 // else the one-wave replay k_fb_replay
 uint64_t fb_window_entries(uint64_t nchain);
 uint32_t fb_window_rounds(uint64_t nchain);
@@ -202,7 +206,8 @@ hipError_t launch_fb_resolve(const uint8_t* stream, const uint64_t* starts, cons
                              const uint64_t* offs, const uint64_t* sizes, uint64_t nchain,
                              const uint64_t* tokoff, const uint32_t* tok, const FbUnit* units,
                              uint16_t* img, uint64_t total, uint8_t* out, uint32_t* err,
-                             uint32_t* win, uint32_t* open, uint32_t* p32, hipStream_t st);
+                             uint32_t* win, uint32_t* open, bool workgroup, unsigned long long* ph,
+                             hipStream_t st);
 // checksums (checksum.hip): scratch of checksum_scratch_bytes(n) bytes; results land in device
 // memory (*d_out).  CRC-32: the zero-start register; crc32_finish applies start value and xor.
 uint64_t checksum_scratch_bytes(uint64_t n);

@@ -40,11 +40,18 @@
 
 namespace dmx {
 
-constexpr uint32_t FB_SCAN_BITS = 16384;  // bit offsets tested per wavefront (2 KiB of stream)
-constexpr uint32_t FB_STEP = 2048;        // offsets per prefilter step (32 per lane)
+#ifndef DMX_FB_SCAN_BITS
+#define DMX_FB_SCAN_BITS 16384
+#endif
+#ifndef DMX_FB_STEP
+#define DMX_FB_STEP 2048
+#endif
+constexpr uint32_t FB_SCAN_BITS = DMX_FB_SCAN_BITS;  // bit offsets tested per wavefront (2 KiB of stream)
+constexpr uint32_t FB_STEP = DMX_FB_STEP;            // offsets per prefilter step (32 per lane)
 constexpr uint32_t FB_STAGE_WORDS = FB_SCAN_BITS / 32 + 128;  // + 4096 bits of header lookahead
-constexpr uint32_t FB_HITS = 48;          // hits kept per scan chunk (zlib at memLevel 1-2 writes
-                                          // blocks of a few hundred bytes)
+constexpr uint32_t FB_HITS = 96;          // candidates kept per scan chunk (true headers -- zlib at
+                                          // memLevel 1-2 writes blocks of a few hundred bytes -- and
+                                          // ~17 per chunk that pass the precode test by chance)
 constexpr uint32_t FB_RING = 32768;       // replay window (entries of 16 bits)
 constexpr uint64_t FB_HIT_STORED = 1ull << 62;  // hit flag: a stored-block header
 constexpr uint32_t FB_GROUP_MAX = 8192;   // output entries per replay group (see k_fb_replay)
@@ -62,8 +69,9 @@ __device__ __forceinline__ uint32_t fb_bits(const uint32_t* w, uint32_t p) {  //
 // lane's 128-entry precode table in LDS (symbol | length << 5, 0 = no code), built here.
 // RFC 1951 rules as zlib's inflate enforces them; A-11/A-12 streams are not block starts any
 // real encoder writes, so rejecting them only costs parallelism.
-__device__ bool fb_check_lengths(const uint32_t* w, uint32_t p, uint64_t pl, uint32_t nlit,
-                                 uint32_t ndist, uint32_t plim, uint8_t* lut) {
+template <class Bits, class Lut>
+__device__ bool fb_check_lengths(const Bits& w, uint64_t p, uint64_t pl, uint32_t nlit,
+                                 uint32_t ndist, uint64_t plim, Lut lut) {
     // canonical codes: counts per length (5-bit fields), first code per length (8-bit fields)
     uint64_t cnt = 0;
     for (uint32_t s = 0; s < 19; s++) {
@@ -76,14 +84,14 @@ __device__ bool fb_check_lengths(const uint32_t* w, uint32_t p, uint64_t pl, uin
         code = (code + (uint32_t)((cnt >> (5 * (l - 1))) & 31)) << 1;  // (no length-0 count)
         nxt |= (uint64_t)code << (8 * l);
     }
-    for (uint32_t v = 0; v < 128; v += 4) *reinterpret_cast<uint32_t*>(lut + v) = 0;
+    lut.clear();
     for (uint32_t s = 0; s < 19; s++) {
         const uint32_t l = (uint32_t)(pl >> (3 * s)) & 7;
         if (!l) continue;
         const uint32_t c = (uint32_t)(nxt >> (8 * l)) & 0xFF;
         nxt += 1ull << (8 * l);
         const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);
-        for (uint32_t v = r; v < 128; v += 1u << l) lut[v] = (uint8_t)(s | (l << 5));
+        for (uint32_t v = r; v < 128; v += 1u << l) lut.set(v, s | (l << 5));
     }
     const uint32_t total = nlit + ndist;
     uint32_t i = 0, prev = 0;
@@ -91,8 +99,8 @@ __device__ bool fb_check_lengths(const uint32_t* w, uint32_t p, uint64_t pl, uin
     bool eob = false;
     while (i < total) {
         if (p > plim) return false;  // longer than any header a real encoder writes
-        const uint32_t v = fb_bits(w, p);
-        const uint32_t e = lut[v & 127];
+        const uint32_t v = w.peek(p);
+        const uint32_t e = lut.get(v & 127);
         if (!e) return false;
         const uint32_t sym = e & 31, len = e >> 5;
         p += len;
@@ -128,20 +136,21 @@ __device__ bool fb_check_lengths(const uint32_t* w, uint32_t p, uint64_t pl, uin
     return eob && kl == 32768 && (kd == 32768 || nd <= 1);
 }
 
-// One wavefront per FB_SCAN_BITS offsets, in three stages so that each test runs on full waves:
+// One wavefront per FB_SCAN_BITS offsets, in two stages so that each test runs on full waves:
 //   0. prefilter, 32 offsets per lane at once with 64-bit word arithmetic on the staged bits:
 //      BTYPE 2, HLIT <= 29, HDIST <= 29 (~21 % of random offsets pass); byte-aligned offsets with
 //      BTYPE 0 get the stored-header test (LEN / NLEN = ~LEN, data inside the stream) directly;
 //   1. the survivors, queued in offset order, one per lane: a complete precode whose last sent
-//      length is nonzero (~0.5 % pass);
-//   2. those, queued again, one per lane: fb_check_lengths.
-// Hits come out in offset order; the chunk keeps its first FB_HITS.
+//      length is nonzero (~0.5 % pass).
+// The chunk keeps its first FB_HITS candidates in offset order; k_fb_check then runs the full
+// code-length test on all chunks' candidates at once, one per lane (round 4 ran it per chunk at
+// the end of the scan: a few lanes of each wave busy for the longest test, and its per-lane
+// tables limited the scan to two waves per SIMD).
 // stage 1: HCLEN + 4 precode lengths (3 bits each, in the kPerm order) form a complete code
 // and the last one sent is nonzero (zlib / libdeflate / libdmx send HCLEN up to the last nonzero
-// length, >= 4)
-__device__ __forceinline__ bool fb_precode_ok(uint32_t h, const uint32_t* stg, uint32_t q) {
+// length, >= 4).  x0, x1: the 64 bits from the first precode length on.
+__device__ __forceinline__ bool fb_precode_ok(uint32_t h, uint32_t x0, uint32_t x1) {
     const uint32_t hclen = ((h >> 13) & 15) + 4;
-    const uint32_t x0 = fb_bits(stg, q + 17), x1 = fb_bits(stg, q + 49);
     uint32_t kr = 0;
 #pragma unroll
     for (uint32_t i = 0; i < 19; i++) {
@@ -153,11 +162,16 @@ __device__ __forceinline__ bool fb_precode_ok(uint32_t h, const uint32_t* stg, u
     return kr == 128 && (last != 0 || hclen == 4);
 }
 // the precode lengths by symbol (3 bits each)
-__device__ __forceinline__ uint64_t fb_precode_lengths(uint32_t h, const uint32_t* stg, uint32_t q) {
+__device__ __forceinline__ uint64_t fb_precode_lengths(uint32_t h, uint32_t x0, uint32_t x1) {
     const uint32_t hclen = ((h >> 13) & 15) + 4;
-    const uint64_t x = (uint64_t)fb_bits(stg, q + 17) | ((uint64_t)fb_bits(stg, q + 49) << 32);
+    const uint64_t x = (uint64_t)x0 | ((uint64_t)x1 << 32);
     uint64_t pl = 0;
-    for (uint32_t i = 0; i < hclen; i++) pl |= ((x >> (3 * i)) & 7) << (3 * kPerm[i]);
+    // kPerm as 5-bit fields in two registers (the table itself is a memory load per length)
+    constexpr uint64_t kPermLo = 0x22caa324e804a30ull, kPermHi = 0x3c2e1346cull;
+    for (uint32_t i = 0; i < hclen; i++) {
+        const uint32_t sym = (uint32_t)((i < 12 ? kPermLo >> (5 * i) : kPermHi >> (5 * (i - 12))) & 31);
+        pl |= ((x >> (3 * i)) & 7) << (3 * sym);
+    }
     return pl;
 }
 
@@ -165,8 +179,6 @@ __global__ __launch_bounds__(64) void k_fb_scan(const uint32_t* in_words, uint64
                                                  uint64_t n, uint32_t* counts, uint64_t* hits) {
     __shared__ uint32_t stg[FB_STAGE_WORDS + 2];
     __shared__ uint32_t q1[FB_STEP + 64];  // offsets r (bit 31: a stored-block hit)
-    __shared__ uint32_t q2[128];
-    __shared__ __attribute__((aligned(4))) uint8_t luts[64 * 128];  // stage 2's precode tables
     const uint32_t lane = threadIdx.x;
     const uint64_t c = blockIdx.x;
     // stage words of the aligned image: bit 0 of word 0 = stream bit b0 - sh
@@ -188,39 +200,9 @@ __global__ __launch_bounds__(64) void k_fb_scan(const uint32_t* in_words, uint64
     }
     __syncthreads();
     const uint64_t nbits = 8 * n;
-    uint32_t found = 0, n1 = 0, n2 = 0;
+    uint32_t found = 0, n1 = 0;
     const uint64_t below = (1ull << lane) - 1ull;
-    // stage 2 on q2[0, m): hits in order; the rest of q2 moves down
-    auto drain2 = [&](uint32_t m) {
-        bool hit = false, stored = false;
-        uint32_t r = 0;
-        if (lane < m) {
-            const uint32_t e = q2[lane];
-            r = e & 0x7FFFFFFFu;
-            stored = (e >> 31) != 0;
-            if (stored) {
-                hit = true;
-            } else {
-                const uint32_t q = sh + r;
-                const uint32_t h = fb_bits(stg, q);
-                hit = fb_check_lengths(stg, q + 17 + 3 * (((h >> 13) & 15) + 4), fb_precode_lengths(h, stg, q),
-                                       ((h >> 3) & 31) + 257, ((h >> 8) & 31) + 1, (FB_STAGE_WORDS - 1) * 32,
-                                       luts + 128 * lane);
-            }
-        }
-        const uint64_t hm = __ballot(hit);
-        const uint32_t before = __popcll(hm & below);
-        if (hit && found + before < FB_HITS)
-            hits[c * FB_HITS + found + before] = (b0 + r) | (stored ? FB_HIT_STORED : 0ull);
-        found += __popcll(hm);
-        const uint32_t rest = n2 - m;
-        const uint32_t mv = lane < rest ? q2[m + lane] : 0u;
-        wave_sync();
-        if (lane < rest) q2[lane] = mv;
-        wave_sync();
-        n2 = rest;
-    };
-    // stage 1 on q1[0, m): survivors to q2 (in order); the rest of q1 moves down
+    // stage 1 on q1[0, m): survivors to the chunk's candidates (in order); the rest of q1 moves down
     auto drain1 = [&](uint32_t m) {
         bool pass = false;
         uint32_t e = 0;
@@ -230,19 +212,20 @@ __global__ __launch_bounds__(64) void k_fb_scan(const uint32_t* in_words, uint64
                 pass = true;
             } else {
                 const uint32_t q = sh + e;
-                pass = fb_precode_ok(fb_bits(stg, q), stg, q);
+                pass = fb_precode_ok(fb_bits(stg, q), fb_bits(stg, q + 17), fb_bits(stg, q + 49));
             }
         }
         const uint64_t pm = __ballot(pass);
-        if (pass) q2[n2 + __popcll(pm & below)] = e;
-        n2 += __popcll(pm);
+        const uint32_t before = __popcll(pm & below);
+        if (pass && found + before < FB_HITS)
+            hits[c * FB_HITS + found + before] = (b0 + (e & 0x7FFFFFFFu)) | ((e >> 31) ? FB_HIT_STORED : 0ull);
+        found += __popcll(pm);
         const uint32_t rest = n1 - m;
         wave_sync();
         for (uint32_t i = lane; i < rest; i += 64) q1[i] = q1[m + i];  // (m = 64: no pass
                                                   // writes an entry that it or a later pass reads)
         wave_sync();
         n1 = rest;
-        if (n2 >= 64) drain2(64);
     };
     for (uint32_t step = 0; step < FB_SCAN_BITS / FB_STEP && found < FB_HITS; step++) {
         const uint32_t o = step * FB_STEP + lane * 32;  // this lane's first offset (relative to b0)
@@ -289,9 +272,84 @@ __global__ __launch_bounds__(64) void k_fb_scan(const uint32_t* in_words, uint64
         wave_sync();
         while (n1 >= 64) drain1(64);
     }
-    while (n1) drain1(n1 < 64 ? n1 : 64u);
-    if (n2 && found < FB_HITS) drain2(n2);
+    while (n1 && found < FB_HITS) drain1(n1 < 64 ? n1 : 64u);
     if (lane == 0) counts[c] = min(found, FB_HITS);
+}
+
+// stream bits from HBM (the aligned image; zero past the stream's last byte)
+struct FbGlobalBits {
+    const uint32_t* w;
+    uint64_t nwords, end_bytes;
+    __device__ uint32_t word(uint64_t i) const {
+        if (i >= nwords) return 0u;
+        uint32_t v = w[i];
+        const uint64_t lim = end_bytes - 4 * i;
+        if (lim < 4) v &= (1u << (8 * lim)) - 1u;
+        return v;
+    }
+    __device__ uint32_t peek(uint64_t p) const {
+        return __builtin_amdgcn_alignbit(word((p >> 5) + 1), word(p >> 5), (uint32_t)(p & 31));
+    }
+};
+
+// The full test of the candidates k_fb_compact listed (stage 2): one per lane.  Each lane's
+// first FBC_WORDS words from the candidate on are staged in LDS (a real header fits; a longer
+// one reads on from HBM), and its precode table is an LDS column; both column-major, so the
+// lanes of a wave read distinct banks.  A candidate that is not a dynamic-block header a real
+// encoder could have written (fb_check_lengths) is marked FB_HIT_REJECT in place.
+constexpr uint32_t FBC_WORDS = 64;  // 2048 bits: the longest false candidates of a wave run ~1.2 Kbit
+typedef __attribute__((address_space(3))) uint32_t FbcLdsU32;
+typedef __attribute__((address_space(3))) uint8_t FbcLdsU8;
+struct FbcLut {
+    FbcLdsU8* col;  // entry v at col[256 (v / 4) + v % 4]: four entries per lane dword, the
+                    // lane's dwords 256 B apart (one bank per lane)
+    __device__ void set(uint32_t v, uint32_t e) const { col[256 * (v >> 2) + (v & 3)] = (uint8_t)e; }
+    __device__ uint32_t get(uint32_t v) const { return col[256 * (v >> 2) + (v & 3)]; }
+    __device__ void clear() const {
+        for (uint32_t k = 0; k < 32; k++) *(__attribute__((address_space(3))) uint32_t*)(col + 256 * k) = 0u;
+    }
+};
+struct FbcBits {
+    FbcLdsU32* col;  // staged word i at col[64 i]: aligned-image word w0 + i
+    uint64_t b0;     // aligned-image bit of staged word 0
+    FbGlobalBits g;
+    __device__ uint32_t peek(uint64_t p) const {
+        const uint64_t r = p - b0;
+        if (r + 64 > 32 * FBC_WORDS) return g.peek(p);
+        const uint32_t i = (uint32_t)(r >> 5);
+        return __builtin_amdgcn_alignbit(col[64 * (i + 1)], col[64 * i], (uint32_t)(r & 31));
+    }
+};
+__global__ __launch_bounds__(64) void k_fb_check(const uint32_t* in_words, uint64_t misalign, uint64_t n,
+                                                  uint64_t* list, uint64_t count) {
+    __shared__ uint32_t stg[FBC_WORDS * 64];
+    __shared__ __attribute__((aligned(16))) uint8_t luts[128 * 64];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * 64 + lane;
+    if (i >= count) return;
+    const uint64_t e = list[i];
+    if (e & FB_HIT_STORED) return;
+    const FbGlobalBits g{in_words, (misalign + n + 3) / 4, misalign + n};
+    const uint64_t q = misalign * 8 + e;
+    FbcLdsU32* col = (FbcLdsU32*)(stg) + lane;
+    const uint64_t w0 = q >> 5;
+    uint32_t v[FBC_WORDS];
+    if (w0 + FBC_WORDS + 1 < g.nwords) {  // inside the stream, short of its last word: no tests,
+#pragma unroll                            // so the loads issue back to back
+        for (uint32_t k = 0; k < FBC_WORDS; k++) v[k] = in_words[w0 + k];
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < FBC_WORDS; k++) v[k] = g.word(w0 + k);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < FBC_WORDS; k++) col[64 * k] = v[k];
+    const FbcBits b{col, w0 * 32, g};
+    const uint32_t h = b.peek(q), x0 = b.peek(q + 17), x1 = b.peek(q + 49);
+    const uint64_t p = q + 17 + 3 * (((h >> 13) & 15) + 4);
+    // a header longer than 4096 bits is none a real encoder writes
+    if (!fb_check_lengths(b, p, fb_precode_lengths(h, x0, x1), ((h >> 3) & 31) + 257, ((h >> 8) & 31) + 1,
+                          q + 4096, FbcLut{(FbcLdsU8*)(luts) + 4 * lane}))
+        list[i] = e | FB_HIT_REJECT;
 }
 
 // compact the per-chunk hits into one sorted list (offsets from the scan of counts)
@@ -639,6 +697,16 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
     __shared__ __attribute__((aligned(16))) FbpSmem S;
     constexpr int NW = FBP_NT / 64;
     const int t = threadIdx.x;
+    // DMX_FB_DEBUG: cycles per phase (thread 0), summed over units in stats[16..]
+    unsigned long long* const ph = A.stats ? reinterpret_cast<unsigned long long*>(A.stats + 16) : nullptr;
+    uint64_t ph_last = ph && t == 0 ? clock64() : 0;
+    auto stamp = [&](int k) {
+        if (ph && t == 0) {
+            const uint64_t now = clock64();
+            atomicAdd(ph + k, (unsigned long long)(now - ph_last));
+            ph_last = now;
+        }
+    };
     const int wave = t >> 6;
     const uint64_t u = A.u0 + blockIdx.x;
     const uint64_t start = A.starts[u];
@@ -713,6 +781,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             S.in[i] = v;
         }
         __syncthreads();
+        stamp(0);
         if (wave == 0) {
             uint64_t hp = base + start + 3;
             uint32_t err = 0;
@@ -742,11 +811,13 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             }
         }
         __syncthreads();
+        stamp(1);
         if (S.kind == 0) {
             fill_lut32_wg<PJ_LL, false>(S.llut, S.T.lm, S.T.lsorted, t, FBP_NT);
             fill_lut32_wg<PJ_LD, true>(S.dlut, S.T.dm, S.T.dsorted, t, FBP_NT);
         }
         __syncthreads();
+        stamp(2);
     }
     // a fixed-code block whose end of block is followed by a non-final fixed-block header runs on
     // into it (the same code): a run of fixed blocks decodes as one block
@@ -809,6 +880,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             if (pn) w1++;
             e1 = p;
         }
+        stamp(3);
         // ---- 3. settle the range starts (k_inflate_pj's protocol) ----
         uint32_t s = s0, e = e1, st = st1;
         uint32_t te = FBP_NT;
@@ -847,6 +919,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             }
             __syncthreads();
         }
+        stamp(4);
         // ---- 4. the block's end; recount ranges that moved ----
         if (t == 0 && !settled) {
             S.kind = 1u;
@@ -904,6 +977,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             }
             if (pn) w1++;
         }
+        stamp(5);
         // ---- 5. scans, then the token words ----
         S.wcnt[r] = r <= te ? w1 : 0u;
         S.bcnt[r] = r <= te ? b1 : 0u;
@@ -937,6 +1011,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             }
         }
         __syncthreads();
+        stamp(6);
         if (S.kind == 0 && r <= te) {
             uint32_t* tk = A.tok + A.tokoff[u] + S.wcnt[r];
             uint32_t o = S.bcnt[r];
@@ -976,6 +1051,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             }
         }
         __syncthreads();
+        stamp(7);
         // the unit ends after this block unless the serial decoder would go on; a fixed block
         // far from the stop ends it too (the host starts a lane-parallel unit at its header)
         if (t == 0 && S.kind == 0 && !S.bfinal && !S.midend) {
@@ -1045,6 +1121,7 @@ struct FbReplayArgs {
     const FbUnit* units;
     uint16_t* img;               // 16-bit output image (total entries)
     uint32_t* err;               // set to 1 when a copy reaches before the stream start
+    unsigned long long* ph;      // DMX_FB_DEBUG: k_fb_units cycles per phase, or nullptr
 };
 
 // ring copy of L entries from src (ring index) to dst, src < dst in stream order (dst - src =
@@ -1221,21 +1298,42 @@ __global__ __launch_bounds__(64) void k_fb_replay(FbReplayArgs A) {
 // ---------------------------------------------------------------------------------------
 // k_fb_units: the replay as pointer jumping, one 1024-lane workgroup per unit on the chain
 // (replaces k_fb_replay's one wavefront, whose copies inside a 64-token group run one after
-// another).  In a 32-bit image P of the unit's output (unit-relative positions, in HBM/L2):
-//   1. the token words, 1024 at a time: block scan of their lengths gives each token's output
-//      offset; a literal writes final bytes, a match writes for each byte the position it
-//      copies from (periodic copies point into the first period), or -- for a position before
-//      the unit -- the final marker 0x8000 | (b - 1); stored blocks are copied by the whole
-//      workgroup from the stream;
-//   2. pointer jumping P[x] = P[P[x]] (up to four hops per entry per round, in place) until
-//      every entry is final (sources are always earlier positions);
-//   3. the low 16 bits -- a byte or a marker, k_fb_replay's image format -- to the image.
+// another).  The unit's output is built in pieces of FBU_PS positions, all in LDS:
+//   1. the token words, 1024 at a time (the next batch's words loaded while this one is
+//      expanded): a block scan of their lengths gives each token's output offset.  A batch of
+//      short tokens expands one token per lane; in a batch whose waves' longest tokens average
+//      more than 40 positions each thread takes FBU_PS / 1024 consecutive positions of the piece, finds the
+//      token of the first by binary search and walks on.  A literal gives a final
+//      byte, a match for each byte the position it copies from (periodic copies point into
+//      the first period) or -- before the unit -- the final marker 0x8000 | (b - 1).  (Round 4
+//      expanded one token per lane: a wave waited for its longest match, 255K of ~330K cycles
+//      per C3 unit.)  Stored blocks are copied by the whole workgroup from the stream.  A
+//      batch that runs past the piece's end finishes the piece (2., 3.) and goes on in the next;
+//   2. pointer jumping in the piece, in place, until every entry is final: a source before
+//      the piece is final in one hop, since the ring R holds the last FBU_R resolved
+//      positions (a match reaches at most 32 KiB back);
+//   3. the piece's low 16 bits -- a byte or a marker, k_fb_replay's image format -- to the
+//      16-bit image in HBM and to R.
+// Round 4 kept a 32-bit image of the whole unit in HBM and jumped through it there: 16 bytes
+// of HBM traffic per output byte (PMC on C3) and a dependent HBM load per hop; now the token
+// words and the 2-byte image are the only HBM traffic.
 // ---------------------------------------------------------------------------------------
 constexpr int FBR_NT = 1024;
 constexpr uint32_t FBR_FINAL = 0x80000000u;
-__global__ __launch_bounds__(FBR_NT) void k_fb_units(FbReplayArgs A, uint32_t* __restrict__ P) {
-    __shared__ uint32_t part[FBR_NT / 64];
-    __shared__ uint32_t slist[FBR_NT / 2][3];  // stored blocks of the chunk: offset, length, source
+constexpr uint32_t FBU_PS = 16384;  // piece positions (32-bit entries: 64 KiB of LDS)
+constexpr uint32_t FBU_R = 32768;   // resolved ring (16-bit entries: 64 KiB)
+constexpr uint32_t FBU_LIT = 1, FBU_MATCH = 2, FBU_STORED = 3;
+#ifndef DMX_FBU_SPREAD
+#define DMX_FBU_SPREAD 40
+#endif
+__global__ __launch_bounds__(FBR_NT) void k_fb_units(FbReplayArgs A) {
+    __shared__ __attribute__((aligned(16))) uint32_t C[FBU_PS];
+    __shared__ __attribute__((aligned(16))) uint16_t R[FBU_R];
+    __shared__ uint32_t Gw[FBR_NT];      // spread batches: the token words,
+    __shared__ uint32_t Go[FBR_NT + 1];  // their unit-relative output offsets (+ the batch end)
+    __shared__ uint8_t Gk[FBR_NT];       // and kinds (FBU_*, 0: no output)
+    __shared__ uint32_t part[FBR_NT / 64], pmax[FBR_NT / 64];
+    __shared__ uint32_t slist[FBR_NT / 2][3];  // stored blocks of the batch: offset, length, source
     __shared__ uint32_t nst;
     constexpr int NW = FBR_NT / 64;
     const uint32_t t = threadIdx.x, wave = t >> 6;
@@ -1245,15 +1343,58 @@ __global__ __launch_bounds__(FBR_NT) void k_fb_units(FbReplayArgs A, uint32_t* _
     const uint64_t off = A.offs[ci];
     const uint32_t* tk = A.tok + A.tokoff[u];
     const uint32_t n = rec.ntok;
+    const uint32_t usize = (uint32_t)rec.size;
     const uint8_t* sbase = A.stream + (A.starts[u] >> 3);  // stored offsets are relative to this byte
-    uint32_t* Pu = P + off;
-    bool bad = false;
-    uint32_t obase = 0;  // unit-relative output offset of the chunk
+    uint16_t* const img = A.img + off;
+    bool bad = false, open = false;
+    uint32_t obase = 0;  // unit-relative output offset of the batch
+    uint32_t pstart = 0; // the current piece: [pstart, pstart + FBU_PS)
     if (t == 0) nst = 0;
+    uint64_t ph_last = A.ph && t == 0 ? clock64() : 0;
+    auto stamp = [&](int k) {
+        if (A.ph && t == 0) {
+            const uint64_t now = clock64();
+            atomicAdd(A.ph + k, (unsigned long long)(now - ph_last));
+            ph_last = now;
+        }
+    };
+    // pointer jumping in the piece's pn entries, then the piece to the image and to R
+    auto finish_piece = [&](uint32_t pn) {
+        __syncthreads();  // every entry of the piece written
+        stamp(1);
+        for (int round = 0; round < 32; round++) {
+            bool pend = false;
+            for (uint32_t x = t; x < pn; x += FBR_NT) {
+                uint32_t v = C[x];
+                if (v & FBR_FINAL) continue;
+#pragma unroll 1
+                for (int h = 0; h < 8 && !(v & FBR_FINAL); h++)
+                    v = v < pstart ? (FBR_FINAL | R[v & (FBU_R - 1)]) : C[v - pstart];
+                C[x] = v;  // at once: entries read later in the round see it
+                pend |= !(v & FBR_FINAL);
+            }
+            if (A.ph && t == 0) atomicAdd(A.ph + 4, 1ull);
+            if (!__syncthreads_or(pend)) break;
+            if (round == 31) open = true;  // cannot happen: chains strictly go back
+        }
+        stamp(2);
+        for (uint32_t x = t; x < pn; x += FBR_NT) {
+            const uint16_t v = (uint16_t)C[x];
+            img[pstart + x] = v;
+            R[(pstart + x) & (FBU_R - 1)] = v;
+        }
+        __syncthreads();  // R and C reused
+        stamp(3);
+        pstart += pn;
+    };
+    uint32_t w = t < n ? tk[t] : 0u;
+    uint32_t wp = t >= 1 && t - 1 < n ? tk[t - 1] : 0u;
     for (uint32_t c0 = 0; c0 < n; c0 += FBR_NT) {
         const uint32_t ti = c0 + t;
-        const uint32_t w = ti < n ? tk[ti] : 0u;
-        const uint32_t wp = ti >= 1 && ti - 1 < n ? tk[ti - 1] : 0u;
+        // the next batch's words, loaded now
+        const uint32_t tn = ti + FBR_NT;
+        const uint32_t wn = tn < n ? tk[tn] : 0u;
+        const uint32_t wpn = tn - 1 < n ? tk[tn - 1] : 0u;
         // the word after a stored header (at an even index) is its offset: any 32-bit value
         const bool isoff = (ti & 1) && !(wp >> 31) && ((wp >> 24) & 127) == 127;
         const bool ism = (w >> 31) != 0 && !isoff;
@@ -1262,32 +1403,41 @@ __global__ __launch_bounds__(FBR_NT) void k_fb_units(FbReplayArgs A, uint32_t* _
         const bool islit = !ism && !isst && !isoff && cnt >= 1 && cnt <= 3;
         uint32_t L = ism ? (w >> 15) & 0xFFFFu : isst ? (w & 0xFFFFFFu) : islit ? cnt : 0u;
         if (ti >= n) L = 0;
-        // block-wide exclusive scan of the lengths
+        // block-wide exclusive scan of the lengths; each wave's longest token
         const uint32_t inc = wave_incl_scan(L);
-        if ((t & 63) == 63) part[wave] = inc;
+        uint32_t lmax = L;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) lmax = max(lmax, (uint32_t)__shfl_xor((int)lmax, o, 64));
+        if ((t & 63) == 63) {
+            part[wave] = inc;
+            pmax[wave] = lmax;
+        }
         __syncthreads();
-        uint32_t before = 0, T = 0;
+        uint32_t before = 0, T = 0, smax = 0;
 #pragma unroll
         for (int k = 0; k < NW; k++) {
             const uint32_t v = part[k];
             before += k < (int)wave ? v : 0u;
             T += v;
+            smax += pmax[k];
         }
         const uint32_t go = obase + before + inc - L;
-        if (islit && L) {
-            Pu[go] = FBR_FINAL | (w & 0xFF);
-            if (cnt > 1) Pu[go + 1] = FBR_FINAL | ((w >> 8) & 0xFF);
-            if (cnt > 2) Pu[go + 2] = FBR_FINAL | ((w >> 16) & 0xFF);
-        } else if (ism && L) {
-            const uint32_t d = (w & 0x7FFFu) + 1;
-            if ((uint64_t)d > off + go) bad = true;  // a copy from before the stream start
-            uint32_t rr = 0;
-            for (uint32_t i = 0; i < L; i++) {
-                const uint32_t src = go + rr - d;  // as signed: the source position
-                Pu[go + i] = (int32_t)src >= 0 ? src : (FBR_FINAL | 0x8000u | (uint32_t)(-(int32_t)src - 1));
-                if (++rr == d) rr = 0;
-            }
-        } else if (isst && L) {
+        const uint32_t d = (w & 0x7FFFu) + 1;
+        if (ism && L && (uint64_t)d > off + go) bad = true;  // a copy from before the stream start
+        const uint32_t gend = go + L;
+        const uint32_t gk = !L ? 0u : islit ? FBU_LIT : ism ? FBU_MATCH : FBU_STORED;
+        const uint32_t bend = obase + T;
+        // one token per lane costs each wave its longest token; spreading the positions costs
+        // ~16 stores per thread plus a binary search: spread when the waves' longest tokens
+        // average more than DMX_FBU_SPREAD positions (image rows, runs)
+        const bool spread = smax > (uint32_t)DMX_FBU_SPREAD * NW;
+        if (spread) {
+            Gw[t] = w;
+            Go[t] = go;
+            Gk[t] = (uint8_t)gk;
+            if (t == 0) Go[FBR_NT] = bend;
+        }
+        if (isst && L) {
             const uint32_t k = atomicAdd(&nst, 1u);
             slist[k][0] = go;
             slist[k][1] = L;
@@ -1295,34 +1445,77 @@ __global__ __launch_bounds__(FBR_NT) void k_fb_units(FbReplayArgs A, uint32_t* _
         }
         __syncthreads();
         const uint32_t ns = nst;
-        for (uint32_t k = 0; k < ns; k++) {
-            const uint32_t o = slist[k][0], len = slist[k][1];
-            const uint8_t* src = sbase + slist[k][2];
-            for (uint32_t j = t; j < len; j += FBR_NT) Pu[o + j] = FBR_FINAL | src[j];
+        stamp(0);
+        while (pstart < bend) {
+            const uint32_t pe = min(pstart + FBU_PS, bend);  // this batch's part of the piece
+            if (!spread) {
+                // short tokens: one per lane
+                const uint32_t lo = max(go, pstart), hi = min(gend, pe);
+                if (gk == FBU_LIT) {
+                    for (uint32_t x = lo; x < hi; x++) C[x - pstart] = FBR_FINAL | ((w >> (8 * (x - go))) & 0xFF);
+                } else if (gk == FBU_MATCH && lo < hi) {
+                    uint32_t rr = lo - go;
+                    if (rr >= d) rr %= d;
+                    for (uint32_t x = lo; x < hi; x++) {
+                        const uint32_t src = go + rr - d;  // as signed: the source position
+                        C[x - pstart] = (int32_t)src >= 0 ? src : (FBR_FINAL | 0x8000u | (uint32_t)(-(int32_t)src - 1));
+                        if (++rr == d) rr = 0;
+                    }
+                }
+            } else {
+                // long tokens (a lane per token would wait for the longest): the batch's part of
+                // the piece spread evenly over the workgroup; a thread finds the token of its
+                // first position by binary search over the batch's offsets and walks on
+                const uint32_t a0 = max(pstart, obase);
+                const uint32_t cs = (pe - a0 + FBR_NT - 1) / FBR_NT;
+                uint32_t x = a0 + t * cs;
+                const uint32_t x1 = min(x + cs, pe);
+                if (x < x1) {
+                    uint32_t lo = 0, hi = FBR_NT;  // the last k with Go[k] <= x (it has output)
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (Go[mid] <= x) lo = mid;
+                        else hi = mid;
+                    }
+                    uint32_t k = lo;
+                    while (x < x1) {
+                        const uint32_t tw = Gw[k], tgo = Go[k], tend = Go[k + 1], kind = Gk[k];
+                        const uint32_t e = min(tend, x1);
+                        if (kind == FBU_LIT) {
+                            for (; x < e; x++) C[x - pstart] = FBR_FINAL | ((tw >> (8 * (x - tgo))) & 0xFF);
+                        } else if (kind == FBU_MATCH) {
+                            const uint32_t td = (tw & 0x7FFFu) + 1;
+                            uint32_t rr = x - tgo;  // nonzero only in the first token of the range
+                            if (rr >= td) rr %= td;
+                            for (; x < e; x++) {
+                                const uint32_t src = tgo + rr - td;  // as signed: the source position
+                                C[x - pstart] = (int32_t)src >= 0 ? src : (FBR_FINAL | 0x8000u | (uint32_t)(-(int32_t)src - 1));
+                                if (++rr == td) rr = 0;
+                            }
+                        } else {
+                            x = e;  // a stored block (copied below), or no output
+                        }
+                        k++;
+                    }
+                }
+            }
+            for (uint32_t q = 0; q < ns; q++) {
+                const uint32_t o = slist[q][0], len = slist[q][1];
+                const uint32_t a = max(o, pstart), b = min(o + len, pe);
+                const uint8_t* src = sbase + slist[q][2] + (a - o);
+                for (uint32_t j = t; a + j < b; j += FBR_NT) C[a + j - pstart] = FBR_FINAL | src[j];
+            }
+            if (pe - pstart < FBU_PS && pe < usize) break;  // the piece goes on in the next batch
+            finish_piece(pe - pstart);
         }
         __syncthreads();
+        stamp(1);
         if (t == 0) nst = 0;
-        obase += T;
+        obase = bend;
+        w = wn;
+        wp = wpn;
     }
-    __syncthreads();
-    const uint32_t total = obase;
-    bool open = true;
-    for (int round = 0; round < 32 && open; round++) {
-        bool pend = false;
-        for (uint32_t x = t; x < total; x += FBR_NT) {
-            uint32_t v = Pu[x];
-            if (v & FBR_FINAL) continue;
-#pragma unroll 1
-            for (int h = 0; h < 4 && !(v & FBR_FINAL); h++) v = Pu[v];
-            Pu[x] = v;
-            pend |= !(v & FBR_FINAL);
-        }
-        open = __syncthreads_or(pend) != 0;
-    }
-    if (open) bad = true;  // cannot happen: chains strictly go back
-    uint16_t* img = A.img + off;
-    for (uint32_t x = t; x < total; x += FBR_NT) img[x] = (uint16_t)Pu[x];
-    if (__syncthreads_or(bad) && t == 0) atomicOr(A.err, 1u);
+    if (__syncthreads_or(bad || open) && t == 0) atomicOr(A.err, 1u);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1758,10 +1951,14 @@ hipError_t launch_fb_scan(const uint32_t* in_words, uint64_t misalign, uint64_t 
     return launch_scan_u32(counts, offs, nc, nhits, st);
 }
 
-hipError_t launch_fb_compact(const uint32_t* counts, const uint64_t* offs, const uint64_t* hits,
-                             uint64_t nchunks, uint64_t* list, hipStream_t st) {
+hipError_t launch_fb_compact(const uint32_t* in_words, uint64_t misalign, uint64_t n, const uint32_t* counts,
+                             const uint64_t* offs, const uint64_t* hits, uint64_t nchunks, uint64_t* list,
+                             uint64_t count, hipStream_t st) {
     hipLaunchKernelGGL(k_fb_compact, dim3((uint32_t)((nchunks + 255) / 256)), dim3(256), 0, st,
                        counts, offs, hits, nchunks, list);
+    if (count)
+        hipLaunchKernelGGL(k_fb_check, dim3((uint32_t)((count + 63) / 64)), dim3(64), 0, st, in_words, misalign,
+                           n, list, count);
     return hipGetLastError();
 }
 
@@ -1790,10 +1987,11 @@ hipError_t launch_fb_resolve(const uint8_t* stream, const uint64_t* starts, cons
                              const uint64_t* offs, const uint64_t* sizes, uint64_t nchain,
                              const uint64_t* tokoff, const uint32_t* tok, const FbUnit* units,
                              uint16_t* img, uint64_t total, uint8_t* out, uint32_t* err,
-                             uint32_t* win, uint32_t* open, uint32_t* p32, hipStream_t st) {
-    FbReplayArgs R{stream, starts, chain, offs, tokoff, tok, units, img, err};
-    if (p32)
-        hipLaunchKernelGGL(k_fb_units, dim3((uint32_t)nchain), dim3(FBR_NT), 0, st, R, p32);
+                             uint32_t* win, uint32_t* open, bool workgroup, unsigned long long* ph,
+                             hipStream_t st) {
+    FbReplayArgs R{stream, starts, chain, offs, tokoff, tok, units, img, err, ph};
+    if (workgroup)
+        hipLaunchKernelGGL(k_fb_units, dim3((uint32_t)nchain), dim3(FBR_NT), 0, st, R);
     else
         hipLaunchKernelGGL(k_fb_replay, dim3((uint32_t)nchain), dim3(64), 0, st, R);
     if (win) {
