@@ -300,8 +300,23 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     std::vector<uint64_t> hits(nhits);
     if (nhits) {
         if (!c->fbl.ensure(nhits * 8)) return DMX_OK;
+        unsigned long long* cph = nullptr;  // DMX_FB_DEBUG: k_fb_check counters
+        if ((c->diag & DIAG_FB) && c->fbph.ensure(256)) {
+            cph = c->fbph.as<unsigned long long>();
+            HIPCHK(hipMemsetAsync(cph, 0, 256, st));
+        }
         HIPCHK(launch_fb_compact(words, misalign, n, c->fbc.as<uint32_t>(), c->fbo.as<uint64_t>(),
-                                 c->fbh.as<uint64_t>(), nc, c->fbl.as<uint64_t>(), nhits, st));
+                                 c->fbh.as<uint64_t>(), nc, c->fbl.as<uint64_t>(), nhits,
+                                 cph, st));
+        if (cph) {
+            unsigned long long q[5];
+            HIPCHK(hipMemcpyAsync(q, cph + 8, sizeof(q), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            const unsigned long long w = q[4] ? q[4] : 1;
+            std::fprintf(stderr, "dmx fb: k_fb_check %llu candidates, %llu waves: per wave refill %llu cycles, "
+                         "steps %llu cycles, %llu steps, %.1f busy lanes per step\n", (unsigned long long)nhits, w,
+                         q[0] / w, q[1] / w, q[2] / w, q[2] ? (double)q[3] / (double)q[2] : 0.0);
+        }
         HIPCHK(hipMemcpyAsync(hits.data(), c->fbl.p, nhits * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
     }
@@ -636,7 +651,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         open = c->fbopen.as<uint32_t>();
     }
     unsigned long long* uph = nullptr;
-    if ((c->diag & DIAG_FB) && c->fbph.ensure(64)) {
+    if ((c->diag & DIAG_FB) && c->fbph.ensure(256)) {
         uph = c->fbph.as<unsigned long long>();
         HIPCHK(hipMemsetAsync(uph, 0, 64, st));
     }

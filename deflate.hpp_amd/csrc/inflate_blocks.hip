@@ -64,77 +64,64 @@ __device__ __forceinline__ uint32_t fb_bits(const uint32_t* w, uint32_t p) {  //
     return __builtin_amdgcn_alignbit(w[i + 1], w[i], p & 31);
 }
 
-// Full check of a candidate whose precode is complete.  pl: 19 precode lengths (3 bits each,
-// by symbol).  p: bit position (in the staged image) of the first code-length symbol.  lut: this
-// lane's 128-entry precode table in LDS (symbol | length << 5, 0 = no code), built here.
-// RFC 1951 rules as zlib's inflate enforces them; A-11/A-12 streams are not block starts any
-// real encoder writes, so rejecting them only costs parallelism.
-template <class Bits, class Lut>
-__device__ bool fb_check_lengths(const Bits& w, uint64_t p, uint64_t pl, uint32_t nlit,
-                                 uint32_t ndist, uint64_t plim, Lut lut) {
-    // canonical codes: counts per length (5-bit fields), first code per length (8-bit fields)
-    uint64_t cnt = 0;
-    for (uint32_t s = 0; s < 19; s++) {
-        const uint32_t l = (uint32_t)(pl >> (3 * s)) & 7;
-        cnt += l ? 1ull << (5 * l) : 0ull;
-    }
-    uint64_t nxt = 0;
-    uint32_t code = 0;
-    for (uint32_t l = 1; l <= 7; l++) {
-        code = (code + (uint32_t)((cnt >> (5 * (l - 1))) & 31)) << 1;  // (no length-0 count)
-        nxt |= (uint64_t)code << (8 * l);
-    }
-    lut.clear();
-    for (uint32_t s = 0; s < 19; s++) {
-        const uint32_t l = (uint32_t)(pl >> (3 * s)) & 7;
-        if (!l) continue;
-        const uint32_t c = (uint32_t)(nxt >> (8 * l)) & 0xFF;
-        nxt += 1ull << (8 * l);
-        const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);
-        for (uint32_t v = r; v < 128; v += 1u << l) lut.set(v, s | (l << 5));
-    }
-    const uint32_t total = nlit + ndist;
-    uint32_t i = 0, prev = 0;
-    uint32_t kl = 0, kd = 0, nd = 0;  // Kraft sums in units of 2^-15, used distance codes
-    bool eob = false;
-    while (i < total) {
-        if (p > plim) return false;  // longer than any header a real encoder writes
-        const uint32_t v = w.peek(p);
-        const uint32_t e = lut.get(v & 127);
-        if (!e) return false;
-        const uint32_t sym = e & 31, len = e >> 5;
-        p += len;
-        uint32_t val = sym, run = 1;
-        if (sym == 16) {
-            if (i == 0) return false;
-            val = prev;
-            run = 3 + ((v >> len) & 3);
-            p += 2;
-        } else if (sym == 17) {
-            val = 0;
-            run = 3 + ((v >> len) & 7);
-            p += 3;
-        } else if (sym == 18) {
-            val = 0;
-            run = 11 + ((v >> len) & 127);
-            p += 7;
+// Full check of a candidate whose precode is complete (k_fb_check), resumable so that a lane
+// can take the next candidate as soon as its own is decided.  RFC 1951 rules as zlib's inflate
+// enforces them; A-11/A-12 streams are not block starts any real encoder writes, so rejecting
+// them only costs parallelism.
+// The code-length sequence, read through a 64-bit bit buffer refilled from the lane's staged
+// column (word wi on; words past the column come from HBM).  step() decodes up to `steps`
+// symbols, branch-free but for the refill; st becomes FBK_PASS (a complete lit/len code with a
+// nonzero end-of-block length and a complete, or at most one-symbol, distance code) or
+// FBK_FAIL.  plim: the bit count a header may take at most.
+constexpr uint32_t FBK_RUN = 0, FBK_PASS = 1, FBK_FAIL = 2;
+struct FbLengthCheck {
+    uint64_t buf;
+    uint32_t nb, wi, used, plim;
+    uint32_t nlit, total, i, prev;
+    uint32_t kl, kd, nd;  // Kraft sums in units of 2^-15, used distance codes
+    bool eob;
+    uint32_t st;
+    // the precode: a 128-entry table (symbol | length << 5) in the lane's LDS column, indexed
+    // by the next 7 stream bits in code order (first bit = MSB), so that each symbol's entries
+    // are one contiguous range; entry c at byte 256 (c / 4) + c % 4 of the column
+    __attribute__((address_space(3))) uint8_t* tab;
+    // from the 19 precode lengths pl (3 bits each, by symbol) of a complete code (stage 1)
+    __device__ void set_precode(uint64_t pl) {
+        uint64_t cnt = 0;  // counts per length, 5-bit fields
+        for (uint32_t s = 0; s < 19; s++) {
+            const uint32_t l = (uint32_t)(pl >> (3 * s)) & 7;
+            cnt += l ? 1ull << (5 * l) : 0ull;
         }
-        if (i + run > total) return false;
-        if (val) {
-            // lengths [i, i + run): split at nlit
-            const uint32_t a = i < nlit ? min(i + run, nlit) - i : 0;
-            const uint32_t b = run - a;
-            kl += a << (15 - val);
-            kd += b << (15 - val);
-            nd += b;
-            if (i <= 256 && 256 < i + a) eob = true;
-            if (kl > 32768 || kd > 32768) return false;
+        uint64_t nxt = 0;  // the next code per length (8-bit fields)
+        uint32_t code = 0;
+        for (uint32_t l = 1; l <= 7; l++) {
+            code = (code + (uint32_t)((cnt >> (5 * (l - 1))) & 31)) << 1;  // (no length-0 count)
+            nxt |= (uint64_t)code << (8 * l);
         }
-        prev = val;
-        i += run;
+        for (uint32_t s = 0; s < 19; s++) {
+            const uint32_t l = (uint32_t)(pl >> (3 * s)) & 7;
+            if (!l) continue;
+            const uint32_t c = (uint32_t)(nxt >> (8 * l)) & 0xFF;
+            nxt += 1ull << (8 * l);
+            const uint32_t e = s | (l << 5);
+            const uint32_t c0 = c << (7 - l);  // entries [c0, c0 + 2^(7 - l))
+            if (l <= 5) {
+                for (uint32_t m = c0 >> 2; m < (c0 >> 2) + (1u << (5 - l)); m++)
+                    *(__attribute__((address_space(3))) uint32_t*)(tab + 256 * m) = e * 0x01010101u;
+            } else {
+                tab[256 * (c0 >> 2) + (c0 & 3)] = (uint8_t)e;
+                if (l == 6) tab[256 * (c0 >> 2) + (c0 & 3) + 1] = (uint8_t)e;
+            }
+        }
     }
-    return eob && kl == 32768 && (kd == 32768 || nd <= 1);
-}
+    // the symbol and length of the code at the low bits of v
+    __device__ __forceinline__ void decode(uint32_t v, uint32_t* sym, uint32_t* len) const {
+        const uint32_t c7 = __builtin_bitreverse32(v) >> 25;
+        const uint32_t e = tab[256 * (c7 >> 2) + (c7 & 3)];
+        *sym = e & 31;
+        *len = e >> 5;
+    }
+};
 
 // One wavefront per FB_SCAN_BITS offsets, in two stages so that each test runs on full waves:
 //   0. prefilter, 32 offsets per lane at once with 64-bit word arithmetic on the staged bits:
@@ -297,18 +284,12 @@ struct FbGlobalBits {
 // one reads on from HBM), and its precode table is an LDS column; both column-major, so the
 // lanes of a wave read distinct banks.  A candidate that is not a dynamic-block header a real
 // encoder could have written (fb_check_lengths) is marked FB_HIT_REJECT in place.
+#ifndef DMX_FBC_PER_WAVE
+#define DMX_FBC_PER_WAVE 64
+#endif
 constexpr uint32_t FBC_WORDS = 64;  // 2048 bits: the longest false candidates of a wave run ~1.2 Kbit
 typedef __attribute__((address_space(3))) uint32_t FbcLdsU32;
 typedef __attribute__((address_space(3))) uint8_t FbcLdsU8;
-struct FbcLut {
-    FbcLdsU8* col;  // entry v at col[256 (v / 4) + v % 4]: four entries per lane dword, the
-                    // lane's dwords 256 B apart (one bank per lane)
-    __device__ void set(uint32_t v, uint32_t e) const { col[256 * (v >> 2) + (v & 3)] = (uint8_t)e; }
-    __device__ uint32_t get(uint32_t v) const { return col[256 * (v >> 2) + (v & 3)]; }
-    __device__ void clear() const {
-        for (uint32_t k = 0; k < 32; k++) *(__attribute__((address_space(3))) uint32_t*)(col + 256 * k) = 0u;
-    }
-};
 struct FbcBits {
     FbcLdsU32* col;  // staged word i at col[64 i]: aligned-image word w0 + i
     uint64_t b0;     // aligned-image bit of staged word 0
@@ -320,36 +301,149 @@ struct FbcBits {
         return __builtin_amdgcn_alignbit(col[64 * (i + 1)], col[64 * i], (uint32_t)(r & 31));
     }
 };
-__global__ __launch_bounds__(64) void k_fb_check(const uint32_t* in_words, uint64_t misalign, uint64_t n,
-                                                  uint64_t* list, uint64_t count) {
-    __shared__ uint32_t stg[FBC_WORDS * 64];
-    __shared__ __attribute__((aligned(16))) uint8_t luts[128 * 64];
-    const uint32_t lane = threadIdx.x;
-    const uint64_t i = (uint64_t)blockIdx.x * 64 + lane;
-    if (i >= count) return;
-    const uint64_t e = list[i];
-    if (e & FB_HIT_STORED) return;
-    const FbGlobalBits g{in_words, (misalign + n + 3) / 4, misalign + n};
-    const uint64_t q = misalign * 8 + e;
-    FbcLdsU32* col = (FbcLdsU32*)(stg) + lane;
-    const uint64_t w0 = q >> 5;
-    uint32_t v[FBC_WORDS];
-    if (w0 + FBC_WORDS + 1 < g.nwords) {  // inside the stream, short of its last word: no tests,
-#pragma unroll                            // so the loads issue back to back
-        for (uint32_t k = 0; k < FBC_WORDS; k++) v[k] = in_words[w0 + k];
-    } else {
-#pragma unroll
-        for (uint32_t k = 0; k < FBC_WORDS; k++) v[k] = g.word(w0 + k);
+// One lane per candidate, a wave per DMX_FBC_PER_WAVE candidates (its own range: a lane whose
+// candidate is decided takes the range's next one once half the wave is idle, so a wave does
+// not wait for its longest candidate -- the test runs 48 symbols on average but ~230 at a
+// wave's slowest lane on C3).
+struct FbcCol {
+    FbcLdsU32* col;
+    const uint32_t* in_words;
+    uint64_t w0;
+    FbGlobalBits g;
+    __device__ uint32_t word(uint32_t k) const { return k < FBC_WORDS ? col[64 * k] : g.word(w0 + k); }
+};
+__device__ __forceinline__ void fbk_step(FbLengthCheck& c, const FbcCol& src, int steps) {
+    for (int k = 0; k < steps; k++) {
+        if (c.st != FBK_RUN) break;
+        if (c.i >= c.total) {
+            c.st = c.eob && c.kl == 32768 && (c.kd == 32768 || c.nd <= 1) ? FBK_PASS : FBK_FAIL;
+            break;
+        }
+        if (c.nb < 32) {  // refill: at least 32 bits stay in the buffer (a symbol takes <= 14)
+            c.buf |= (uint64_t)src.word(c.wi) << c.nb;
+            c.wi++;
+            c.nb += 32;
+        }
+        const uint32_t v = (uint32_t)c.buf;
+        uint32_t sym, len;
+        c.decode(v, &sym, &len);
+        const uint32_t eb = sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u;
+        const uint32_t rb = sym == 16 ? 3u : sym == 17 ? 3u : sym == 18 ? 11u : 1u;
+        const uint32_t run = rb + ((v >> len) & ((1u << eb) - 1u));
+        const uint32_t val = sym < 16 ? sym : sym == 16 ? c.prev : 0u;
+        const uint32_t cons = len + eb;
+        c.buf >>= cons;
+        c.nb -= cons;
+        c.used += cons;
+        // lengths [i, i + run): split at nlit
+        const uint32_t a = c.i < c.nlit ? min(c.i + run, c.nlit) - c.i : 0u;
+        const uint32_t b = run - a;
+        const uint32_t sh = 15 - (val ? val : 15u);
+        c.kl += val ? a << sh : 0u;
+        c.kd += val ? b << sh : 0u;
+        c.nd += val ? b : 0u;
+        c.eob |= val && c.i <= 256 && 256 < c.i + a;
+        const bool bad = !len || (sym == 16 && c.i == 0) || c.i + run > c.total || c.kl > 32768 || c.kd > 32768 ||
+                         c.used > c.plim;
+        c.prev = val;
+        c.i += run;
+        if (bad) c.st = FBK_FAIL;
     }
+}
+__global__ __launch_bounds__(64) void k_fb_check(const uint32_t* in_words, uint64_t misalign, uint64_t n,
+                                                  uint64_t* list, uint64_t count, unsigned long long* ph) {
+    __shared__ uint32_t stg[FBC_WORDS * 64];
+    __shared__ __attribute__((aligned(16))) uint8_t tabs[128 * 64];
+    const uint32_t lane = threadIdx.x;
+    const FbGlobalBits g{in_words, (misalign + n + 3) / 4, misalign + n};
+    FbcLdsU32* col = (FbcLdsU32*)(stg) + lane;
+    const uint64_t below = (1ull << lane) - 1ull;
+    FbLengthCheck ck;
+    ck.st = FBK_FAIL;
+    ck.tab = (FbcLdsU8*)(tabs) + 4 * lane;
+    FbcCol src{col, in_words, 0, g};
+    bool busy = false;
+    uint64_t nxt = (uint64_t)blockIdx.x * DMX_FBC_PER_WAVE;
+    const uint64_t end = min(count, nxt + DMX_FBC_PER_WAVE);
+    uint64_t idx = 0, e = 0;
+    uint64_t c_ref = 0, c_step = 0, n_out = 0, n_busy = 0, tl = ph ? clock64() : 0;
+    for (;;) {
+        // refill the idle lanes once half the wave is idle (or all of it)
+        const uint64_t idle = __ballot(!busy);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (nxt < end && (nidle >= 32 || nidle == 64)) {
+            if (!busy) {
+                idx = nxt + (uint64_t)__popcll(idle & below);
+                if (idx < end) {
+                    e = list[idx];
+                    if (!(e & FB_HIT_STORED)) {
+                        busy = true;
+                        const uint64_t q = misalign * 8 + e;
+                        const uint64_t w0 = q >> 5;
+                        uint32_t v[FBC_WORDS];
+                        if (w0 + FBC_WORDS + 1 < g.nwords) {  // no tests: the loads issue back to back
 #pragma unroll
-    for (uint32_t k = 0; k < FBC_WORDS; k++) col[64 * k] = v[k];
-    const FbcBits b{col, w0 * 32, g};
-    const uint32_t h = b.peek(q), x0 = b.peek(q + 17), x1 = b.peek(q + 49);
-    const uint64_t p = q + 17 + 3 * (((h >> 13) & 15) + 4);
-    // a header longer than 4096 bits is none a real encoder writes
-    if (!fb_check_lengths(b, p, fb_precode_lengths(h, x0, x1), ((h >> 3) & 31) + 257, ((h >> 8) & 31) + 1,
-                          q + 4096, FbcLut{(FbcLdsU8*)(luts) + 4 * lane}))
-        list[i] = e | FB_HIT_REJECT;
+                            for (uint32_t k = 0; k < FBC_WORDS; k++) v[k] = in_words[w0 + k];
+                        } else {
+#pragma unroll
+                            for (uint32_t k = 0; k < FBC_WORDS; k++) v[k] = g.word(w0 + k);
+                        }
+#pragma unroll
+                        for (uint32_t k = 0; k < FBC_WORDS; k++) col[64 * k] = v[k];
+                        src.w0 = w0;
+                        const FbcBits bits{col, w0 * 32, g};
+                        const uint32_t h = bits.peek(q), x0 = bits.peek(q + 17), x1 = bits.peek(q + 49);
+                        ck.set_precode(fb_precode_lengths(h, x0, x1));
+                        // the code lengths from bit q + 17 + 3 HCLEN on; a header longer than 4096
+                        // bits is none a real encoder writes
+                        const uint32_t r = (uint32_t)(q - w0 * 32) + 17 + 3 * (((h >> 13) & 15) + 4);
+                        ck.wi = (r >> 5) + 2;
+                        ck.buf = (((uint64_t)src.word((r >> 5) + 1) << 32) | src.word(r >> 5)) >> (r & 31);
+                        ck.nb = 64 - (r & 31);
+                        ck.used = 0;
+                        ck.plim = 4096 - (r - (uint32_t)(q - w0 * 32));
+                        ck.nlit = ((h >> 3) & 31) + 257;
+                        ck.total = ck.nlit + ((h >> 8) & 31) + 1;
+                        ck.i = ck.prev = ck.kl = ck.kd = ck.nd = 0;
+                        ck.eob = false;
+                        ck.st = FBK_RUN;
+                    }
+                }
+            }
+            nxt += nidle;
+        }
+        if (ph) {
+            const uint64_t now = clock64();
+            c_ref += now - tl;
+            tl = now;
+        }
+        const uint64_t bm = __ballot(busy);
+        if (!bm) {
+            if (nxt >= end) break;
+            continue;
+        }
+        n_out++;
+        n_busy += (uint64_t)__popcll(bm);
+        if (busy) {
+            fbk_step(ck, src, 16);
+            if (ck.st != FBK_RUN) {
+                if (ck.st == FBK_FAIL) list[idx] = e | FB_HIT_REJECT;
+                busy = false;
+            }
+        }
+        if (ph) {
+            const uint64_t now = clock64();
+            c_step += now - tl;
+            tl = now;
+        }
+    }
+    if (ph && lane == 0) {  // DMX_FB_DEBUG: refill and step cycles, steps, busy lanes per step
+        atomicAdd(ph + 8, (unsigned long long)c_ref);
+        atomicAdd(ph + 9, (unsigned long long)c_step);
+        atomicAdd(ph + 10, (unsigned long long)n_out);
+        atomicAdd(ph + 11, (unsigned long long)n_busy);
+        atomicAdd(ph + 12, 1ull);
+    }
 }
 
 // compact the per-chunk hits into one sorted list (offsets from the scan of counts)
@@ -650,7 +744,10 @@ constexpr int FBP_NT = 1024;
 constexpr uint32_t FBP_IN = 14336;    // staged words (a block body of up to ~56 KB: zlib's
                                       // blocks of 16 K symbols at up to ~27 bits each)
 constexpr uint32_t FBP_MINBITS = 128;  // shortest range a lane decodes
-constexpr uint32_t FBP_WARM = 320;     // warm-up bits before a range
+#ifndef DMX_FBP_WARM
+#define DMX_FBP_WARM 320
+#endif
+constexpr uint32_t FBP_WARM = DMX_FBP_WARM;  // warm-up bits before a range
 constexpr uint32_t TK_NOP = 4;         // a fixed block's end of block + the next fixed header
 constexpr int FBP_ROUNDS = 1024;  // a settle cascade (data that re-synchronises slowly) still
                                    // beats the serial decoder by far
@@ -1953,12 +2050,14 @@ hipError_t launch_fb_scan(const uint32_t* in_words, uint64_t misalign, uint64_t 
 
 hipError_t launch_fb_compact(const uint32_t* in_words, uint64_t misalign, uint64_t n, const uint32_t* counts,
                              const uint64_t* offs, const uint64_t* hits, uint64_t nchunks, uint64_t* list,
-                             uint64_t count, hipStream_t st) {
+                             uint64_t count, unsigned long long* ph, hipStream_t st) {
     hipLaunchKernelGGL(k_fb_compact, dim3((uint32_t)((nchunks + 255) / 256)), dim3(256), 0, st,
                        counts, offs, hits, nchunks, list);
-    if (count)
-        hipLaunchKernelGGL(k_fb_check, dim3((uint32_t)((count + 63) / 64)), dim3(64), 0, st, in_words, misalign,
-                           n, list, count);
+    if (count) {
+        // a wave per DMX_FBC_PER_WAVE candidates: its first 64, then refills as its lanes finish
+        const uint32_t g = (uint32_t)((count + DMX_FBC_PER_WAVE - 1) / DMX_FBC_PER_WAVE);
+        hipLaunchKernelGGL(k_fb_check, dim3(g), dim3(64), 0, st, in_words, misalign, n, list, count, ph);
+    }
     return hipGetLastError();
 }
 

@@ -14,8 +14,12 @@ for spec in ${SPECS:-bmp:0:1 text:64:1}; do
     cut -d, -f1-4 $(find $d -name "*kernel_stats.csv") | grep "k_fb" | sed 's/(.*)"//' | cut -c1-100
   done
 done
-# pdecode phase cycles (DMX_FB_DEBUG) of the in-tree build
+# pdecode / k_fb_units phase cycles (DMX_FB_DEBUG) of each build
 for spec in ${SPECS:-bmp:0:1 text:64:1}; do
-  DMX_FB_DEBUG=1 timeout -k 10 120 python3 tools/foreign_probe.py $spec > gpurun_out/abp5/dbg_${spec//:/_}.txt 2>&1 || true
-  echo "== debug $spec"; grep "pdecode cycles\|lane-parallel\|k_fb_units cycles" gpurun_out/abp5/dbg_${spec//:/_}.txt | tail -3 | cut -c1-400
+  for v in ${LIBS:-base}; do
+    lib=ab/libdmx_$v.so; [ $v = base ] && lib=deflate.hpp_amd/lib/libdmx.so
+    f=gpurun_out/abp5/dbg_${v}_${spec//:/_}.txt
+    DMX_LIB=$lib DMX_FB_DEBUG=1 timeout -k 10 120 python3 tools/foreign_probe.py $spec > $f 2>&1 || true
+    echo "== debug $v $spec"; grep "pdecode cycles\|k_fb_units cycles\|k_fb_check" $f | tail -3 | cut -c1-300
+  done
 done
