@@ -1709,7 +1709,10 @@ __global__ __launch_bounds__(FB_TNT) void k_fb_tails(const uint16_t* __restrict_
 //   k_fb_final      every output byte: an image byte, or its marker's window entry.
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t FB_WLIT = 0x80000000u;
-constexpr int FB_HOPS = 8;
+#ifndef DMX_FB_HOPS
+#define DMX_FB_HOPS 8
+#endif
+constexpr int FB_HOPS = DMX_FB_HOPS;
 constexpr uint32_t FB_WIN_BLK = 4096;  // window entries per k_fb_win_init workgroup
 __global__ __launch_bounds__(256) void k_fb_win_init(const uint16_t* __restrict__ img,
                                                      const uint64_t* __restrict__ offs,
@@ -1734,16 +1737,43 @@ __global__ __launch_bounds__(256) void k_fb_win_init(const uint16_t* __restrict_
     }
 }
 
+// Four entries per thread at a time: their hops are independent gathers, issued together.
 __global__ __launch_bounds__(256) void k_fb_win_jump(uint32_t* W, uint64_t nent, uint32_t* open, int round) {
     if (round > 0 && __builtin_nontemporal_load(&open[round - 1]) == 0) return;
     bool left = false;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nent; i += (uint64_t)gridDim.x * 256) {
-        uint32_t v = W[i];
-        if (v & FB_WLIT) continue;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; i0 < nent; i0 += 4 * stride) {
+        uint32_t v[4];
+        bool in[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t i = i0 + k * stride;
+            in[k] = i < nent;
+            v[k] = in[k] ? W[i] : FB_WLIT;
+        }
+        const bool todo = !((v[0] & v[1] & v[2] & v[3]) & FB_WLIT);
+        if (!todo) continue;
+        bool chg[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) chg[k] = !(v[k] & FB_WLIT);
 #pragma unroll 1
-        for (int h = 0; h < FB_HOPS && !(v & FB_WLIT); h++) v = W[v];
-        W[i] = v;
-        left |= !(v & FB_WLIT);
+        for (int h = 0; h < FB_HOPS; h++) {
+            uint32_t nv[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) nv[k] = W[(v[k] & FB_WLIT) ? 0u : v[k]];  // (entry 0: a valid index)
+            bool open_k = false;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                v[k] = (v[k] & FB_WLIT) ? v[k] : nv[k];
+                open_k |= !(v[k] & FB_WLIT);
+            }
+            if (!open_k) break;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (chg[k]) W[i0 + k * stride] = v[k];
+            left |= in[k] && !(v[k] & FB_WLIT);
+        }
     }
     if (__ballot(left) && lane_id() == 0) atomicOr(&open[round], 1u);
 }
