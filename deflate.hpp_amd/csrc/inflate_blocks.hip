@@ -1798,6 +1798,34 @@ __global__ __launch_bounds__(256) void k_fb_final(const uint16_t* img, const uin
     }
     uint64_t k = lo;
     uint64_t uoff = offs[k], uend = uoff + sizes[k];
+    if (W) {
+        // four entries per thread at a time, 256 apart (a wave's image loads, window reads and
+        // stores stay contiguous), their window reads issued together
+        for (uint64_t x0 = s0 + threadIdx.x; x0 < s1; x0 += 4 * 256) {
+            uint32_t e[4], wi[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) e[j] = x0 + 256 * j < s1 ? img[x0 + 256 * j] : 0u;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint64_t x = x0 + 256 * j;
+                while (x >= uend && x < s1) {
+                    k++;
+                    uoff = offs[k];
+                    uend = uoff + sizes[k];
+                }
+                // a marker's window entry (a marker before the stream start was flagged)
+                wi[j] = e[j] >= 0x8000u && k > 0 ? (uint32_t)(k * FB_RING - ((e[j] & 0x7FFFu) + 1)) : 0xFFFFFFFFu;
+            }
+            uint32_t wv[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) wv[j] = wi[j] == 0xFFFFFFFFu ? 0u : W[wi[j]];
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (x0 + 256 * j < s1)
+                    out[x0 + 256 * j] = e[j] < 0x8000u ? (uint8_t)e[j] : wi[j] != 0xFFFFFFFFu ? (uint8_t)wv[j] : (uint8_t)0;
+        }
+        return;
+    }
     for (uint64_t x = s0 + threadIdx.x; x < s1; x += 256) {
         while (x >= uend) {
             k++;
@@ -1806,9 +1834,7 @@ __global__ __launch_bounds__(256) void k_fb_final(const uint16_t* img, const uin
         }
         const uint32_t v = img[x];
         const uint64_t b = (v & 0x7FFFu) + 1;  // a marker before the stream start was flagged
-        if (W) {
-            out[x] = v < 0x8000u ? (uint8_t)v : k > 0 ? (uint8_t)W[k * FB_RING - b] : (uint8_t)0;
-        } else {
+        {
             const uint64_t s = uend - uoff;
             if (x - uoff >= s - min(s, (uint64_t)FB_RING)) continue;  // tail: k_fb_tails wrote it
             out[x] = v < 0x8000u ? (uint8_t)v : (b <= uoff ? out[uoff - b] : (uint8_t)0);
