@@ -373,7 +373,7 @@ def c3_record(torch, ctx, dev, stream):
                      "inflate_GBps": round(C3_N / (med * 1e-3) / 1e9, 3), "path": int(ctx.stats().path),
                      "roofline_frac": round((C3_N + len(st)) / (med * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
                      "bit_exact": ok}
-    res["zlib1"]["traffic"] = traffic_of("c3_zlib1:", ["k_fb_scan", "k_fb_compact", "k_fb_pdecode", "k_fb_units",
+    res["zlib1"]["traffic"] = traffic_of("c3_zlib1:", ["k_fb_scan", "k_fb_compact", "k_fb_check", "k_fb_pdecode", "k_fb_units",
                                                        "k_fb_win_init", "k_fb_win_jump", "k_fb_final"])
     res["zlib1"]["profile"] = profile_path("kstats_c3_zlib1.csv")
     return res

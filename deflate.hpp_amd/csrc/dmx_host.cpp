@@ -422,13 +422,14 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     if (decode(0, K) != DMX_OK) return DMX_ERR_DEVICE;
     if (dstats) {
         uint32_t hs[16];
-        unsigned long long ph[8];
+        unsigned long long ph[10];
         HIPCHK(hipMemcpyAsync(hs, dstats, 64, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(ph, dstats + 16, 64, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(ph, dstats + 16, 80, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         std::fprintf(stderr, "dmx fb: pdecode cycles per unit: stage %llu, header %llu, tables %llu, first pass %llu, "
-                     "settle %llu, recount %llu, scans %llu, words %llu\n",
-                     ph[0] / K, ph[1] / K, ph[2] / K, ph[3] / K, ph[4] / K, ph[5] / K, ph[6] / K, ph[7] / K);
+                     "settle %llu (%.1f rounds, %.1f lane redos), recount %llu, scans %llu, words %llu\n",
+                     ph[0] / K, ph[1] / K, ph[2] / K, ph[3] / K, ph[4] / K, (double)ph[8] / K, (double)ph[9] / K,
+                     ph[5] / K, ph[6] / K, ph[7] / K);
         std::fprintf(stderr, "dmx fb: %llu units: %u lane-parallel, %u serial, %u serial after a parallel block, %u weak; "
                      "serial because: header %u, unsettled %u, no end of block %u, bad end %u, capacity %u, "
                      "stream-start copy %u\n",

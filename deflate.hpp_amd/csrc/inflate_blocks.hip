@@ -990,6 +990,8 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             te = S.te2[round & 1];
             const uint32_t want = r == 0 ? 0 : S.endp[r - 1];
             const bool redo = r > 0 && r <= te && want != s;
+            if (ph && t == 0) atomicAdd(ph + 8, 1ull);  // DMX_FB_DEBUG: settle rounds
+            if (ph && redo) atomicAdd(ph + 9, 1ull);    // and lanes that redo
             if (!__syncthreads_or(redo)) {
                 settled = true;
                 break;
