@@ -357,17 +357,21 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
             if (strong[k]) next_strong = starts[k];
         }
     }
-    // Token words: at most one per bit up to where a unit can stop, plus room for the block
-    // that crosses its stop; a weak unit with a hard stop (a stored block -- two words -- then
-    // possibly fixed-code blocks up to the next dynamic one) gets 64 Ki words; a region head at
-    // most its staged first block.  A unit that fills its space stops softly and a repair unit
-    // continues it.  Inside a fixed-code region a token word covers at least 7 bits (fixed codes
-    // are 7-9 bits, three literals per word), so a third of a word per bit.  16-B groups.
+    // Token words: up to where a unit can stop, plus room for the block that crosses its stop.
+    // A token word takes at least 1.5 bits of stream: a match at least 2 (a lit/len and a
+    // distance code, each at least 1 bit), a word of literals up to three of them; the densest
+    // packing is a 1-bit literal then a 2-bit match, two words per 3 bits -- so 2/3 of a word per
+    // bit always suffices (C3 uses 0.37).  A weak unit with a hard stop (a stored block -- two
+    // words -- then possibly fixed-code blocks up to the next dynamic one) gets 64 Ki words; a
+    // region head at most its staged first block.  A unit that fills its space stops softly and
+    // a repair unit continues it.  Inside a fixed-code region a token word covers at least 7 bits
+    // (fixed codes are 7-9 bits, three literals per word), so a third of a word per bit.  16-B
+    // groups.
     auto words_of = [&](uint64_t pos, uint64_t stop) -> uint64_t {
         const uint64_t s = std::min<uint64_t>(stop & FB_STOP_MASK, nbits), p = std::min(pos, nbits);
         uint64_t w = 4096 + 65536;
-        if (stop & FB_STOP_REGION) w = std::min<uint64_t>(s - p, 458752 + 65536) + 4096;
-        else if (!(stop & FB_STOP_WEAK)) w = s - p + 4096;
+        if (stop & FB_STOP_REGION) w = std::min<uint64_t>(2 * (s - p) / 3, 458752 + 65536) + 4096;
+        else if (!(stop & FB_STOP_WEAK)) w = 2 * (s - p) / 3 + 4096;
         return (w + 63) & ~63ull;
     };
     auto region_words = [](uint64_t span) -> uint64_t { return ((span / 3 + 4096) + 63) & ~63ull; };
