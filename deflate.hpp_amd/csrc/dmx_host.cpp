@@ -237,7 +237,7 @@ int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, 
     const uint32_t slot_bytes = c->seg + 256;
     const uint32_t tok_stride = level >= 2 ? deflate_tok_stride(c->seg) : 0u;
     if (!c->slots.ensure(nseg * (size_t)slot_bytes) || !c->sizes.ensure(nseg * 4) ||
-        !c->offs.ensure(nseg * 8) || !c->scal.ensure(sizeof(Scal)) ||
+        !c->offs.ensure(scan_words(nseg) * 8) || !c->scal.ensure(sizeof(Scal)) ||
         !c->dtok.ensure(std::max<uint64_t>(1, nseg * (uint64_t)tok_stride) * 4) || !c->dntok.ensure(nseg * 4))
         return DMX_ERR_NOMEM;
     DeflateArgs A;
@@ -290,7 +290,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     const uint64_t misalign = (uintptr_t)d_in & 3;
     const uint32_t* words = reinterpret_cast<const uint32_t*>(d_in - misalign);
     const uint64_t nc = fb_scan_chunks(n);
-    if (!c->fbc.ensure(nc * 4) || !c->fbh.ensure(nc * fb_hits_per_chunk() * 8) || !c->fbo.ensure(nc * 8 + 8))
+    if (!c->fbc.ensure(nc * 4) || !c->fbh.ensure(nc * fb_hits_per_chunk() * 8) || !c->fbo.ensure(scan_words(nc) * 8))
         return DMX_OK;
     HIPCHK(launch_fb_scan(words, misalign, n, c->fbc.as<uint32_t>(), c->fbh.as<uint64_t>(),
                           c->fbo.as<uint64_t>(), &ds->nmarkers, st));
@@ -702,7 +702,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
 
     // candidate segment starts
     const uint64_t ntiles = marker_tiles(n, misalign);
-    if (!c->tiles.ensure(ntiles * 4) || !c->tileoffs.ensure(ntiles * 8)) return DMX_ERR_NOMEM;
+    if (!c->tiles.ensure(ntiles * 4) || !c->tileoffs.ensure(scan_words(ntiles) * 8)) return DMX_ERR_NOMEM;
     HIPCHK(launch_marker_count(words, misalign, n, c->tiles.as<uint32_t>(), ntiles, st));
     HIPCHK(launch_scan_u32(c->tiles.as<uint32_t>(), c->tileoffs.as<uint64_t>(), ntiles, &ds->nmarkers, st));
     uint64_t nmarkers = 0;
@@ -773,7 +773,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     uint32_t heavy = 0, heavy_limit = 0;
     if (path_env == -1 || path_env == 4) {
         const uint64_t words = std::min<uint64_t>(ncand * 16404ull, 8ull * n + 20ull * ncand);  // k_lane_caps
-        if (c->ltok.ensure(words * 4) && c->ltokoff.ensure((ncand + 1) * 8) &&
+        if (c->ltok.ensure(words * 4) && c->ltokoff.ensure(scan_words(ncand) * 8) &&
             c->lntok.ensure(ncand * 4) && c->lcaps.ensure(ncand * 4)) {
             plan[np][0] = 4, plan[np][1] = c->seg, np++;
             if (heavy_bytes && ncand < 0xFFFFFFF0ull && c->lheavy.ensure((ncand + 2) * 4)) {
@@ -1538,7 +1538,7 @@ int dmx_segment_starts_device(dmx_ctx* c, const void* d_in, size_t n, uint64_t* 
     const uint64_t misalign = (uintptr_t)in & 3;
     const uint32_t* words = reinterpret_cast<const uint32_t*>(in - misalign);
     const uint64_t ntiles = marker_tiles(n, misalign);
-    if (!c->tiles.ensure(ntiles * 4) || !c->tileoffs.ensure(ntiles * 8)) return DMX_ERR_NOMEM;
+    if (!c->tiles.ensure(ntiles * 4) || !c->tileoffs.ensure(scan_words(ntiles) * 8)) return DMX_ERR_NOMEM;
     HIPCHK(launch_marker_count(words, misalign, n, c->tiles.as<uint32_t>(), ntiles, st));
     HIPCHK(launch_scan_u32(c->tiles.as<uint32_t>(), c->tileoffs.as<uint64_t>(), ntiles, &ds->nmarkers, st));
     uint64_t nm = 0;

@@ -102,6 +102,9 @@ hipError_t launch_marker_write(const uint32_t* in_words, uint64_t misalign, uint
                                const uint64_t* tile_offs, uint64_t ntiles, uint64_t* cands,
                                uint64_t* ncand_out, hipStream_t st);
 uint64_t marker_tiles(uint64_t n, uint64_t misalign);
+// exclusive scan of n values into offs (64-bit) and *total; offs must hold scan_words(n)
+// entries (the block sums of the multi-workgroup scan follow the n offsets)
+uint64_t scan_words(uint64_t n);
 hipError_t launch_scan_u32(const uint32_t* v, uint64_t* offs, uint64_t n, uint64_t* total,
                            hipStream_t st);
 hipError_t launch_inflate_segments(const InflateArgs& A, hipStream_t st, hipEvent_t ev0,

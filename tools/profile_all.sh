@@ -27,7 +27,7 @@ if [ "$mode" = collect ]; then
   if [ -d $P/s_c3 ]; then
     cp $(ls -t $(find $P/s_c3 -name "*kernel_stats.csv") | head -1) profiles/${tag}_kstats_c3_zlib1.csv
     for k in k_fb_scan k_fb_compact k_fb_check k_fb_pdecode k_fb_units k_fb_win_init k_fb_win_jump k_fb_final \
-             k_marker_count k_marker_write k_scan_sizes; do
+             k_marker_count k_marker_write k_scan_part k_scan_apply; do
       python3 tools/traffic.py $P/f_c3 $P/w_c3 c3_zlib1:$k $k profiles/traffic.json || true
     done
   fi
