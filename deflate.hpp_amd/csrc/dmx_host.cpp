@@ -75,6 +75,9 @@ struct dmx_ctx {
     DevBuf fbc, fbh, fbo, fbl, fbs, fbt, fbk, fbu, fbch, fbco, fbcs, fbimg, fbstop, fbwin, fbopen;
     DevBuf fbvm, fbvh;  // per-unit start mode and code state (region and repair units)
     DevBuf fbph;  // DMX_FB_DEBUG: k_fb_units phase cycles
+    // path 5: the accepted unit starts, written by k_fb_check straight into host memory
+    uint64_t* fbkeep_h = nullptr;
+    uint64_t* fbkeep_d = nullptr;
     DevBuf fbreg, fbJ, fbvis;  // fixed-code regions: {E, T, first super block} + super-block regions, jumps, visits
     DevBuf ck;  // checksum scratch (checksum.hip) + the 4-byte result at its start
     bool timing = false;
@@ -127,6 +130,7 @@ struct Scal {  // small device-side scalars, one allocation
     uint64_t nmarkers;
     uint32_t ticket;
     uint32_t fb_err;  // block-parallel path: a copy reached before the stream start
+    uint32_t fb_nkeep;  // block-parallel path: accepted unit starts (k_fb_check)
     InflateResult res;
     ValidateWords vw;
 };
@@ -294,29 +298,69 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         return DMX_OK;
     HIPCHK(launch_fb_scan(words, misalign, n, c->fbc.as<uint32_t>(), c->fbh.as<uint64_t>(),
                           c->fbo.as<uint64_t>(), &ds->nmarkers, st));
+    // The check appends the accepted starts to a host-mapped list, so one sync gives them (the
+    // candidate count need not come back first); its grid is sized for the most the scan can
+    // list.  Without that list (or when it overflows) the candidates come back in two steps.
+    constexpr uint32_t kKeepCap = 1u << 20;
+    if (!c->fbkeep_h) {
+        void* h = nullptr;
+        if (hipHostMalloc(&h, kKeepCap * 8ull, hipHostMallocMapped) == hipSuccess) {
+            void* d = nullptr;
+            if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess) {
+                c->fbkeep_h = static_cast<uint64_t*>(h);
+                c->fbkeep_d = static_cast<uint64_t*>(d);
+            } else {
+                (void)hipHostFree(h);
+            }
+        }
+    }
+    const uint64_t max_hits = nc * (uint64_t)fb_hits_per_chunk();
+    const bool one_sync = c->fbkeep_d && c->fbl.ensure(max_hits * 8);
+    unsigned long long* cph = nullptr;  // DMX_FB_DEBUG: k_fb_check counters
+    if ((c->diag & DIAG_FB) && c->fbph.ensure(256)) {
+        cph = c->fbph.as<unsigned long long>();
+        HIPCHK(hipMemsetAsync(cph, 0, 256, st));
+    }
     uint64_t nhits = 0;
-    HIPCHK(hipMemcpyAsync(&nhits, &ds->nmarkers, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    std::vector<uint64_t> hits(nhits);
-    if (nhits) {
-        if (!c->fbl.ensure(nhits * 8)) return DMX_OK;
-        unsigned long long* cph = nullptr;  // DMX_FB_DEBUG: k_fb_check counters
-        if ((c->diag & DIAG_FB) && c->fbph.ensure(256)) {
-            cph = c->fbph.as<unsigned long long>();
-            HIPCHK(hipMemsetAsync(cph, 0, 256, st));
-        }
+    std::vector<uint64_t> hits;
+    bool have_hits = false;
+    if (one_sync) {
+        HIPCHK(hipMemsetAsync(&ds->fb_nkeep, 0, 4, st));
         HIPCHK(launch_fb_compact(words, misalign, n, c->fbc.as<uint32_t>(), c->fbo.as<uint64_t>(),
-                                 c->fbh.as<uint64_t>(), nc, c->fbl.as<uint64_t>(), nhits,
-                                 cph, st));
-        if (cph) {
-            unsigned long long q[5];
-            HIPCHK(hipMemcpyAsync(q, cph + 8, sizeof(q), hipMemcpyDeviceToHost, st));
-            HIPCHK(hipStreamSynchronize(st));
-            const unsigned long long w = q[4] ? q[4] : 1;
-            std::fprintf(stderr, "dmx fb: k_fb_check %llu candidates, %llu waves: per wave refill %llu cycles, "
-                         "steps %llu cycles, %llu steps, %.1f busy lanes per step\n", (unsigned long long)nhits, w,
-                         q[0] / w, q[1] / w, q[2] / w, q[2] ? (double)q[3] / (double)q[2] : 0.0);
+                                 c->fbh.as<uint64_t>(), nc, c->fbl.as<uint64_t>(), &ds->nmarkers, max_hits, cph,
+                                 c->fbkeep_d, &ds->fb_nkeep, kKeepCap, st));
+        uint32_t nkeep = 0;
+        HIPCHK(hipMemcpyAsync(&nhits, &ds->nmarkers, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(&nkeep, &ds->fb_nkeep, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (nkeep <= kKeepCap) {
+            hits.assign(c->fbkeep_h, c->fbkeep_h + nkeep);
+            std::sort(hits.begin(), hits.end(), [](uint64_t a, uint64_t b) {
+                return (a & FB_STOP_MASK) < (b & FB_STOP_MASK);
+            });
+            have_hits = true;
         }
+    } else {
+        HIPCHK(hipMemcpyAsync(&nhits, &ds->nmarkers, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (nhits) {
+            if (!c->fbl.ensure(nhits * 8)) return DMX_OK;
+            HIPCHK(launch_fb_compact(words, misalign, n, c->fbc.as<uint32_t>(), c->fbo.as<uint64_t>(),
+                                     c->fbh.as<uint64_t>(), nc, c->fbl.as<uint64_t>(), &ds->nmarkers, nhits, cph,
+                                     nullptr, nullptr, 0, st));
+        }
+    }
+    if (cph) {
+        unsigned long long q[5];
+        HIPCHK(hipMemcpyAsync(q, cph + 8, sizeof(q), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        const unsigned long long w = q[4] ? q[4] : 1;
+        std::fprintf(stderr, "dmx fb: k_fb_check %llu candidates, %llu waves: per wave refill %llu cycles, "
+                     "steps %llu cycles, %llu steps, %.1f busy lanes per step\n", (unsigned long long)nhits, w,
+                     q[0] / w, q[1] / w, q[2] / w, q[2] ? (double)q[3] / (double)q[2] : 0.0);
+    }
+    if (!have_hits && nhits) {  // the candidates with their reject marks
+        hits.resize(nhits);
         HIPCHK(hipMemcpyAsync(hits.data(), c->fbl.p, nhits * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
     }
@@ -1354,6 +1398,7 @@ void dmx_destroy(dmx_ctx* c) {
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_df) (void)hipEventDestroy(c->ev_df);
+    if (c->fbkeep_h) (void)hipHostFree(c->fbkeep_h);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }

@@ -175,12 +175,15 @@ hipError_t launch_fb_scan(const uint32_t* in_words, uint64_t misalign, uint64_t 
                           uint32_t* counts, uint64_t* hits, uint64_t* offs, uint64_t* nhits,
                           hipStream_t st);
 // compacts the scan's candidates into one sorted list of count entries and runs the full header
-// test on them (k_fb_check): a candidate that fails it gets FB_HIT_REJECT.  ph: DMX_FB_DEBUG
-// counters (or nullptr)
+// test on them (k_fb_check): a candidate that fails it gets FB_HIT_REJECT.  *pcount: the
+// candidates (device), max_count: the most there can be (sizes the grids).  keep (host memory
+// mapped into the device, or nullptr): the accepted starts, unordered, *nkeep of them (entries
+// past keep_cap dropped).  ph: DMX_FB_DEBUG counters (or nullptr)
 constexpr uint64_t FB_HIT_REJECT = 1ull << 63;
 hipError_t launch_fb_compact(const uint32_t* in_words, uint64_t misalign, uint64_t n, const uint32_t* counts,
                              const uint64_t* offs, const uint64_t* hits, uint64_t nchunks, uint64_t* list,
-                             uint64_t count, unsigned long long* ph, hipStream_t st);
+                             const uint64_t* pcount, uint64_t max_count, unsigned long long* ph, uint64_t* keep,
+                             uint32_t* nkeep, uint32_t keep_cap, hipStream_t st);
 // hits carry bit 62 for a stored-block header; stops[u] = the next dynamic-header start after u
 // units [u0, u0 + count) of the nunits listed; vmode / vhdr as above
 // fixed-code regions (k_fb_smap + k_fb_swalk): reg = nreg x {E, T, first super block}, sbreg =

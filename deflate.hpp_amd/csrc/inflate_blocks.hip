@@ -350,8 +350,19 @@ __device__ __forceinline__ void fbk_step(FbLengthCheck& c, const FbcCol& src, in
         if (bad) c.st = FBK_FAIL;
     }
 }
+// A candidate that passes (and every stored-header hit) is also appended to keep (host memory
+// mapped into the device; *nkeep counts, entries past keep_cap are dropped): the host reads the
+// accepted starts -- a few hundred -- instead of the whole candidate list.
 __global__ __launch_bounds__(64) void k_fb_check(const uint32_t* in_words, uint64_t misalign, uint64_t n,
-                                                  uint64_t* list, uint64_t count, unsigned long long* ph) {
+                                                  uint64_t* list, const uint64_t* pcount, unsigned long long* ph,
+                                                  uint64_t* keep, uint32_t* nkeep, uint32_t keep_cap) {
+    const uint64_t count = *pcount;  // (the grid is sized for the most the scan could list)
+    if ((uint64_t)blockIdx.x * DMX_FBC_PER_WAVE >= count) return;
+    auto accept = [&](uint64_t e) {
+        if (!keep) return;
+        const uint32_t k = atomicAdd(nkeep, 1u);
+        if (k < keep_cap) keep[k] = e;
+    };
     __shared__ uint32_t stg[FBC_WORDS * 64];
     __shared__ __attribute__((aligned(16))) uint8_t tabs[128 * 64];
     const uint32_t lane = threadIdx.x;
@@ -376,7 +387,9 @@ __global__ __launch_bounds__(64) void k_fb_check(const uint32_t* in_words, uint6
                 idx = nxt + (uint64_t)__popcll(idle & below);
                 if (idx < end) {
                     e = list[idx];
-                    if (!(e & FB_HIT_STORED)) {
+                    if (e & FB_HIT_STORED) {
+                        accept(e);
+                    } else {
                         busy = true;
                         const uint64_t q = misalign * 8 + e;
                         const uint64_t w0 = q >> 5;
@@ -428,6 +441,7 @@ __global__ __launch_bounds__(64) void k_fb_check(const uint32_t* in_words, uint6
             fbk_step(ck, src, 16);
             if (ck.st != FBK_RUN) {
                 if (ck.st == FBK_FAIL) list[idx] = e | FB_HIT_REJECT;
+                else accept(e);
                 busy = false;
             }
         }
@@ -2108,13 +2122,15 @@ hipError_t launch_fb_scan(const uint32_t* in_words, uint64_t misalign, uint64_t 
 
 hipError_t launch_fb_compact(const uint32_t* in_words, uint64_t misalign, uint64_t n, const uint32_t* counts,
                              const uint64_t* offs, const uint64_t* hits, uint64_t nchunks, uint64_t* list,
-                             uint64_t count, unsigned long long* ph, hipStream_t st) {
+                             const uint64_t* pcount, uint64_t max_count, unsigned long long* ph, uint64_t* keep,
+                             uint32_t* nkeep, uint32_t keep_cap, hipStream_t st) {
     hipLaunchKernelGGL(k_fb_compact, dim3((uint32_t)((nchunks + 255) / 256)), dim3(256), 0, st,
                        counts, offs, hits, nchunks, list);
-    if (count) {
+    if (max_count) {
         // a wave per DMX_FBC_PER_WAVE candidates: its first 64, then refills as its lanes finish
-        const uint32_t g = (uint32_t)((count + DMX_FBC_PER_WAVE - 1) / DMX_FBC_PER_WAVE);
-        hipLaunchKernelGGL(k_fb_check, dim3(g), dim3(64), 0, st, in_words, misalign, n, list, count, ph);
+        const uint32_t g = (uint32_t)((max_count + DMX_FBC_PER_WAVE - 1) / DMX_FBC_PER_WAVE);
+        hipLaunchKernelGGL(k_fb_check, dim3(g), dim3(64), 0, st, in_words, misalign, n, list, pcount, ph, keep, nkeep,
+                           keep_cap);
     }
     return hipGetLastError();
 }
