@@ -778,7 +778,7 @@ struct FbpSmem {
     uint32_t te2[2];
     uint32_t kind;            // 0 parallel, 1 serial from the unit start, 2 serial continuation,
                               // 3 an error the serial decoder would report (S.err), 4 again
-    uint32_t btype, bfinal, hs, nst, words, bytes, err;
+    uint32_t btype, bfinal, hs, nst, nst1, words, bytes, err;  // nst1: words staged so far
     uint32_t midend;          // the unit stopped inside a block (soft stop)
     uint32_t crossed;         // the settled path passed a fixed-block header (TK_NOP)
     uint64_t ws, he, hecap, endbit;
@@ -831,6 +831,18 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
     const uint64_t nbits = 8 * A.n;
     const bool rfc = (A.flags & DMX_CFG_RFC_STRICT) != 0;
     const bool stream_start = u == 0 && !(A.flags & DMX_IFLAG_PIECE);
+    auto stage_rest = [&]() {  // the staging window past S.nst1 (all threads; the caller syncs)
+        for (uint32_t i = S.nst1 + t; i < S.nst + 8; i += FBP_NT) {
+            uint32_t v = 0;
+            if (i < S.nst) {
+                const uint64_t wi = S.ws + i;
+                v = A.in_words[wi];
+                const uint64_t lim = end_bytes - 4 * wi;
+                if (lim < 4) v &= (1u << (8 * lim)) - 1u;
+            }
+            S.in[i] = v;
+        }
+    };
     auto hdr3 = [&](uint64_t b) -> uint32_t {  // the 3 header bits at aligned-image bit b
         const uint32_t w0 = A.in_words[b >> 5];
         const uint32_t w1 = (b >> 5) + 1 < nwords ? A.in_words[(b >> 5) + 1] : 0u;
@@ -865,6 +877,10 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             S.nst = (uint32_t)(min(ws + FBP_IN - 13, nwords) - ws);
             S.he = min(stop, hecap);
             S.hecap = hecap;
+            // the first attempt reads up to he (and a token's lookahead): stage that much; the
+            // rest only for a second attempt (a C3 unit's block is ~15 KB of the 56 KB window)
+            // (at least 160 words past the start: the header a wave reads first)
+            S.nst1 = (uint32_t)min((uint64_t)S.nst, max(((base + S.he) >> 5) - ws + 16, (b >> 5) - ws + 160));
         }
         // a region head whose first block is not dynamic: the unit is empty, the region map
         // takes the run of blocks from its header on
@@ -880,7 +896,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
     __syncthreads();
     if (S.kind == 0) {
         const uint64_t ws = S.ws;
-        const uint32_t nst = S.nst;
+        const uint32_t nst = S.nst1;
         for (uint32_t i = t; i < nst + 8; i += FBP_NT) {
             uint32_t v = 0;
             if (i < nst) {
@@ -923,6 +939,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
         }
         __syncthreads();
         stamp(1);
+        if (S.kind == 0 && S.he == S.hecap) stage_rest();  // the stop lay inside the header
         if (S.kind == 0) {
             fill_lut32_wg<PJ_LL, false>(S.llut, S.T.lm, S.T.lsorted, t, FBP_NT);
             fill_lut32_wg<PJ_LD, true>(S.dlut, S.T.dm, S.T.dsorted, t, FBP_NT);
@@ -1065,6 +1082,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
         const uint32_t kk = S.kind;
         if (kk != 0) {
             __syncthreads();  // every lane has read it
+            if (kk == 4) stage_rest();  // again up to the staging's end
             if (kk == 4 && t == 0) S.kind = 0;
             __syncthreads();
             continue;
