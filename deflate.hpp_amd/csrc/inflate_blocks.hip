@@ -790,13 +790,13 @@ static_assert(sizeof(FbpSmem) <= 160 * 1024, "LDS");
 // header reader's registers would otherwise spill in the 1024-lane kernel)
 __device__ __attribute__((noinline)) uint32_t fbp_header(Tables& T, uint32_t btype, const uint32_t* in,
                                                          uint64_t ws, uint32_t nst, uint64_t* hp,
-                                                         uint64_t end_bits, bool rfc) {
+                                                         uint64_t end_bits, bool rfc, uint64_t* stamps) {
     if (btype == 1) {
         load_fixed(T);
         return 0;
     }
     const StagedWords src{in, ws, nst};
-    return fast_header(src, hp, end_bits, T, rfc, false);
+    return fast_header(src, hp, end_bits, T, rfc, false, stamps);
 }
 // the same for the header of the block a mid-block unit starts in, read from HBM
 __device__ __attribute__((noinline)) uint32_t fbp_header_g(Tables& T, const uint32_t* words, uint64_t nwords,
@@ -913,7 +913,10 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             uint64_t hp = base + start + 3;
             uint32_t err = 0;
             if (vm == FB_V_HEADER) {
-                err = fbp_header(S.T, S.btype, S.in, ws, nst, &hp, end_bytes * 8, rfc);
+                uint64_t hst[4] = {0, 0, 0, 0};  // DMX_FB_DEBUG: the header's phases
+                err = fbp_header(S.T, S.btype, S.in, ws, nst, &hp, end_bytes * 8, rfc, ph ? hst : nullptr);
+                if (ph && lane_id() == 0)
+                    for (int k = 0; k < 4; k++) atomicAdd(ph + 10 + k, (unsigned long long)hst[k]);
             } else {
                 if (S.btype == 1) {
                     load_fixed(S.T);
