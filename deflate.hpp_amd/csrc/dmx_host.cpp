@@ -78,6 +78,10 @@ struct dmx_ctx {
     // path 5: the accepted unit starts, written by k_fb_check straight into host memory
     uint64_t* fbkeep_h = nullptr;
     uint64_t* fbkeep_d = nullptr;
+    // path 5: pinned staging of host-to-device uploads (a copy from pageable memory goes through
+    // the driver's own staging); reused per batch -- a stream sync separates the batches
+    uint8_t* pin = nullptr;
+    size_t pin_cap = 0, pin_off = 0;
     DevBuf fbreg, fbJ, fbvis;  // fixed-code regions: {E, T, first super block} + super-block regions, jumps, visits
     DevBuf ck;  // checksum scratch (checksum.hip) + the 4-byte result at its start
     bool timing = false;
@@ -95,8 +99,9 @@ namespace {
 //   DMX_DEBUG=1       names the failing HIP call on stderr (process-wide)
 //   DMX_PHASES=<file> per-phase s_memtime timelines of the segmented kernels
 //   DMX_FB_DEBUG=1    block-parallel path: unit outcomes and chain breaks on stderr
+//   DMX_FB_HOSTTIME=1 block-parallel path: host wall clock per phase on stderr
 //   DMX_RECS=1        segmented inflate: per-candidate outcome of each pass on stderr
-enum : uint32_t { DIAG_PHASES = 1, DIAG_FB = 2, DIAG_RECS = 4, DIAG_DEBUG = 8 };
+enum : uint32_t { DIAG_PHASES = 1, DIAG_FB = 2, DIAG_RECS = 4, DIAG_DEBUG = 8, DIAG_FBT = 16 };
 struct Diag {
     uint32_t bits = 0;
     std::string phases_path;
@@ -107,6 +112,7 @@ static const Diag& diag_env() {  // first use (a dmx_create) reads the environme
         if (std::getenv("DMX_DEBUG")) r.bits |= DIAG_DEBUG;
         if (const char* e = std::getenv("DMX_PHASES")) r.bits |= DIAG_PHASES, r.phases_path = e;
         if (const char* e = std::getenv("DMX_FB_DEBUG"); e && *e) r.bits |= DIAG_FB;
+        if (const char* e = std::getenv("DMX_FB_HOSTTIME"); e && *e) r.bits |= DIAG_FBT;
         if (std::getenv("DMX_RECS")) r.bits |= DIAG_RECS;
         return r;
     }();
@@ -286,11 +292,30 @@ int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, 
 // DMX_CFG_FB_SERIAL: path 5 decodes every unit with one wavefront (A/B reference for k_fb_pdecode)
 static bool fb_serial_only(const dmx_ctx* c) { return (c->flags & DMX_CFG_FB_SERIAL) != 0; }
 
+// host-to-device copy through the context's pinned staging (see dmx_ctx::pin); the caller
+// resets c->pin_off once the previous batch's copies are known complete
+static hipError_t pin_h2d(dmx_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
+    if (!bytes) return hipSuccess;
+    constexpr size_t kPinCap = 1u << 20;
+    if (!c->pin && hipHostMalloc(reinterpret_cast<void**>(&c->pin), kPinCap, hipHostMallocDefault) == hipSuccess)
+        c->pin_cap = kPinCap;
+    if (!c->pin || c->pin_off + bytes > c->pin_cap) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+    uint8_t* h = c->pin + c->pin_off;
+    std::memcpy(h, src, bytes);
+    c->pin_off += (bytes + 255) & ~size_t(255);
+    return hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, st);
+}
+
 int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_out, size_t cap,
                       size_t* total_out, uint8_t** dev_out, hipStream_t st, bool* handled, uint32_t iflags) {
     *handled = false;
     Scal* ds = c->scal.as<Scal>();
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
+    // DMX_FB_HOSTTIME: host-side wall clock per phase (us)
+    using hclock = std::chrono::steady_clock;
+    hclock::time_point ht[8];
+    auto hmark = [&](int k) { if (c->diag & DIAG_FBT) ht[k] = hclock::now(); };
+    hmark(0);
     const uint64_t misalign = (uintptr_t)d_in & 3;
     const uint32_t* words = reinterpret_cast<const uint32_t*>(d_in - misalign);
     const uint64_t nc = fb_scan_chunks(n);
@@ -364,6 +389,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         HIPCHK(hipMemcpyAsync(hits.data(), c->fbl.p, nhits * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
     }
+    hmark(1);
     // units: bit 0, then every hit (sorted: chunks in order, lanes in order within a chunk);
     // dynamic-header hits are "strong" (practically never false), stored-header hits "weak".
     // A gap of more than kRegionGap bits between two strong starts is a run of blocks the scan
@@ -442,15 +468,18 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         !c->fbu.ensure(Kcap * sizeof(FbUnit)) || !c->fbstop.ensure(Kcap * 8) || !c->fbvm.ensure(Kcap) ||
         !c->fbvh.ensure(Kcap * 8))
         return DMX_OK;
-    auto upload = [&](uint64_t k0, uint64_t cnt) -> int {
-        HIPCHK(hipMemcpyAsync(c->fbs.as<uint64_t>() + k0, &starts[k0], cnt * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(c->fbstop.as<uint64_t>() + k0, &stops[k0], cnt * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(c->fbt.as<uint64_t>() + k0, &tokoff[k0], (cnt + 1) * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(c->fbvm.as<uint8_t>() + k0, &vmode[k0], cnt, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(c->fbvh.as<uint64_t>() + k0, &vhdr[k0], cnt * 8, hipMemcpyHostToDevice, st));
+    auto upload = [&](uint64_t k0, uint64_t cnt) -> int {  // (each batch follows a stream sync)
+        c->pin_off = 0;
+        HIPCHK(pin_h2d(c, c->fbs.as<uint64_t>() + k0, &starts[k0], cnt * 8, st));
+        HIPCHK(pin_h2d(c, c->fbstop.as<uint64_t>() + k0, &stops[k0], cnt * 8, st));
+        HIPCHK(pin_h2d(c, c->fbt.as<uint64_t>() + k0, &tokoff[k0], (cnt + 1) * 8, st));
+        HIPCHK(pin_h2d(c, c->fbvm.as<uint8_t>() + k0, &vmode[k0], cnt, st));
+        HIPCHK(pin_h2d(c, c->fbvh.as<uint64_t>() + k0, &vhdr[k0], cnt * 8, st));
         return DMX_OK;
     };
+    hmark(2);
     if (upload(0, K) != DMX_OK) return DMX_ERR_DEVICE;
+    hmark(3);
     const bool fb_debug = (c->diag & DIAG_FB) != 0;  // developer aid: unit outcomes, chain breaks
     uint32_t* dstats = nullptr;
     if (fb_debug && c->fbopen.ensure(256)) {
@@ -468,6 +497,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         return DMX_OK;
     };
     if (decode(0, K) != DMX_OK) return DMX_ERR_DEVICE;
+    hmark(4);
     if (dstats) {
         uint32_t hs[16];
         unsigned long long ph[14];
@@ -690,9 +720,11 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     } else if (total > cap) {
         return DMX_ERR_CAPACITY;
     }
-    HIPCHK(hipMemcpyAsync(c->fbch.p, chain.data(), nch * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->fbco.p, coffs.data(), nch * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->fbcs.p, csizes.data(), nch * 8, hipMemcpyHostToDevice, st));
+    hmark(5);
+    c->pin_off = 0;  // (the chain walk followed a stream sync)
+    HIPCHK(pin_h2d(c, c->fbch.p, chain.data(), nch * 4, st));
+    HIPCHK(pin_h2d(c, c->fbco.p, coffs.data(), nch * 8, st));
+    HIPCHK(pin_h2d(c, c->fbcs.p, csizes.data(), nch * 8, st));
     HIPCHK(hipMemsetAsync(&ds->fb_err, 0, 4, st));
     // the parallel window hand-off when its scratch fits (nch * 128 KiB), else the serial one
     uint32_t *win = nullptr, *open = nullptr;
@@ -716,6 +748,13 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         HIPCHK(hipStreamSynchronize(st));
         std::fprintf(stderr, "dmx fb: k_fb_units cycles per unit: batches %llu, expansion %llu, jumping %llu (%llu rounds "
                      "in all), write-out %llu\n", ph[0] / nch, ph[1] / nch, ph[2] / nch, ph[4], ph[3] / nch);
+    }
+    hmark(6);
+    if (c->diag & DIAG_FBT) {
+        auto us = [&](int a, int b) { return std::chrono::duration<double, std::micro>(ht[b] - ht[a]).count(); };
+        std::fprintf(stderr, "dmx fb: host us: scan+check+starts %.1f, unit setup %.1f, upload %.1f, pass-1 decode "
+                     "(launch to records) %.1f, chain walk %.1f, chain upload + launches %.1f\n", us(0, 1), us(1, 2),
+                     us(2, 3), us(3, 4), us(4, 5), us(5, 6));
     }
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     uint32_t ferr = 0;
@@ -1401,6 +1440,7 @@ void dmx_destroy(dmx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->ev_df) (void)hipEventDestroy(c->ev_df);
     if (c->fbkeep_h) (void)hipHostFree(c->fbkeep_h);
+    if (c->pin) (void)hipHostFree(c->pin);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
