@@ -1750,6 +1750,7 @@ constexpr uint32_t FB_WLIT = 0x80000000u;
 #define DMX_FB_HOPS 8
 #endif
 constexpr int FB_HOPS = DMX_FB_HOPS;
+constexpr uint32_t FB_WIN_ROUNDS = 3;  // jump rounds launched (k_fb_final finishes the chains)
 constexpr uint32_t FB_WIN_BLK = 4096;  // window entries per k_fb_win_init workgroup
 __global__ __launch_bounds__(256) void k_fb_win_init(const uint16_t* __restrict__ img,
                                                      const uint64_t* __restrict__ offs,
@@ -1855,7 +1856,11 @@ __global__ __launch_bounds__(256) void k_fb_final(const uint16_t* img, const uin
             }
             uint32_t wv[4];
 #pragma unroll
-            for (int j = 0; j < 4; j++) wv[j] = wi[j] == 0xFFFFFFFFu ? 0u : W[wi[j]];
+            for (int j = 0; j < 4; j++) wv[j] = wi[j] == 0xFFFFFFFFu ? FB_WLIT : W[wi[j]];
+            // an entry the (at most FB_WIN_ROUNDS) jump rounds left open: follow it to its byte
+#pragma unroll
+            for (int j = 0; j < 4; j++)  // (entries point strictly back: the walk ends; bounded anyway)
+                for (uint32_t h = 0; h < (1u << 20) && !(wv[j] & FB_WLIT); h++) wv[j] = W[wv[j]];
 #pragma unroll
             for (int j = 0; j < 4; j++)
                 if (x0 + 256 * j < s1)
@@ -2192,7 +2197,9 @@ hipError_t launch_fb_resolve(const uint8_t* stream, const uint64_t* starts, cons
         const uint64_t nent = fb_window_entries(nchain);
         hipLaunchKernelGGL(k_fb_win_init, dim3((uint32_t)nchain, FB_RING / FB_WIN_BLK), dim3(256), 0, st,
                            img, offs, sizes, win);
-        const uint32_t rounds = fb_window_rounds(nchain);
+        // a few rounds resolve almost every entry (C3: the third finds nothing left); k_fb_final
+        // follows the rest to their bytes instead of ceil(log2 units) + 1 early-returning launches
+        const uint32_t rounds = std::min<uint32_t>(fb_window_rounds(nchain), FB_WIN_ROUNDS);
         (void)hipMemsetAsync(open, 0, rounds * 4, st);
         // one grid-striding wave of workgroups per round: a round with nothing left returns in
         // microseconds.  (Round 4 ran all rounds in one cooperative launch with a grid barrier
