@@ -1750,7 +1750,10 @@ constexpr uint32_t FB_WLIT = 0x80000000u;
 #define DMX_FB_HOPS 8
 #endif
 constexpr int FB_HOPS = DMX_FB_HOPS;
-constexpr uint32_t FB_WIN_ROUNDS = 3;  // jump rounds launched (k_fb_final finishes the chains)
+#ifndef DMX_FB_WIN_ROUNDS
+#define DMX_FB_WIN_ROUNDS 2
+#endif
+constexpr uint32_t FB_WIN_ROUNDS = DMX_FB_WIN_ROUNDS;  // jump rounds launched (k_fb_final finishes the chains)
 constexpr uint32_t FB_WIN_BLK = 4096;  // window entries per k_fb_win_init workgroup
 __global__ __launch_bounds__(256) void k_fb_win_init(const uint16_t* __restrict__ img,
                                                      const uint64_t* __restrict__ offs,
