@@ -811,6 +811,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
     // DMX_FB_DEBUG: cycles per phase (thread 0), summed over units in stats[16..]
     unsigned long long* const ph = A.stats ? reinterpret_cast<unsigned long long*>(A.stats + 16) : nullptr;
     uint64_t ph_last = ph && t == 0 ? clock64() : 0;
+    const uint64_t ph_t0 = ph_last;
     auto stamp = [&](int k) {
         if (ph && t == 0) {
             const uint64_t now = clock64();
@@ -961,7 +962,9 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
         }
         return k;
     };
+    uint32_t dbg_rounds = 0, dbg_attempts = 0;  // DMX_FB_DEBUG (thread 0)
     for (int attempt = 0; attempt < 2 && S.kind == 0; attempt++) {
+        dbg_attempts++;
         const uint32_t* win = S.in;
         const uint32_t hs = S.hs, hlen = (uint32_t)(base + S.he - S.ws * 32 - hs);
         const uint32_t nl = max(1u, min((uint32_t)FBP_NT, hlen / FBP_MINBITS));
@@ -1025,6 +1028,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             const uint32_t want = r == 0 ? 0 : S.endp[r - 1];
             const bool redo = r > 0 && r <= te && want != s;
             if (ph && t == 0) atomicAdd(ph + 8, 1ull);  // DMX_FB_DEBUG: settle rounds
+            dbg_rounds++;
             if (ph && redo) atomicAdd(ph + 9, 1ull);    // and lanes that redo
             if (!__syncthreads_or(redo)) {
                 settled = true;
@@ -1230,6 +1234,13 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
             A.units[u].start = rstart;
             if (kind == 2 && crossed) A.units[u].flags |= SEGF_CROSSED;
         }
+    }
+    // DMX_FB_DEBUG: the longest unit of each kind (wave 0's span), in ph[14..17]: lane-parallel,
+    // serial from the start, serial after a parallel block, weak
+    if (ph && t == 0) {
+        const uint32_t slot = weak ? 3u : kind == 1 ? 1u : kind == 2 ? 2u : 0u;
+        const uint64_t dur = clock64() - ph_t0;  // (the longest's settle rounds and attempts below it)
+        atomicMax(ph + 14 + slot, (unsigned long long)((dur << 24) | (min(dbg_rounds, 4095u) << 4) | min(dbg_attempts, 15u)));
     }
 }
 

@@ -20,6 +20,6 @@ for spec in ${SPECS:-bmp:0:1 text:64:1}; do
     lib=ab/libdmx_$v.so; [ $v = base ] && lib=deflate.hpp_amd/lib/libdmx.so
     f=gpurun_out/abp5/dbg_${v}_${spec//:/_}.txt
     DMX_LIB=$lib DMX_FB_DEBUG=1 timeout -k 10 120 python3 tools/foreign_probe.py $spec > $f 2>&1 || true
-    echo "== debug $v $spec"; grep "pdecode cycles\|pdecode header\|k_fb_units cycles\|k_fb_check\|host us" $f | tail -5 | cut -c1-300
+    echo "== debug $v $spec"; grep "pdecode cycles\|pdecode header\|k_fb_units cycles\|k_fb_check\|host us\|longest" $f | tail -6 | cut -c1-300
   done
 done
