@@ -500,15 +500,16 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     hmark(4);
     if (dstats) {
         uint32_t hs[16];
-        unsigned long long ph[18];
+        unsigned long long ph[21];
         HIPCHK(hipMemcpyAsync(hs, dstats, 64, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(ph, dstats + 16, sizeof(ph), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         std::fprintf(stderr, "dmx fb: pdecode header cycles per unit: precode %llu, code lengths %llu, trees %llu, "
                      "tables %llu; longest unit: lane-parallel %llu, serial %llu, serial after a block %llu, weak %llu\n",
                      ph[10] / K, ph[11] / K, ph[12] / K, ph[13] / K, ph[14] >> 24, ph[15] >> 24, ph[16] >> 24, ph[17] >> 24);
-        std::fprintf(stderr, "dmx fb: longest lane-parallel unit: %llu settle rounds, %llu attempts\n",
-                     (ph[14] >> 4) & 4095, ph[14] & 15);
+        std::fprintf(stderr, "dmx fb: longest lane-parallel unit: %llu settle rounds, %llu attempts; "
+                     "settle re-decodes %llu cycles per unit\n",
+                     (ph[14] >> 4) & 4095, ph[14] & 15, ph[20] / K);
         std::fprintf(stderr, "dmx fb: pdecode cycles per unit: stage %llu, header %llu, tables %llu, first pass %llu, "
                      "settle %llu (%.1f rounds, %.1f lane redos), recount %llu, scans %llu, words %llu\n",
                      ph[0] / K, ph[1] / K, ph[2] / K, ph[3] / K, ph[4] / K, (double)ph[8] / K, (double)ph[9] / K,

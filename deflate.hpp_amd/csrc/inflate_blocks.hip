@@ -1035,6 +1035,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
                 break;
             }
             if (round == FBP_ROUNDS) break;
+            const uint64_t rd0 = ph && t == 0 ? clock64() : 0;
             if (redo) {
                 s = want;
                 uint32_t p = want, pa = hs + want, stn = 0;
@@ -1055,6 +1056,7 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
                 st = merged ? st1 : stn;
             }
             __syncthreads();
+            if (ph && t == 0) atomicAdd(ph + 20, (unsigned long long)(clock64() - rd0));  // DMX_FB_DEBUG
         }
         stamp(4);
         // ---- 4. the block's end; recount ranges that moved ----
