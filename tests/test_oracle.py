@@ -112,3 +112,21 @@ def test_oracle_quirk_path5_stream_matches_reference():
     assert len(s) == q["stream_len"] and hashlib.sha256(s).hexdigest() == q["stream_sha256"]
     out = orc.inflate(s)
     assert len(out) == q["out_len"] and hashlib.sha256(out).hexdigest() == q["out_sha256"]
+
+
+@pytest.mark.skipif(not Reference.available(), reason="oracle/_ref not built (no /root/reference)")
+def test_config0_test_bmp_round_trip_on_cpu(oracle):
+    """BASELINE config 0: deflate::compress + inflate::decompress of test.bmp on the CPU (the
+    reference's own case, deflate.hpp:779-815 / inflate.hpp:326).  Level 1 (literals only)
+    round-trips exactly; level 2 (the "fast" matcher, getMatches) is lossy by SURVEY A-1, and the
+    oracle must give the reference's own lossy bytes for it -- the checker the GPU tests rely on
+    agrees with the reference on the reference's streams."""
+    ref = Reference()
+    data = open(os.path.join(GOLD, "test.bmp"), "rb").read()
+    s1 = ref.compress(data, 1)
+    assert ref.decompress(s1) == data == oracle.inflate(s1)
+    s2 = ref.compress(data, 2)
+    out = ref.decompress(s2)
+    assert len(s2) < len(data) and len(out) == len(data)
+    assert oracle.inflate(s2) == out
+    assert out == open(os.path.join(GOLD, "expect", "ref_L2_test.bmp.bin"), "rb").read()
