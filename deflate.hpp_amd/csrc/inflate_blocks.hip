@@ -754,8 +754,14 @@ __global__ __launch_bounds__(64) void k_fb_decode(FbDecodeArgs A) {
 // unit 0 -- makes wave 0 decode the whole unit with fb_serial instead, so results and error
 // codes are the serial decoder's.
 // ---------------------------------------------------------------------------------------
-constexpr int FBP_NT = 1024;
-constexpr uint32_t FBP_IN = 14336;    // staged words (a block body of up to ~56 KB: zlib's
+#ifndef DMX_FBP_NT
+#define DMX_FBP_NT 1024
+#endif
+#ifndef DMX_FBP_IN
+#define DMX_FBP_IN 14336
+#endif
+constexpr int FBP_NT = DMX_FBP_NT;
+constexpr uint32_t FBP_IN = DMX_FBP_IN;  // staged words (a block body of up to ~56 KB: zlib's
                                       // blocks of 16 K symbols at up to ~27 bits each)
 constexpr uint32_t FBP_MINBITS = 128;  // shortest range a lane decodes
 #ifndef DMX_FBP_WARM
