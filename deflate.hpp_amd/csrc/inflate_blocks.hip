@@ -763,7 +763,10 @@ __global__ __launch_bounds__(64) void k_fb_decode(FbDecodeArgs A) {
 constexpr int FBP_NT = DMX_FBP_NT;
 constexpr uint32_t FBP_IN = DMX_FBP_IN;  // staged words (a block body of up to ~56 KB: zlib's
                                       // blocks of 16 K symbols at up to ~27 bits each)
-constexpr uint32_t FBP_MINBITS = 128;  // shortest range a lane decodes
+#ifndef DMX_FBP_MINBITS
+#define DMX_FBP_MINBITS 96
+#endif
+constexpr uint32_t FBP_MINBITS = DMX_FBP_MINBITS;  // shortest range a lane decodes
 #ifndef DMX_FBP_WARM
 #define DMX_FBP_WARM 320
 #endif
