@@ -312,7 +312,65 @@ struct FbcCol {
     FbGlobalBits g;
     __device__ uint32_t word(uint32_t k) const { return k < FBC_WORDS ? col[64 * k] : g.word(w0 + k); }
 };
+// DMX_FBK_DEFER (default): the tests that can only turn true once and stay true (a Kraft sum
+// past 1, the sequence past HLIT + HDIST, the header past plim, an invalid code, a repeat with
+// nothing before it) are folded into one sticky flag per symbol and decided once per call, so
+// the serial symbol loop -- a true header's ~230 symbols set each wave's time -- carries fewer
+// instructions; a failing candidate runs on for at most `steps` - 1 symbols.
+#ifndef DMX_FBK_DEFER
+#define DMX_FBK_DEFER 1
+#endif
+__device__ __forceinline__ void fbk_step_deferred(FbLengthCheck& c, const FbcCol& src, int steps) {
+    if (c.st != FBK_RUN) return;
+    uint32_t i = c.i, prev = c.prev, kl = c.kl, kd = c.kd, nd = c.nd, nb = c.nb, used = c.used, wi = c.wi;
+    uint64_t buf = c.buf;
+    bool eob = c.eob, bad = false;
+    const uint32_t nlit = c.nlit, total = c.total;
+    for (int k = 0; k < steps && i < total; k++) {
+        if (nb < 32) {  // refill: at least 32 bits stay in the buffer (a symbol takes <= 14)
+            buf |= (uint64_t)src.word(wi) << nb;
+            wi++;
+            nb += 32;
+        }
+        const uint32_t v = (uint32_t)buf;
+        uint32_t sym, len;
+        c.decode(v, &sym, &len);
+        const uint32_t x = sym >= 16 ? 4u * (sym - 16) : 12u;  // (symbols 19+ do not occur)
+        const uint32_t eb = (0x0732u >> x) & 15u;               // 16: 2, 17: 3, 18: 7 extra bits
+        const uint32_t run = ((0x1B33u >> x) & 15u) + ((v >> len) & ((1u << eb) - 1u));  // 3, 3, 11; 1
+        const uint32_t val = sym < 16 ? sym : sym == 16 ? prev : 0u;
+        const uint32_t cons = len + eb;
+        buf >>= cons;
+        nb -= cons;
+        used += cons;
+        const uint32_t a = i < nlit ? min(i + run, nlit) - i : 0u;
+        const uint32_t sh = 15 - (val ? val : 15u);
+        kl += val ? a << sh : 0u;
+        kd += val ? (run - a) << sh : 0u;
+        nd += val ? run - a : 0u;
+        eob |= val && i <= 256 && 256 < i + a;
+        bad |= !len || (sym == 16 && i == 0);
+        prev = val;
+        i += run;
+    }
+    c.i = i;
+    c.prev = prev;
+    c.kl = kl;
+    c.kd = kd;
+    c.nd = nd;
+    c.nb = nb;
+    c.used = used;
+    c.wi = wi;
+    c.buf = buf;
+    c.eob = eob;
+    if (bad || i > total || kl > 32768 || kd > 32768 || used > c.plim) c.st = FBK_FAIL;
+    else if (i == total) c.st = eob && kl == 32768 && (kd == 32768 || nd <= 1) ? FBK_PASS : FBK_FAIL;
+}
 __device__ __forceinline__ void fbk_step(FbLengthCheck& c, const FbcCol& src, int steps) {
+    if (DMX_FBK_DEFER) {
+        fbk_step_deferred(c, src, steps);
+        return;
+    }
     for (int k = 0; k < steps; k++) {
         if (c.st != FBK_RUN) break;
         if (c.i >= c.total) {
