@@ -317,6 +317,9 @@ struct FbcCol {
 // nothing before it) are folded into one sticky flag per symbol and decided once per call, so
 // the serial symbol loop -- a true header's ~230 symbols set each wave's time -- carries fewer
 // instructions; a failing candidate runs on for at most `steps` - 1 symbols.
+#ifndef DMX_FBK_STEPS
+#define DMX_FBK_STEPS 32  // symbols per fbk_step call (the wave refills idle lanes between calls)
+#endif
 #ifndef DMX_FBK_DEFER
 #define DMX_FBK_DEFER 1
 #endif
@@ -496,7 +499,7 @@ __global__ __launch_bounds__(64) void k_fb_check(const uint32_t* in_words, uint6
         n_out++;
         n_busy += (uint64_t)__popcll(bm);
         if (busy) {
-            fbk_step(ck, src, 16);
+            fbk_step(ck, src, DMX_FBK_STEPS);
             if (ck.st != FBK_RUN) {
                 if (ck.st == FBK_FAIL) list[idx] = e | FB_HIT_REJECT;
                 else accept(e);
