@@ -829,7 +829,7 @@ constexpr uint32_t FBP_IN = DMX_FBP_IN;  // staged words (a block body of up to 
 #endif
 constexpr uint32_t FBP_MINBITS = DMX_FBP_MINBITS;  // shortest range a lane decodes
 #ifndef DMX_FBP_WARM
-#define DMX_FBP_WARM 320
+#define DMX_FBP_WARM 448
 #endif
 constexpr uint32_t FBP_WARM = DMX_FBP_WARM;  // warm-up bits before a range
 constexpr uint32_t TK_NOP = 4;         // a fixed block's end of block + the next fixed header
