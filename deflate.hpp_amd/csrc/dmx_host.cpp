@@ -245,10 +245,13 @@ int deflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, int level, 
     }
     const uint64_t nseg = (n + c->seg - 1) / c->seg;
     const uint32_t slot_bytes = c->seg + 256;
-    const uint32_t tok_stride = level >= 2 ? deflate_tok_stride(c->seg) : 0u;
+    // the front kernel's segments: 64 KiB blocks are matched as two 32 KiB halves
+    const uint32_t fseg_bytes = std::min<uint32_t>(c->seg, 32768);
+    const uint64_t nfront = (n + fseg_bytes - 1) / fseg_bytes;
+    const uint32_t tok_stride = level >= 2 ? deflate_tok_stride(fseg_bytes) : 0u;
     if (!c->slots.ensure(nseg * (size_t)slot_bytes) || !c->sizes.ensure(nseg * 4) ||
         !c->offs.ensure(scan_words(nseg) * 8) || !c->scal.ensure(sizeof(Scal)) ||
-        !c->dtok.ensure(std::max<uint64_t>(1, nseg * (uint64_t)tok_stride) * 4) || !c->dntok.ensure(nseg * 4))
+        !c->dtok.ensure(std::max<uint64_t>(1, nfront * (uint64_t)tok_stride) * 4) || !c->dntok.ensure(nfront * 4))
         return DMX_ERR_NOMEM;
     DeflateArgs A;
     A.in = d_in;
@@ -594,7 +597,13 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
                 for (uint64_t k = first; k < Ku; k++) {
                     stops[k] = k + 1 < Ku ? (starts[k + 1] | FB_STOP_SOFT) : regs[r].T;
                     const uint64_t w = region_words(std::min(stops[k] & FB_STOP_MASK, nbits) - starts[k]);
-                    if (rep_used + w > rep_words) return DMX_OK;
+                    if (rep_used + w > rep_words) {
+                        if (fb_debug)  // (say so instead of a silent serial decode)
+                            std::fprintf(stderr, "dmx fb: region token space (%llu words) exhausted at unit %llu: "
+                                         "the serial decoder takes the stream\n",
+                                         (unsigned long long)rep_words, (unsigned long long)k);
+                        return DMX_OK;
+                    }
                     tokoff[k + 1] = tokoff[k] + w;
                     rep_used += w;
                     prim.push_back({starts[k], (uint8_t)(k == first ? 0 : 2)});
@@ -637,19 +646,44 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         return DMX_OK;
     };
     std::vector<std::pair<uint64_t, uint64_t>> repaired;  // (end bit, state) already given a repair unit
+    // A unit that starts on the chain (at bit 0, or exactly where the chain's last unit ended, in
+    // the code state it ended in) decodes the stream's own blocks from there, so an over-read or
+    // an undecodable code it reports is the error realDecompress meets (inflate.hpp:277-322):
+    // the stream ends with that error at once instead of a serial re-decode from bit 0 to find
+    // it again (a truncated 1 GiB stream took ~75 s on the serial decoder).  Only
+    // pure stream errors count; token space, staging or exotic-layout flags are this decoder's
+    // own limits and still go to the serial decoder.
+    auto stream_error = [&](const FbUnit& u) -> int {
+        constexpr uint32_t kStreamErr = SEGF_OVERREAD | SEGF_ERR_DATA;
+        if (!(u.flags & kStreamErr) || (u.flags & ~(kStreamErr | SEGF_CROSSED | SEGF_FINAL))) return DMX_OK;
+        return (u.flags & SEGF_OVERREAD) ? DMX_ERR_OVERREAD : DMX_ERR_DATA;  // as k_inflate_serial maps it
+    };
+    auto chain_error = [&](int rc, uint64_t k) {
+        if (fb_debug)
+            std::fprintf(stderr, "dmx fb: the chain meets a stream error at unit %llu (start %llu): %s\n",
+                         (unsigned long long)k, (unsigned long long)units[k].start, dmx_strerror(rc));
+        *handled = true;
+        *total_out = 0;
+        c->stats.segments = chain.size();
+        return rc;
+    };
     for (int round = 0;; round++) {
-        std::vector<std::pair<uint64_t, uint32_t>> by;  // (start, unit) of units decoded without error
+        std::vector<std::pair<uint64_t, uint32_t>> by, bad;  // (start, unit) decoded without / with an error
         by.reserve(Ku);
         for (uint64_t k = 0; k < Ku; k++)
-            if (!(units[k].flags & SEGF_ERRORS)) by.emplace_back(units[k].start, (uint32_t)k);
+            (units[k].flags & SEGF_ERRORS ? bad : by).emplace_back(units[k].start, (uint32_t)k);
         std::sort(by.begin(), by.end());
+        std::sort(bad.begin(), bad.end());
         chain.clear();
         coffs.clear();
         csizes.clear();
         total = 0;
         std::vector<std::pair<uint64_t, uint64_t>> breaks;  // (end bit, code state)
         bool fin = false;
-        if (units[0].flags & SEGF_ERRORS) return chain_break("unit error", 0);
+        if (units[0].flags & SEGF_ERRORS) {
+            if (const int rc = stream_error(units[0])) return chain_error(rc, 0);
+            return chain_break("unit error", 0);
+        }
         uint64_t k = 0;
         for (;;) {
             const FbUnit& u = units[k];
@@ -673,6 +707,12 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
             if (best != ~0ull) {
                 k = best;
                 continue;
+            }
+            if (breaks.empty()) {  // the first break: everything before it is the stream's true path
+                for (auto it = std::lower_bound(bad.begin(), bad.end(), std::make_pair(u.end, 0u));
+                     it != bad.end() && it->first == u.end; ++it)
+                    if (expects(it->second) == state)
+                        if (const int rc = stream_error(units[it->second])) return chain_error(rc, it->second);
             }
             breaks.emplace_back(u.end, state);
             // (optimistic: on with the unit after this one in start order)
@@ -812,7 +852,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     if (!out) {
         size_t freeb = 0, totb = 0;
         if (hipMemGetInfo(&freeb, &totb) != hipSuccess) freeb = 0;
-        const size_t want = ncand * (size_t)kSegCap;
+        const size_t want = ncand * (size_t)std::max<uint32_t>(kSegCap, c->seg);
         if ((want <= c->out.cap || want <= freeb / 2) && c->out.ensure(want)) {
             out = c->out.as<uint8_t>();
             cap = c->out.cap;
@@ -861,11 +901,14 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     r.status = 2;
     uint32_t heavy = 0, heavy_limit = 0;
     if (path_env == -1 || path_env == 4) {
-        const uint64_t words = std::min<uint64_t>(ncand * 16404ull, 8ull * n + 20ull * ncand);  // k_lane_caps
+        // k_lane_caps: min(8 bits, slot / 2 + 2) + 16 words per candidate, in groups of four
+        const uint64_t per = (std::max<uint64_t>(LN_OUT_CAP_BYTES, c->seg) / 2 + 2 + 16 + 3) & ~3ull;
+        const uint64_t words = std::min<uint64_t>(ncand * per, 8ull * n + 20ull * ncand);
         if (c->ltok.ensure(words * 4) && c->ltokoff.ensure(scan_words(ncand) * 8) &&
             c->lntok.ensure(ncand * 4) && c->lcaps.ensure(ncand * 4)) {
             plan[np][0] = 4, plan[np][1] = c->seg, np++;
-            if (heavy_bytes && ncand < 0xFFFFFFF0ull && c->lheavy.ensure((ncand + 2) * 4)) {
+            // (the workgroup decoder of the heavy route takes segments of <= 32 KiB)
+            if (heavy_bytes && c->seg <= 32768 && ncand < 0xFFFFFFF0ull && c->lheavy.ensure((ncand + 2) * 4)) {
                 if (c->ncu <= 0 && hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
                     c->ncu = 256;
                 heavy = (!heavy_env && ncand <= (uint64_t)c->ncu) ? 256u : heavy_bytes;
@@ -880,7 +923,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     } else if (path_env == 4) {
     } else if (few_bits && path_env != 2) {
         plan[np][0] = 0, plan[np][1] = 0, np++;
-    } else {
+    } else if (c->seg <= 32768) {  // (the workgroup decoder's slots are 16 or 32 KiB)
         plan[np][0] = 2, plan[np][1] = c->seg, np++;
         plan[np][0] = 3, plan[np][1] = c->seg, np++;
         plan[np][0] = 2, plan[np][1] = c->seg == 32768 ? 16384u : 32768u, np++;
@@ -1067,7 +1110,10 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     if (!fixed_out) {
         size_t freeb = 0, totb = 0;
         if (hipMemGetInfo(&freeb, &totb) != hipSuccess) freeb = 0;
-        const uint64_t guess = std::min<uint64_t>(64ull * n + (16ull << 20), freeb / 4);
+        // a generous first buffer saves the second pass on high-ratio streams, but it is kept
+        // by the context: bounded by 4 GiB (64 n alone held ~72 GiB for a 1 GiB
+        // stream); a larger output is counted by the first pass and decoded by a second
+        const uint64_t guess = std::min<uint64_t>({64ull * n + (16ull << 20), 4ull << 30, freeb / 4});
         if (c->out.cap < guess && !c->out.ensure(guess)) (void)c->out.ensure(1);
         A.out = c->out.as<uint8_t>();
         A.cap = c->out.p ? c->out.cap : 0;
@@ -1381,7 +1427,7 @@ int dmx_create(dmx_ctx** out, const dmx_config* cfg) {
     dmx_config d;
     dmx_config_default(&d);
     if (!cfg) cfg = &d;
-    if (cfg->segment_bytes != 16384 && cfg->segment_bytes != 32768) return DMX_ERR_ARG;
+    if (cfg->segment_bytes != 16384 && cfg->segment_bytes != 32768 && cfg->segment_bytes != 65536) return DMX_ERR_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return DMX_ERR_DEVICE;
     int dev = cfg->device;

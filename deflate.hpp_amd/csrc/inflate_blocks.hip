@@ -1910,7 +1910,8 @@ __global__ __launch_bounds__(256) void k_fb_win_jump(uint32_t* W, uint64_t nent,
 constexpr uint32_t FB_FIN_SPAN = 16384;
 __global__ __launch_bounds__(256) void k_fb_final(const uint16_t* img, const uint64_t* offs,
                                                   const uint64_t* sizes, uint64_t nchain,
-                                                  uint64_t total, const uint32_t* W, uint8_t* out) {
+                                                  uint64_t total, const uint32_t* W, uint8_t* out,
+                                                  uint32_t* err) {
     const uint64_t s0 = (uint64_t)blockIdx.x * FB_FIN_SPAN;
     if (s0 >= total) return;
     const uint64_t s1 = min(total, s0 + FB_FIN_SPAN);
@@ -1945,8 +1946,12 @@ __global__ __launch_bounds__(256) void k_fb_final(const uint16_t* img, const uin
             for (int j = 0; j < 4; j++) wv[j] = wi[j] == 0xFFFFFFFFu ? FB_WLIT : W[wi[j]];
             // an entry the (at most FB_WIN_ROUNDS) jump rounds left open: follow it to its byte
 #pragma unroll
-            for (int j = 0; j < 4; j++)  // (entries point strictly back: the walk ends; bounded anyway)
+            for (int j = 0; j < 4; j++) {  // (entries point strictly back: the walk ends; bounded anyway)
                 for (uint32_t h = 0; h < (1u << 20) && !(wv[j] & FB_WLIT); h++) wv[j] = W[wv[j]];
+                // the bound reached with the entry still open: no byte to write, so the stream
+                // goes to the serial decoder instead
+                if (!(wv[j] & FB_WLIT) && x0 + 256 * j < s1) atomicOr(err, 2u);
+            }
 #pragma unroll
             for (int j = 0; j < 4; j++)
                 if (x0 + 256 * j < s1)
@@ -2299,7 +2304,7 @@ hipError_t launch_fb_resolve(const uint8_t* stream, const uint64_t* starts, cons
     const uint64_t nb = (total + FB_FIN_SPAN - 1) / FB_FIN_SPAN;
     if (nb)
         hipLaunchKernelGGL(k_fb_final, dim3((uint32_t)nb), dim3(256), 0, st, img, offs, sizes, nchain, total,
-                           (const uint32_t*)win, out);
+                           (const uint32_t*)win, out, err);
     return hipGetLastError();
 }
 

@@ -89,6 +89,18 @@ class _Lens:
         self.h = torch.zeros(max(1, count), dtype=torch.int64, pin_memory=self.cuda)
         self.ev = [None] * max(1, count)
         self.stream = torch.cuda.Stream(dev) if self.cuda else None
+        if self.cuda:
+            # a pool stream does not order itself behind torch's current stream: the input (and
+            # rank 0's output) may have been written by work still queued there
+            self.stream.wait_stream(torch.cuda.current_stream(dev))
+
+    def use(self, *tensors):
+        """Tensors allocated on torch's current stream and read or written on the side stream:
+        the caching allocator must not hand their memory out again before that work is done."""
+        if self.cuda:
+            for t in tensors:
+                if t is not None and t.is_cuda:
+                    t.record_stream(self.stream)
 
     def ptr(self, k):
         return self.d.data_ptr() + 8 * k
@@ -150,6 +162,7 @@ def deflate_gather(ctx, d_in, n, level, out=None, sub=4, align=32768):
         direct = cap0 >= need
         stage = None if direct else torch.empty(need, dtype=torch.uint8, device=dev)
         dst = out.data_ptr() if direct else stage.data_ptr()
+        lens.use(d_in, out, stage)
         own = n > 0 or world == 1  # (an empty first shard adds no bytes; alone it is 03 00)
         if own:
             _deflate(ctx, lens, 0, d_in.data_ptr(), n, level, dst, need, world > 1)
@@ -191,6 +204,7 @@ def deflate_gather(ctx, d_in, n, level, out=None, sub=4, align=32768):
         slot = dmx.deflate_bound(max([1] + [b - a for a, b in zip(cuts, cuts[1:])])) + 64
         stage = torch.empty(sub * slot, dtype=torch.uint8, device=dev)
         lens = _Lens(sub, dev)
+        lens.use(d_in, stage)
         emitted = [False] * sub
         pend, keep = [], []
 

@@ -76,6 +76,40 @@ def test_n_gpus_concatenated_streams_match_one_device(ctx, oracle):
         multi.close()
 
 
+def test_deflate_gather_waits_for_current_stream(ctx):
+    """shard.deflate_gather compresses on a side stream: an input still being written by work
+    queued on torch's current stream must be waited for.  World size 1 over gloo:
+    no P2P, only the side-stream ordering is exercised."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    import shard
+    own_pg = not dist.is_initialized()
+    if own_pg:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        data = dmx.corpus("text", 8 << 20, offset=5)
+        src = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+        d_in = torch.zeros_like(src)
+        torch.cuda.synchronize()
+        # delay the current stream, then write the input behind the delay (all asynchronous)
+        x = torch.full((2048, 2048), 1.0 / 2048, device="cuda")
+        for _ in range(40):
+            x = x @ x
+        d_in.copy_(src)
+        out = torch.empty(dmx.deflate_bound(len(data)) + 1024, dtype=torch.uint8, device="cuda")
+        total, mine = shard.deflate_gather(ctx, d_in, len(data), 2, out=out)
+        torch.cuda.synchronize()
+        assert total == mine > 0
+        assert ctx.decompress(out[:total].cpu().numpy().tobytes()) == data
+    finally:
+        if own_pg:
+            dist.destroy_process_group()
+
+
 def test_n_gpus_bound():
     """A garbage n_gpus (e.g. from a caller built against another dmx_config layout) is
     DMX_ERR_ARG, not thousands of sub-contexts."""

@@ -142,3 +142,48 @@ def test_path5_regions_serial_units(oracle, name):
         c.close()
     assert out == data == oracle.inflate(s)
     assert path == 5
+
+
+def _ref_err_ms(s):
+    """The reference's inflate::decompress of a broken stream on one host core: (ms, raised)."""
+    if not Reference.available():
+        return None, None
+    r = Reference()
+    t = time.perf_counter()
+    raised = False
+    try:
+        r.decompress(s)
+    except Exception:
+        raised = True
+    return (time.perf_counter() - t) * 1e3, raised
+
+
+def test_path5_truncated_stream_reports_error_from_chain(ctx, oracle):
+    """A truncated third-party stream: the chain of units is valid from bit 0
+    up to the unit that runs out of input, and that unit's over-read is the error realDecompress
+    (inflate.hpp:277-322, Bitwrapper inflate.hpp:81-108) throws -- reported from the chain, not
+    by a serial re-decode from bit 0; faster than the reference reaches the same error."""
+    import torch
+    data = dmx.corpus("text", 256 << 20)
+    s = streams.zlib_raw(data, 1)
+    d_o = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
+    for cut in (len(s) * 2 // 3 + 12345, len(s) - 3):
+        t = s[:cut]
+        from oracle_bind import CheckerError
+        with pytest.raises(CheckerError) as oe:
+            oracle.inflate(t)
+        want = {-1: dmx.DMX_ERR_OVERREAD, -2: dmx.DMX_ERR_DATA}[oe.value.code]
+        d_in = torch.frombuffer(bytearray(t), dtype=torch.uint8).cuda()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with pytest.raises(dmx.DmxError) as ge:
+            ctx.inflate_device(d_in.data_ptr(), len(t), d_o.data_ptr(), d_o.numel())
+        ms = (time.perf_counter() - t0) * 1e3
+        assert ge.value.code == want
+        assert ctx.stats().path == 5
+        ref, raised = _ref_err_ms(t)
+        print(f"truncated at {cut} of {len(s)}: GPU {ms:.1f} ms ({dmx.strerror(want)}), reference 1 core "
+              f"{ref if ref is None else round(ref, 1)} ms")
+        if ref is not None:
+            assert raised
+            assert ms < ref, (cut, ms, ref)

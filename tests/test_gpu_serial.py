@@ -1,8 +1,10 @@
 """The serial decoder (k_inflate_serial), the safety net for every stream the parallel paths
 decline: forced with dev_inflate_pass (7 = the serial decoder alone), it must
 give the oracle's bytes -- realDecompress, /root/reference/include/inflate.hpp:277-322 -- and
-errors, at >= 30 MB/s on a 16 MiB stream (the reference inflates zlib streams
-at ~25-48 MB/s on one CPU core)."""
+errors.  Speed bar: faster than the reference's own inflate::decompress of
+the same stream on one core of the same host (the rule of test_gpu_path5_foreign.py), not a
+floor taken from the decoder's own measurements.  The two cases the one-wavefront decoder does
+not win yet are expected failures with the measured rates, not passes."""
 import time
 import zlib
 
@@ -34,25 +36,61 @@ def _run(c, s, n):
     return d_o[:olen].cpu().numpy().tobytes(), path, ms
 
 
-# MB/s floors of the forced serial decoder on 16 MiB (one MI355X, round 5: bmp Z_FIXED 35.7, mixed
-# zlib-6 29.5, text zlib-1 13.6, one literal-only fixed block 10.9; round 4: 2.7 MB/s on the last).
 # The decoder is one wavefront (the stream is one dependency chain): it decodes the token at 128
-# consecutive bit offsets at once and walks the true chain four tokens per scalar step.
-FLOOR = {("bmp", "zfixed"): 30, ("mixed", "zlib6"): 25, ("text", "zlib1"): 11, ("mixed", "single"): 9}
+# consecutive bit offsets at once and walks the true chain four tokens per scalar step.  Round 6 on
+# one MI355X against the reference on one core of the box's EPYC 9575F (16 MiB, MB/s GPU / ref):
+# mixed zlib-6 29.7 / 127, text zlib-1 13.8 / 76, one literal-only fixed block 10.8 / 26, bmp
+# Z_FIXED 35.9 / 84.  The one-wavefront decoder loses every case, so each is an expected failure
+# (non-strict: an XPASS shows the day it wins) instead of a floor that certifies it.  Streams the
+# parallel paths take never reach it; a truncated or corrupt stream now gets its error from the
+# block-parallel chain (test_gpu_path5_foreign.py), not from this decoder.
+SLOW = pytest.mark.xfail(reason="one-wavefront serial decoder below the reference's one-core rate "
+                                "(round 6: 2.3-5.5x slower on the EPYC 9575F)", strict=False)
+
+
+def _ref_ms(s):
+    """The reference's inflate::decompress of s on one host core (oracle/_ref), best of 2."""
+    from oracle_bind import Reference
+    if not Reference.available():
+        return None
+    r = Reference()
+    best = 1e30
+    for _ in range(2):
+        t = time.perf_counter()
+        r.decompress(s)
+        best = min(best, (time.perf_counter() - t) * 1e3)
+    return best
 
 
 @pytest.mark.parametrize("kind,shape", [("mixed", "zlib6"), ("text", "zlib1"), ("mixed", "single"),
                                         ("bmp", "zfixed")])
-def test_serial_16MiB(sctx, oracle, kind, shape):
+def test_serial_16MiB_bytes(sctx, oracle, kind, shape):
+    """Bit-exact against the oracle on the forced serial decoder (parity: always required)."""
     data = dmx.corpus(kind, 16 << 20)
-    s = {"zlib6": lambda: streams.zlib_raw(data, 6), "zlib1": lambda: streams.zlib_raw(data, 1),
-         "single": lambda: streams.single_fixed_block(data), "zfixed": lambda: streams.zfixed(data)}[shape]()
+    s = _STREAMS[shape](data)
     out, path, ms = _run(sctx, s, len(data))
     assert path == 2
     assert out == data == oracle.inflate(s)
+
+
+_STREAMS = {"zlib6": lambda d: streams.zlib_raw(d, 6), "zlib1": lambda d: streams.zlib_raw(d, 1),
+            "single": lambda d: streams.single_fixed_block(d), "zfixed": lambda d: streams.zfixed(d)}
+
+
+@SLOW
+@pytest.mark.parametrize("kind,shape", [("mixed", "zlib6"), ("text", "zlib1"), ("mixed", "single"),
+                                        ("bmp", "zfixed")])
+def test_serial_16MiB_speed(sctx, oracle, kind, shape):
+    data = dmx.corpus(kind, 16 << 20)
+    s = _STREAMS[shape](data)
+    out, path, ms = _run(sctx, s, len(data))
+    assert path == 2 and out == data
     mbps = len(data) / ms / 1e3
-    print(f"serial {kind} {shape}: stream {len(s)} B, {ms:.1f} ms = {mbps:.1f} MB/s")
-    assert mbps >= FLOOR[(kind, shape)], (kind, shape, mbps)
+    ref = _ref_ms(s)
+    print(f"serial {kind} {shape}: stream {len(s)} B, {ms:.1f} ms = {mbps:.1f} MB/s; reference 1 core "
+          f"{ref if ref is None else round(ref, 1)} ms")
+    if ref is not None:
+        assert ms < ref, (kind, shape, ms, ref)
 
 
 def test_serial_host_api_and_errors(sctx, oracle):
