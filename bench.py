@@ -25,6 +25,7 @@ Prints ONE JSON line on rank 0.  Besides the contract fields it carries, at N = 
                stream of it, bit-exact checked
   c5_level3    config C5: level 3 on the 1 GiB text corpus, ratio next to the reference L3's
                and zlib-6's
+  c4_64k       config C4's 64 KiB blocks: the mixed round trip with segment_bytes = 65536
   cpu_baseline the reference compiled from its headers (oracle/_ref), 1 core and `nproc`
                processes on disjoint slices, with the host CPU model
 """
@@ -319,7 +320,9 @@ def zlib_ratio(kind, level, nbytes=16 << 20, chunk=None):
     return round(len(d) / tot, 4)
 
 
-def corpus_record(run, kind, level, steps):
+def corpus_record(run, kind, level, steps, tag=None):
+    """tag: the key of this record's profiles and PMC traffic (default: the corpus)."""
+    tag = tag or kind
     run.load(kind, 0)
     run.step(level)
     ev, clen, olen, _, _ = run.step(level)
@@ -342,9 +345,27 @@ def corpus_record(run, kind, level, steps):
             "inflate_path": s["path"],
             "alg_bytes": s["alg"],
             "roofline_frac": {"deflate": round(s["frac_def"], 5), "inflate": round(s["frac_inf"], 5)},
-            "traffic": {"deflate": traffic_of(f"{kind}:{n}:{level}:", DEF_KERNELS),
-                        "inflate": traffic_of(f"{kind}:{n}:{level}:", inf_k)},
-            "profile": profile_path(f"kstats_{kind}_L{level}.csv")}
+            "traffic": {"deflate": traffic_of(f"{tag}:{n}:{level}:", DEF_KERNELS),
+                        "inflate": traffic_of(f"{tag}:{n}:{level}:", inf_k)},
+            "profile": profile_path(f"kstats_{tag}_L{level}.csv")}
+
+
+def c4_record(run, dev, level, steps):
+    """Config C4's block size: the mixed corpus as 64 KiB DEFLATE blocks (one
+    Huffman block per 64 KiB of input, its two 32 KiB halves matched independently), the same
+    round trip as the corpora records (whose mixed entry is at 32 KiB segments), on this GPU's
+    1 GiB shard; the 8-GPU gather of C4 is the N > 1 bench step."""
+    ctx64 = dmx.Context(device=dev.index or 0, segment_bytes=65536)
+    ctx64.set_timing(True)
+    saved = run.ctx
+    run.ctx = ctx64
+    try:
+        rec = corpus_record(run, "mixed", level, steps, tag="c4_64k")
+    finally:
+        run.ctx = saved
+        ctx64.close()
+    rec["segment_bytes"] = 65536
+    return rec
 
 
 def c3_record(torch, ctx, dev, stream):
@@ -540,6 +561,7 @@ def main():
         res["c5_level3"].update({"ref_ratio_L3_1MiB": REF_RATIO_L3_TEXT, "zlib6_ratio_16MiB": zlib_ratio("text", 6),
                                  "zlib6_ratio_32KiB_chunks_16MiB": zlib_ratio("text", 6, chunk=32768)})
         res["c3_inflate"] = c3_record(torch, ctx, dev, stream)
+        res["c4_64k"] = c4_record(run, dev, a.level, 3)
     if rank == 0:
         if world == 1 and not a.no_cpu_baseline:
             try:

@@ -96,10 +96,8 @@ constexpr bool DF_SKIP = DMX_DF_SKIP != 0;
 #ifndef DMX_DF_HIST
 #define DMX_DF_HIST 0
 #endif
-// the emission kernel loads its token words two blocks ahead
-#ifndef DMX_EM_PREF
-#define DMX_EM_PREF 0
-#endif
+// (round 4's DMX_EM_PREF -- token words loaded two blocks ahead -- measured no gain, DESIGN
+// 4.1, and was removed in round 6 with the per-part token sources of 64 KiB blocks)
 // level 2: half-size parse chunks for segments without a run (see the parse walk)
 #ifndef DMX_DF_ADAPT
 #define DMX_DF_ADAPT 0
@@ -1472,32 +1470,27 @@ __device__ __forceinline__ void em_flush(uint32_t* stg, uint32_t* dst, uint32_t 
         if ((dbg) && lane_id() == 0) (dbg)[(seg) * kPhaseSlots + (slot)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
-template <int SEG, bool RAW>
-__device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
-    const int lane = lane_id();
-    EM_PHASE(A.dbg, seg, 4);
-    const uint64_t base = seg * (uint64_t)SEG;
-    const uint32_t nb = (uint32_t)min((uint64_t)SEG, A.n - base);
-    const bool is_final = (seg + 1 == A.nseg) && A.final_last;
-    uint32_t* const slot = reinterpret_cast<uint32_t*>(A.slots + seg * (uint64_t)A.slot_bytes);
-    // token source: level 1 reads the input's words (four literals each; the segment base is
-    // 4-aligned when the input is: SEG is a multiple of 4), levels 2-3 the front kernel's words
-    const uint8_t* const inb = A.in + base;
-    const uintptr_t mis = reinterpret_cast<uintptr_t>(inb) & 3;
-    const uint32_t* const inw = reinterpret_cast<const uint32_t*>(inb - mis);
-    const uint64_t in_words_end = (A.n - base + mis + 3) / 4;  // readable words from inw
-    auto raw_word = [&](uint32_t k) -> uint32_t {  // input bytes 4k .. 4k + 3 of the segment
-        const uint32_t x = 4 * k + (uint32_t)mis;
+// The token source of one front-kernel segment: the whole block, or one 32 KiB half of a
+// 64 KiB block (config C4's block size).  Level 1 reads the input's words (four
+// literals each; the part's base is 4-aligned when the input is: parts are multiples of 4),
+// levels 2-3 the front kernel's words; a part the front kernel found no match in is all
+// literals: its input's words too.
+struct EmSrc {
+    const uint32_t* inw;    // 4-aligned base at or below the part's first input byte
+    const uint32_t* tok;    // front-kernel words (raw: unused)
+    uint64_t in_words_end;  // readable words from inw
+    uint32_t mis;           // the part's first byte - inw
+    uint32_t nb;            // input bytes of the part
+    uint32_t ntok;          // token words (raw: input words)
+    bool raw;
+    __device__ uint32_t raw_word(uint32_t k) const {  // input bytes 4k .. 4k + 3 of the part
+        const uint32_t x = 4 * k + mis;
         const uint32_t a = inw[x >> 2];
         const uint32_t b = (x >> 2) + 1 < in_words_end ? inw[(x >> 2) + 1] : 0u;
         return mis ? __builtin_amdgcn_alignbyte(b, a, x & 3) : a;
-    };
-    // (a segment the front kernel found no match in is all literals: its input's words too)
-    const bool raw = RAW || A.ntok[seg] == EM_ALL_LITERALS;
-    const uint32_t ntok = raw ? (nb + 3) / 4 : A.ntok[seg];
-    const uint32_t* const tok = raw ? nullptr : A.tok + seg * (uint64_t)A.tok_stride;
-    auto load4 = [&](uint32_t blk, uint32_t (&v)[4]) {
-        const uint32_t i0 = blk * 256 + 4 * lane;
+    }
+    __device__ void load4(uint32_t blk, uint32_t (&v)[4]) const {
+        const uint32_t i0 = blk * 256 + 4 * lane_id();
 #pragma unroll
         for (int j = 0; j < 4; j++) v[j] = 0;
         if (raw) {
@@ -1512,20 +1505,58 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
             for (int j = 0; j < 4; j++)
                 if (i0 + j < ntok) v[j] = tok[i0 + j];
         }
-    };
-    auto count_of = [&](uint32_t v, uint32_t idx) -> uint32_t {  // literals in the word
+    }
+    __device__ uint32_t count_of(uint32_t v, uint32_t idx) const {  // literals in the word
         if (raw) return min(4u, nb - 4 * idx);
         return (v >> 31) ? 0u : (v >> 24) & 3u;
-    };
-    const uint32_t nblk = (ntok + 255) / 256;
-    const uint64_t stored_bytes = 5ull + nb + (is_final ? 0 : 5);
+    }
+};
+template <bool RAW>
+__device__ EmSrc em_src(const DeflateArgs& A, uint64_t fseg, uint64_t base, uint32_t nb) {
+    EmSrc s;
+    const uint8_t* const inb = A.in + base;
+    s.mis = (uint32_t)(reinterpret_cast<uintptr_t>(inb) & 3);
+    s.inw = reinterpret_cast<const uint32_t*>(inb - s.mis);
+    s.in_words_end = (A.n - base + s.mis + 3) / 4;
+    s.nb = nb;
+    s.raw = RAW || A.ntok[fseg] == EM_ALL_LITERALS;
+    s.ntok = s.raw ? (nb + 3) / 4 : A.ntok[fseg];
+    s.tok = s.raw ? nullptr : A.tok + fseg * (uint64_t)A.tok_stride;
+    return s;
+}
+
+// stored-block header byte q (0..4): [BFINAL|00] LEN NLEN (deflate.hpp:387-399, padded on the
+// global bit position: every stored block here starts byte-aligned)
+__device__ __forceinline__ uint32_t em_stored_hdr(uint32_t q, bool fin, uint32_t len) {
+    return q == 0 ? (fin ? 1u : 0u) : q == 1 ? len & 0xFFu : q == 2 ? (len >> 8) & 0xFFu
+         : q == 3 ? ~len & 0xFFu : (~len >> 8) & 0xFFu;
+}
+
+// One block of SEG input bytes.  SEG = 65536 (C4's 64 KiB blocks): the front kernel matched the
+// two 32 KiB halves as independent segments (its LDS holds one 32 KiB image; the halves are
+// front segments 2s and 2s + 1), and this wave codes both halves' token words as ONE block --
+// one histogram, one code, one header -- so the block is a 64 KiB DEFLATE block whose second
+// half simply never refers into the first (valid: a reference may, but need not, reach back).
+template <int SEG, bool RAW>
+__device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
+    constexpr uint32_t NH = SEG > 32768 ? 2u : 1u;  // front segments per block
+    constexpr uint32_t HB = (uint32_t)SEG / NH;
+    const int lane = lane_id();
+    EM_PHASE(A.dbg, seg, 4);
+    const uint64_t base = seg * (uint64_t)SEG;
+    const uint32_t nb = (uint32_t)min((uint64_t)SEG, A.n - base);
+    const uint32_t np = (nb + HB - 1) / HB;  // parts of this block (the last block may be short)
+    const bool is_final = (seg + 1 == A.nseg) && A.final_last;
+    uint32_t* const slot = reinterpret_cast<uint32_t*>(A.slots + seg * (uint64_t)A.slot_bytes);
+    auto part = [&](uint32_t h) { return em_src<RAW>(A, seg * NH + h, base + (uint64_t)h * HB, min(HB, nb - h * HB)); };
+    // a stored form longer than 65535 bytes (LEN is 16 bits) is two stored blocks of 32 KiB
+    const uint32_t nsto = nb > 65535u ? 2u : 1u;
+    const uint32_t n1 = nsto == 2 ? 32768u : nb;
+    const uint64_t stored_bytes = 5ull * nsto + nb + (is_final ? 0 : 5);
 
     if (A.level != 0) {
         // ---- histogram ------------------------------------------------------------------
-        // token words come two blocks ahead (each block's load is a full HBM latency, which the
-        // block's own work does not cover)
-        uint32_t va[4], vb[4];
-        if (DMX_DF_HIST && !RAW) {  // the front kernel's counts
+        if (DMX_DF_HIST && !RAW && NH == 1) {  // the front kernel's counts
             const uint32_t* const hs = A.tok + seg * (uint64_t)A.tok_stride + A.tok_stride - kDeflateHistWords;
             for (int i = lane; i < (int)kDeflateHistWords; i += 64) {
                 const uint32_t x = hs[i];
@@ -1533,36 +1564,30 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
                 W.freq[2 * i + 1] = x >> 16;
             }
         } else {
-        for (int i = lane; i < EM_SYM; i += 64) W.freq[i] = 0;
-        wave_sync();
-        if (DMX_EM_PREF) {
-            load4(0, va);
-            if (nblk > 1) load4(1, vb);
-        }
-        for (uint32_t blk = 0; blk < nblk; blk++) {
-            uint32_t v[4];
-            if (DMX_EM_PREF) {
+            for (int i = lane; i < EM_SYM; i += 64) W.freq[i] = 0;
+            wave_sync();
+            for (uint32_t h = 0; h < np; h++) {
+                const EmSrc S = part(h);
+                const uint32_t nblk = (S.ntok + 255) / 256;
+                for (uint32_t blk = 0; blk < nblk; blk++) {
+                    uint32_t v[4];
+                    S.load4(blk, v);
 #pragma unroll
-                for (int j = 0; j < 4; j++) v[j] = va[j], va[j] = vb[j];
-                if (blk + 2 < nblk) load4(blk + 2, vb);
-            } else {
-                load4(blk, v);
-            }
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t idx = blk * 256 + 4 * lane + j;
+                        if (idx >= S.ntok) continue;
+                        if (!S.raw && (v[j] >> 31)) {
+                            atomicAdd(&W.freq[len_sym(((v[j] >> 16) & 0xFFu) + 3)], 1u);
+                            atomicAdd(&W.freq[EM_LIT + dist_sym((v[j] & 0x7FFFu) + 1)], 1u);
+                        } else {
+                            const uint32_t cnt = S.count_of(v[j], idx);
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t idx = blk * 256 + 4 * lane + j;
-                if (idx >= ntok) continue;
-                if (!raw && (v[j] >> 31)) {
-                    atomicAdd(&W.freq[len_sym(((v[j] >> 16) & 0xFFu) + 3)], 1u);
-                    atomicAdd(&W.freq[EM_LIT + dist_sym((v[j] & 0x7FFFu) + 1)], 1u);
-                } else {
-                    const uint32_t cnt = count_of(v[j], idx);
-#pragma unroll
-                    for (uint32_t i = 0; i < 4u; i++)
-                        if (i < cnt) atomicAdd(&W.freq[(v[j] >> (8 * i)) & 0xFFu], 1u);
+                            for (uint32_t i = 0; i < 4u; i++)
+                                if (i < cnt) atomicAdd(&W.freq[(v[j] >> (8 * i)) & 0xFFu], 1u);
+                        }
+                    }
                 }
             }
-        }
         }
         wave_sync();
         if (lane == 0) atomicAdd(&W.freq[256], 1u);  // end-of-block
@@ -1570,7 +1595,6 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
         EM_PHASE(A.dbg, seg, 5);
         const EmCodes ec = em_build_codes(W);
         EM_PHASE(A.dbg, seg, 6);
-
         // ---- dynamic header: RLE runs over (len[0..nlit), len[288..288+ndist)) -------------
         const uint32_t nlit = ec.nlit, ndist = ec.ndist, nall = nlit + ndist;
         auto seqv = [&](uint32_t i) -> uint32_t { return i < nlit ? W.len[i] : W.len[EM_LIT + i - nlit]; };
@@ -1688,43 +1712,37 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
             // ---- tokens -------------------------------------------------------------------
             uint32_t cur = 3 + (use_dyn ? hdr_bits : 0u);  // bit position in the window
             uint32_t* dst = slot;                          // next HBM word of the slot
-            if (DMX_EM_PREF) {
-                load4(0, va);
-                if (nblk > 1) load4(1, vb);
-            }
-            for (uint32_t blk = 0; blk < nblk; blk++) {
-                uint32_t v[4], nbit[4];
-                uint64_t pat[4];
-                if (DMX_EM_PREF) {
+            for (uint32_t h = 0; h < np; h++) {
+                const EmSrc S = part(h);
+                const uint32_t nblk = (S.ntok + 255) / 256;
+                for (uint32_t blk = 0; blk < nblk; blk++) {
+                    uint32_t v[4], nbit[4];
+                    uint64_t pat[4];
+                    S.load4(blk, v);
+                    uint32_t mine = 0;
 #pragma unroll
-                    for (int j = 0; j < 4; j++) v[j] = va[j], va[j] = vb[j];
-                    if (blk + 2 < nblk) load4(blk + 2, vb);
-                } else {
-                    load4(blk, v);
-                }
-                uint32_t mine = 0;
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t idx = blk * 256 + 4 * lane + j;
+                        nbit[j] = 0;
+                        pat[j] = 0;
+                        if (idx < S.ntok) pat[j] = em_pattern(W, v[j], S.count_of(v[j], idx), nbit[j], S.raw);
+                        mine += nbit[j];
+                    }
+                    const uint32_t inc = wave_incl_scan(mine);
+                    uint32_t pos = cur + inc - mine;
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const uint32_t idx = blk * 256 + 4 * lane + j;
-                    nbit[j] = 0;
-                    pat[j] = 0;
-                    if (idx < ntok) pat[j] = em_pattern(W, v[j], count_of(v[j], idx), nbit[j], raw);
-                    mine += nbit[j];
-                }
-                const uint32_t inc = wave_incl_scan(mine);
-                uint32_t pos = cur + inc - mine;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    em_put(W.stg, pos, pat[j], nbit[j]);
-                    pos += nbit[j];
-                }
-                cur += __shfl(inc, 63, 64);
-                wave_sync();
-                if (cur >= 32u * EM_FLUSH) {
-                    const uint32_t nw = cur >> 5;
-                    em_flush(W.stg, dst, nw);
-                    dst += nw;
-                    cur &= 31;
+                    for (int j = 0; j < 4; j++) {
+                        em_put(W.stg, pos, pat[j], nbit[j]);
+                        pos += nbit[j];
+                    }
+                    cur += __shfl(inc, 63, 64);
+                    wave_sync();
+                    if (cur >= 32u * EM_FLUSH) {
+                        const uint32_t nw = cur >> 5;
+                        em_flush(W.stg, dst, nw);
+                        dst += nw;
+                        cur &= 31;
+                    }
                 }
             }
             EM_PHASE(A.dbg, seg, 8);
@@ -1748,18 +1766,29 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
             return;
         }
     }
-    // ---- stored block: [BFINAL|00][LEN][NLEN][data] (+ the empty stored block) ------------
+    // ---- stored: [BFINAL|00][LEN][NLEN][data] (two such blocks above 65535 bytes), then the
+    // empty stored block unless final ------------------------------------------------------
     const uint32_t total = (uint32_t)stored_bytes;
+    const uint8_t* const inb = A.in + base;
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(inb) & 3);
+    const uint32_t* const inw = reinterpret_cast<const uint32_t*>(inb - mis);
+    const uint64_t in_words_end = (A.n - base + mis + 3) / 4;  // readable words from inw
+    const uint32_t d2 = 10 + n1;  // first output byte of the second block's data (nsto == 2)
     // 16 output bytes per lane and step, four steps in flight (the copy is latency-bound):
-    // output bytes [16 k, 16 k + 16) are input bytes [16 k - 5, 16 k + 11), five input words
-    // funnelled by the segment's constant misalignment; the first 16 bytes (header) and the
-    // tail go word by word
+    // output bytes [16 k, 16 k + 16) inside a block's data are input bytes shifted by that
+    // block's header bytes (5, or 10 in the second block), five input words funnelled by the
+    // segment's constant misalignment; headers and the tail go word by word
     const uint32_t n16 = (total + 15) / 16;
     uint4* const slot4 = reinterpret_cast<uint4*>(slot);
+    auto data_shift = [&](uint32_t a, uint32_t b) -> uint32_t {  // output bytes [a, b) all data: the shift
+        if (a >= 5 && b <= 5 + n1) return 5u;
+        if (nsto == 2 && a >= d2 && b <= 10 + nb) return 10u;
+        return 0u;
+    };
     auto word_at = [&](uint32_t k) -> uint32_t {  // output word k = bytes 4k .. 4k + 3
         uint32_t w = 0;
-        if (k >= 2 && 4 * k + 3 < 5 + nb) {
-            const uint32_t x = 4 * k - 5 + (uint32_t)mis;  // aligned-base byte of the first
+        if (const uint32_t sh = data_shift(4 * k, 4 * k + 4)) {
+            const uint32_t x = 4 * k - sh + mis;  // aligned-base byte of the first
             const uint32_t a = inw[x >> 2];
             const uint32_t b = (x >> 2) + 1 < in_words_end ? inw[(x >> 2) + 1] : 0u;
             w = __builtin_amdgcn_alignbyte(b, a, x & 3);
@@ -1768,13 +1797,11 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
             for (int j = 0; j < 4; j++) {
                 const uint32_t pos = 4 * k + j;
                 uint32_t byte;
-                if (pos == 0) byte = is_final ? 1u : 0u;
-                else if (pos == 1) byte = nb & 0xFFu;
-                else if (pos == 2) byte = (nb >> 8) & 0xFFu;
-                else if (pos == 3) byte = ~nb & 0xFFu;
-                else if (pos == 4) byte = (~nb >> 8) & 0xFFu;
-                else if (pos < 5 + nb) byte = inb[pos - 5];
-                else byte = (!is_final && pos >= 5 + nb + 3 && pos < total) ? 0xFFu : 0u;
+                if (pos < 5) byte = em_stored_hdr(pos, is_final && nsto == 1, n1);
+                else if (pos < 5 + n1) byte = inb[pos - 5];
+                else if (nsto == 2 && pos < d2) byte = em_stored_hdr(pos - 5 - n1, is_final, nb - n1);
+                else if (nsto == 2 && pos < 10 + nb) byte = inb[pos - 10];
+                else byte = (!is_final && pos >= 5 * nsto + nb + 3 && pos < total) ? 0xFFu : 0u;
                 w |= byte << (8 * j);
             }
         }
@@ -1783,14 +1810,14 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
 #pragma unroll 4
     for (uint32_t k4 = lane; k4 < n16; k4 += 64) {
         uint4 o;
-        if (k4 >= 1 && 16 * k4 + 15 < 5 + nb) {
-            const uint32_t x = 16 * k4 - 5 + (uint32_t)mis, i0 = x >> 2, sh = x & 3;
+        if (const uint32_t sh = data_shift(16 * k4, 16 * k4 + 16)) {
+            const uint32_t x = 16 * k4 - sh + mis, i0 = x >> 2, s = x & 3;
             const uint32_t a0 = inw[i0], a1 = inw[i0 + 1], a2 = inw[i0 + 2], a3 = inw[i0 + 3];
             const uint32_t a4 = i0 + 4 < in_words_end ? inw[i0 + 4] : 0u;
-            o.x = __builtin_amdgcn_alignbyte(a1, a0, sh);
-            o.y = __builtin_amdgcn_alignbyte(a2, a1, sh);
-            o.z = __builtin_amdgcn_alignbyte(a3, a2, sh);
-            o.w = __builtin_amdgcn_alignbyte(a4, a3, sh);
+            o.x = __builtin_amdgcn_alignbyte(a1, a0, s);
+            o.y = __builtin_amdgcn_alignbyte(a2, a1, s);
+            o.z = __builtin_amdgcn_alignbyte(a3, a2, s);
+            o.w = __builtin_amdgcn_alignbyte(a4, a3, s);
         } else {
             o.x = word_at(4 * k4);
             o.y = word_at(4 * k4 + 1);
@@ -1948,7 +1975,7 @@ hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t 
     int dev = 0, ncu = 0, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (seg_bytes == 32768)
+    if (seg_bytes >= 32768)
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_deflate_segments<32768, false>, DF_NT, 0);
     else
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_deflate_segments16<false>, DF_NT, 0);
@@ -1957,7 +1984,14 @@ hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t 
     if (ev_main0) (void)hipEventRecord(ev_main0, st);
     if (grid && A.level >= 2) {  // match finding + parse -> token words (levels 0-1 have none)
         const bool l3 = A.level >= 3;
-        if (seg_bytes == 32768) {
+        if (seg_bytes == 65536) {  // 64 KiB blocks: the front kernel matches their 32 KiB halves
+            DeflateArgs H = A;
+            H.nseg = (A.n + 32767) / 32768;
+            H.dbg = nullptr;
+            const uint32_t hg = (uint32_t)std::min<uint64_t>(H.nseg, fit);
+            if (l3) hipLaunchKernelGGL((k_deflate_segments<32768, true>), dim3(hg), dim3(DF_NT), 0, st, H);
+            else hipLaunchKernelGGL((k_deflate_segments<32768, false>), dim3(hg), dim3(DF_NT), 0, st, H);
+        } else if (seg_bytes == 32768) {
             if (l3) hipLaunchKernelGGL((k_deflate_segments<32768, true>), dim3(grid), dim3(DF_NT), 0, st, A);
             else hipLaunchKernelGGL((k_deflate_segments<32768, false>), dim3(grid), dim3(DF_NT), 0, st, A);
         } else {
@@ -1968,7 +2002,10 @@ hipError_t launch_deflate(const DeflateArgs& A, uint32_t seg_bytes, hipStream_t 
     if (A.nseg) {  // entropy coding and bit packing, one wavefront per segment
         const uint32_t eg = (uint32_t)((A.nseg + EM_NW - 1) / EM_NW);
         const bool raw = A.level < 2;
-        if (seg_bytes == 32768) {
+        if (seg_bytes == 65536) {
+            if (raw) hipLaunchKernelGGL((k_deflate_emit<65536, true>), dim3(eg), dim3(64 * EM_NW), 0, st, A);
+            else hipLaunchKernelGGL((k_deflate_emit<65536, false>), dim3(eg), dim3(64 * EM_NW), 0, st, A);
+        } else if (seg_bytes == 32768) {
             if (raw) hipLaunchKernelGGL((k_deflate_emit<32768, true>), dim3(eg), dim3(64 * EM_NW), 0, st, A);
             else hipLaunchKernelGGL((k_deflate_emit<32768, false>), dim3(eg), dim3(64 * EM_NW), 0, st, A);
         } else {

@@ -83,6 +83,7 @@ struct dmx_ctx {
     uint8_t* pin = nullptr;
     size_t pin_cap = 0, pin_off = 0;
     DevBuf fbreg, fbJ, fbvis;  // fixed-code regions: {E, T, first super block} + super-block regions, jumps, visits
+    DevBuf fbJraw, fbJsub, fbcbit, fbucb;  // regions: chunk maps, sub-chunk entries, chunk entries, unit chunk
     DevBuf ck;  // checksum scratch (checksum.hip) + the 4-byte result at its start
     bool timing = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -409,6 +410,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     const uint64_t nbits = 8ull * n;
     std::vector<uint64_t> starts, vhdr;
     std::vector<uint8_t> strong, vmode;
+    std::vector<uint32_t> ucb;  // region units: the first global chunk of their super block
     starts.push_back(0);
     strong.push_back(1);
     for (uint64_t h : hits) {
@@ -463,14 +465,16 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     starts.resize(Kcap);
     vhdr.assign(Kcap, 0);
     vmode.assign(Kcap, FB_V_HEADER);
+    ucb.assign(Kcap, ~0u);
     stops.resize(Kcap);
     tokoff[0] = 0;
     for (uint64_t k = 0; k < K; k++) tokoff[k + 1] = tokoff[k] + words_of(starts[k], stops[k]);
     const uint64_t rep_words = std::min<uint64_t>(tokoff[K] + 2 * reg_budget + 4096 * R, 1ull << 29);
     if (!c->fbs.ensure(Kcap * 8) || !c->fbt.ensure((Kcap + 1) * 8) || !c->fbk.ensure((tokoff[K] + rep_words) * 4) ||
         !c->fbu.ensure(Kcap * sizeof(FbUnit)) || !c->fbstop.ensure(Kcap * 8) || !c->fbvm.ensure(Kcap) ||
-        !c->fbvh.ensure(Kcap * 8))
+        !c->fbvh.ensure(Kcap * 8) || !c->fbucb.ensure(Kcap * 4))
         return DMX_OK;
+    const uint64_t* dcbit = nullptr;  // set once the regions' chunk entries exist
     auto upload = [&](uint64_t k0, uint64_t cnt) -> int {  // (each batch follows a stream sync)
         c->pin_off = 0;
         HIPCHK(pin_h2d(c, c->fbs.as<uint64_t>() + k0, &starts[k0], cnt * 8, st));
@@ -478,6 +482,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         HIPCHK(pin_h2d(c, c->fbt.as<uint64_t>() + k0, &tokoff[k0], (cnt + 1) * 8, st));
         HIPCHK(pin_h2d(c, c->fbvm.as<uint8_t>() + k0, &vmode[k0], cnt, st));
         HIPCHK(pin_h2d(c, c->fbvh.as<uint64_t>() + k0, &vhdr[k0], cnt * 8, st));
+        HIPCHK(pin_h2d(c, c->fbucb.as<uint32_t>() + k0, &ucb[k0], cnt * 4, st));
         return DMX_OK;
     };
     hmark(2);
@@ -494,7 +499,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         HIPCHK(launch_fb_decode(words, misalign, n, c->fbs.as<uint64_t>(), c->fbstop.as<uint64_t>(),
                                 c->fbvm.as<uint8_t>(), c->fbvh.as<uint64_t>(), K, u0, cnt, c->fbt.as<uint64_t>(),
                                 c->fbk.as<uint32_t>(), c->fbu.as<FbUnit>(), c->flags | iflags, !fb_serial_only(c),
-                                dstats, st));
+                                dstats, dcbit, dcbit ? c->fbucb.as<uint32_t>() : nullptr, st));
         HIPCHK(hipMemcpyAsync(&units[u0], c->fbu.as<FbUnit>() + u0, cnt * sizeof(FbUnit), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         return DMX_OK;
@@ -553,7 +558,9 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         if (!regs.empty()) {
             const uint64_t nreg = regs.size();
             if (!c->fbreg.ensure(nreg * 24 + nsb * 4) || !c->fbJ.ensure(nsb * (uint64_t)fb_region_nodes() * 4) ||
-                !c->fbvis.ensure((nsb + nreg) * 4))
+                !c->fbvis.ensure((nsb + nreg) * 4) || !c->fbJraw.ensure(nsb * (uint64_t)fb_region_nodes() * 4) ||
+                !c->fbJsub.ensure(nsb * (uint64_t)fb_region_nodes() * 8) ||
+                !c->fbcbit.ensure(nsb * (uint64_t)fb_region_entries() * 8))
                 return DMX_OK;
             std::vector<uint64_t> hreg(3 * nreg);
             std::vector<uint32_t> sbreg(nsb);
@@ -569,7 +576,9 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
             HIPCHK(hipMemcpyAsync(dreg, hreg.data(), nreg * 24, hipMemcpyHostToDevice, st));
             HIPCHK(hipMemcpyAsync(dsbr, sbreg.data(), nsb * 4, hipMemcpyHostToDevice, st));
             HIPCHK(launch_fb_regions(words, misalign, n, dreg, (uint32_t)nreg, dsbr, nsb, c->fbJ.as<uint32_t>(), dvis,
-                                     dvis + nsb, st));
+                                     dvis + nsb, c->fbJraw.as<uint32_t>(), c->fbJsub.as<uint64_t>(),
+                                     c->fbcbit.as<uint64_t>(), st));
+            dcbit = c->fbcbit.as<uint64_t>();
             std::vector<uint32_t> vis(nsb + nreg);
             HIPCHK(hipMemcpyAsync(vis.data(), dvis, (nsb + nreg) * 4, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
@@ -592,6 +601,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
                     starts[Ku] = regs[r].E + (uint64_t)(v >> 6) * ch + (v & 31u);
                     vmode[Ku] = head ? FB_V_HEADER : FB_V_EXACT;
                     vhdr[Ku] = head ? 0 : (FB_STATE_FIXED | ((v >> 5) & 1u ? FB_STATE_FINAL : 0ull));
+                    ucb[Ku] = (uint32_t)((regs[r].sb0 + j) * 64);  // its super block's first chunk
                     Ku++;
                 }
                 for (uint64_t k = first; k < Ku; k++) {

@@ -194,14 +194,20 @@ constexpr uint32_t FB_REGION_END = 0x80000001u, FB_REGION_LINK = 0x80000002u;
 uint64_t fb_region_super_bits();
 uint64_t fb_region_chunk_bits();
 uint32_t fb_region_nodes();
+// Jraw (nsb * fb_region_nodes() words): the chunk maps before pointer jumping; cbit: the stream
+// bit where the true path enters each chunk and sub-chunk (~0: not entered), k_fb_schunks
 hipError_t launch_fb_regions(const uint32_t* in_words, uint64_t misalign, uint64_t n, const uint64_t* reg,
                              uint32_t nreg, const uint32_t* sbreg, uint64_t nsb, uint32_t* J, uint32_t* visit,
-                             uint32_t* rstat, hipStream_t st);
+                             uint32_t* rstat, uint32_t* Jraw, uint64_t* Jsub, uint64_t* cbit, hipStream_t st);
+// (Jsub: nsb * fb_region_nodes() 64-bit words; cbit: nsb * fb_region_entries() words)
+uint32_t fb_region_entries();
 hipError_t launch_fb_decode(const uint32_t* in_words, uint64_t misalign, uint64_t n,
                             const uint64_t* starts, const uint64_t* stops, const uint8_t* vmode,
                             const uint64_t* vhdr, uint64_t nunits, uint64_t u0, uint64_t count,
                             const uint64_t* tokoff, uint32_t* tok, FbUnit* units, uint32_t flags,
-                            bool parallel, uint32_t* stats, hipStream_t st);
+                            bool parallel, uint32_t* stats, const uint64_t* cbit, const uint32_t* ucb,
+                            hipStream_t st);
+// (cbit / ucb: the region units' exact chunk entries, see FbDecodeArgs; nullptr when none)
 // replay + window hand-off + final resolve; *err (zeroed by the caller) becomes nonzero when a
 // copy reaches before the stream start.  win (fb_window_entries(nchain) words, 0 = not
 // available) and open (fb_window_rounds(nchain) words): the parallel hand-off; win == nullptr:

@@ -635,6 +635,11 @@ struct FbDecodeArgs {
     uint32_t flags;
     uint32_t* stats;  // optional (DMX_FB_DEBUG): units decoded lane-parallel, serially from the
                       // start, serially after a parallel first block, weak units
+    // fixed-code regions (k_fb_schunks): cbit[g] = the stream bit where the true token path
+    // enters global region chunk g (~0: not entered); ucb[u] = the first global chunk of unit u's
+    // super block, ~0 for a unit that is not a region unit (or nullptr: none)
+    const uint64_t* cbit;
+    const uint32_t* ucb;
 };
 
 // A fixed block that follows inside a unit is decoded serially only when it lies within this
@@ -835,6 +840,11 @@ constexpr uint32_t FBP_WARM = DMX_FBP_WARM;  // warm-up bits before a range
 constexpr uint32_t TK_NOP = 4;         // a fixed block's end of block + the next fixed header
 constexpr int FBP_ROUNDS = 1024;  // a settle cascade (data that re-synchronises slowly) still
                                    // beats the serial decoder by far
+// exact range starts of a region unit: the entries of its super block's 64 chunks x 8
+// sub-chunks of 512 bits (k_fb_schunks, below)
+constexpr uint32_t FBS_SUBS = 8;
+constexpr uint32_t FBS_XS = 64 * FBS_SUBS;
+static_assert(FBS_XS <= (uint32_t)FBP_NT, "one candidate start per thread");
 struct FbpSmem {
     uint32_t in[FBP_IN + 8];  // stream words [ws, ws + nst), zero after; fb_serial's ring later
     uint32_t bmap[FBP_IN];    // token starts of the first pass (bit p = body bit p)
@@ -845,6 +855,8 @@ struct FbpSmem {
     uint32_t wcnt[FBP_NT];    // words of range r, then its exclusive word offset
     uint32_t bcnt[FBP_NT];    // output bytes of range r, then its exclusive byte offset
     uint32_t part[2][FBP_NT / 64];
+    uint32_t xs[FBS_XS + 1];  // exact range starts (region units: the chunk entries), body bits
+    uint32_t nx;              // their count (0: ranges split evenly, warm-up + settle)
     uint32_t te2[2];
     uint32_t kind;            // 0 parallel, 1 serial from the unit start, 2 serial continuation,
                               // 3 an error the serial decoder would report (S.err), 4 again
@@ -1037,17 +1049,45 @@ __global__ __launch_bounds__(FBP_NT) void k_fb_pdecode(FbDecodeArgs A) {
         dbg_attempts++;
         const uint32_t* win = S.in;
         const uint32_t hs = S.hs, hlen = (uint32_t)(base + S.he - S.ws * 32 - hs);
-        const uint32_t nl = max(1u, min((uint32_t)FBP_NT, hlen / FBP_MINBITS));
+        // A region unit's chunks each have a known entry on the true token path (k_fb_schunks):
+        // its ranges start exactly there, with no warm-up, and settle at once.  (Evenly split
+        // ranges inside a fixed-code run need not re-synchronise -- literal runs of one code
+        // length stay misaligned -- and settled one range per round: 3.7 ms per 32 KB unit.)
+        {
+            constexpr uint32_t NX = FBS_XS;  // entries per super block (chunks x sub-chunks)
+            const uint64_t body = S.ws * 32 + hs - base;  // stream bit of the body's first token
+            const uint32_t cb = A.ucb ? A.ucb[u] : ~0u;
+            const uint64_t x = (cb != ~0u && (uint32_t)t < NX) ? A.cbit[(uint64_t)cb * FBS_SUBS + t] : ~0ull;
+            const bool v = x != ~0ull && x > body && x - body < hlen;
+            const uint64_t m = __ballot(v);
+            if ((t & 63) == 0) S.part[0][wave] = (uint32_t)__popcll(m);
+            __syncthreads();
+            uint32_t before = 0, tot = 0;
+#pragma unroll
+            for (int w = 0; w < NW; w++) {
+                const uint32_t c = S.part[0][w];
+                before += w < wave ? c : 0u;
+                tot += c;
+            }
+            if (v) S.xs[1 + before + __popcll(m & ((1ull << (t & 63)) - 1ull))] = (uint32_t)(x - body);
+            if (t == 0) {
+                S.xs[0] = 0;
+                S.nx = cb != ~0u ? 1u + tot : 0u;
+            }
+        }
+        __syncthreads();
+        const uint32_t nx = S.nx;
+        const uint32_t nl = nx ? nx : max(1u, min((uint32_t)FBP_NT, hlen / FBP_MINBITS));
         const uint32_t r = (uint32_t)((t & 63) * NW + wave);
-        const uint32_t sp = r < nl ? (uint32_t)(((uint64_t)hlen * r) / nl) : hlen;
-        const uint32_t sp1 = r + 1 < nl ? (uint32_t)(((uint64_t)hlen * (r + 1)) / nl) : hlen;
+        const uint32_t sp = r < nl ? (nx ? S.xs[r] : (uint32_t)(((uint64_t)hlen * r) / nl)) : hlen;
+        const uint32_t sp1 = r + 1 < nl ? (nx ? S.xs[r + 1] : (uint32_t)(((uint64_t)hlen * (r + 1)) / nl)) : hlen;
         const uint32_t cw = hlen / 32 + 2;
         for (uint32_t i = t; i < cw; i += FBP_NT) S.bmap[i] = 0;
         if (t < 2) S.te2[t] = FBP_NT;
         __syncthreads();
         // ---- 2. warm-up, first pass ----
         uint32_t s0 = sp;
-        if (r > 0 && r < nl) {
+        if (r > 0 && r < nl && !nx) {
             int32_t p = (int32_t)sp - (int32_t)FBP_WARM;
             if (p < 0) p = 0;
             uint32_t pa = (uint32_t)((int32_t)hs + p);
@@ -2016,7 +2056,12 @@ constexpr uint32_t FBS_CH = 4096;             // bits per chunk
 constexpr uint32_t FBS_K = 64;                // chunks per super block
 constexpr uint32_t FBS_SB = FBS_CH * FBS_K;   // 2^18 bits
 constexpr uint32_t FBS_NODES = FBS_K * 64;    // nodes per super block
-constexpr int FBS_NT = 256;
+constexpr uint32_t FBS_SUB = FBS_SUBS;        // sub-chunks per chunk whose entries a lane records
+constexpr uint32_t FBS_SUBB = FBS_CH / FBS_SUB;  // 512 bits
+constexpr uint64_t FBS_SUB_NONE = (1ull << (5 * (FBS_SUB - 1))) - 1;  // every sub-entry 31 = none
+// 512 threads (two chunks of 32 entries per wave, four tasks per thread): 52 KB of LDS leaves
+// three workgroups, i.e. 24 waves, per CU (256 threads: 12 -- the lanes are LDS-latency-bound)
+constexpr int FBS_NT = 512;
 constexpr uint32_t FBS_STG = FBS_SB / 32 + 128;  // staged words: one before the super block, 4 KiB bits after
 constexpr uint32_t FBS_TERM = 0x80000000u;
 constexpr uint32_t FBS_END = FB_REGION_END, FBS_LINK = FB_REGION_LINK, FBS_FAIL = FBS_TERM | 3u;
@@ -2040,6 +2085,11 @@ struct FbsBits {
         const uint64_t lim = end_bytes - 4 * i;
         return lim >= 4 ? v : v & ((1u << (8 * lim)) - 1u);
     }
+    // aligned-image word i: staged when the staging holds it (FBS_STG + 2 words from a0)
+    __device__ uint32_t wordx(uint64_t i) const {
+        const uint64_t j = i - (a0 >> 5);
+        return (i >= (a0 >> 5) && j < FBS_STG + 2) ? stg[j] : word(i);
+    }
     __device__ uint32_t peek(uint64_t p) const {
         const uint64_t a = base + p;
         const uint64_t rel = a - a0;
@@ -2054,23 +2104,48 @@ struct FbsBits {
 
 // One lane: the token path from stream bit p (hstate: p is the region head's block header)
 // to the first fixed-code token boundary at or past the next chunk (chunk grid from E).
-// *r0 / *r1: the result for entry f = 0 / f = 1.
+// *r0 / *r1: the result for entry f = 0 / f = 1.  The stream comes through a 64-bit register
+// window holding >= 32 valid bits before every token (a fixed-code token is <= 31 bits), so a
+// token costs one table read: literal or match by selects, the distance code from the same
+// window.  (Round 5 re-read the stream per token, 2 + 2 LDS reads and 64-bit address math.)
 __device__ void fbs_lane(const FbsBits& B, const uint32_t* lut, uint64_t p, bool hstate, uint64_t E,
-                         uint64_t T, uint64_t nbits, uint32_t* r0, uint32_t* r1) {
+                         uint64_t T, uint64_t nbits, uint32_t* r0, uint32_t* r1, uint64_t* subs) {
     uint64_t target = p - ((p - E) % FBS_CH) + FBS_CH;
+    // sub-chunk entries: the first token boundary at or past each FBS_SUBB-bit mark of the chunk
+    // (5 bits each: a token is <= 31 bits, so it is < 31 bits past the mark; 31 = not recorded)
+    uint64_t sub_at = target - FBS_CH + FBS_SUBB, sb = FBS_SUB_NONE;
+    uint32_t sk = 0;
     bool eob_seen = false;  // an end of block met with f unknown: the f = 1 entry ended there
     bool hdr = hstate;      // a header is next
     uint32_t fcur = 0;      // BFINAL of the last header read (valid once one was read)
     bool hdr_read = false;
     uint32_t res = 0;
+    uint64_t w = 0, wi = 0;  // window: the bits from p on (nb valid), next word to load
+    uint32_t nb = 0;
+    auto seek = [&](uint64_t q) {
+        const uint64_t a = B.base + q;
+        wi = a >> 5;
+        const uint32_t sh = (uint32_t)(a & 31);
+        w = (((uint64_t)B.wordx(wi + 1) << 32) | B.wordx(wi)) >> sh;
+        nb = 64 - sh;
+        wi += 2;
+    };
+    seek(p);
     for (;;) {
+        if (nb < 32) {
+            w |= (uint64_t)B.wordx(wi) << nb;
+            nb += 32;
+            wi++;
+        }
         if (hdr) {
             // block headers up to the next fixed block (stored data skipped, BTYPE 3 empty)
             if (p >= T || p + 3 > nbits) { res = (p == T && T < nbits) ? FBS_LINK : FBS_FAIL; break; }
-            const uint32_t h = B.peek(p) & 7u;
+            const uint32_t h = (uint32_t)w & 7u;
             const uint32_t bfinal = h & 1u, btype = h >> 1;
             if (btype == 2) { res = FBS_FAIL; break; }  // a dynamic header before T: not scanned
             p += 3;
+            w >>= 3;
+            nb -= 3;
             hdr_read = true;
             if (btype == 1) {
                 fcur = bfinal;
@@ -2083,6 +2158,7 @@ __device__ void fbs_lane(const FbsBits& B, const uint32_t* lut, uint64_t p, bool
                 const uint32_t len = B.peek(p) & 0xFFFFu;  // NLEN unchecked (inflate.hpp:293-303)
                 p += 32 + 8ull * len;
                 if (p > nbits) { res = FBS_FAIL; break; }
+                seek(p);
             }
             if (bfinal) { res = FBS_END; break; }
             continue;
@@ -2099,21 +2175,29 @@ __device__ void fbs_lane(const FbsBits& B, const uint32_t* lut, uint64_t p, bool
             }
             target = E + (cc + 1) * FBS_CH;  // a stored block's data ended deep inside a chunk
         }
-        const uint32_t v = B.peek(p);
-        const uint32_t e = lut[v & 511u];
+        while (p >= sub_at && sk < FBS_SUB - 1) {
+            const uint64_t o = p - sub_at;
+            if (o < 31) sb = (sb & ~(31ull << (5 * sk))) | (o << (5 * sk));
+            sk++;
+            sub_at += FBS_SUBB;
+        }
+        const uint32_t e = lut[(uint32_t)w & 511u];
         const uint32_t cl = e & 15u, ty = (e >> 4) & 3u;
-        if (ty == 0) {
-            p += cl;
-        } else if (ty == 2) {
-            const uint32_t ex = (e >> 6) & 15u;
-            p += cl + ex;
-            const uint32_t ds = __builtin_bitreverse32(B.peek(p)) >> 27;  // 5-bit distance code
-            p += 5 + (ds < 30 ? dist_extra(ds) : 0u);
-        } else {  // end of block
+        if (ty == 1) {  // end of block
             p += 7;
+            w >>= 7;
+            nb -= 7;
             if (!hdr_read) eob_seen = true;
             else if (fcur) { res = FBS_END; break; }
             hdr = true;
+        } else {  // literal (ty 0) or length (ty 2) + distance, <= 31 bits of the window
+            const bool m = ty == 2;
+            const uint32_t n1 = cl + (m ? (e >> 6) & 15u : 0u);
+            const uint32_t ds = __builtin_bitreverse32((uint32_t)(w >> n1)) >> 27;  // 5-bit distance code
+            const uint32_t n = m ? n1 + 5 + (ds < 30 ? dist_extra(ds) : 0u) : cl;
+            p += n;
+            w >>= n;
+            nb -= n;
         }
         if (p > nbits) { res = FBS_FAIL; break; }
     }
@@ -2124,6 +2208,7 @@ __device__ void fbs_lane(const FbsBits& B, const uint32_t* lut, uint64_t p, bool
         *r0 = res;
         *r1 = eob_seen ? FBS_END : res;
     }
+    *subs = sb;
 }
 
 struct FbsArgs {
@@ -2135,6 +2220,10 @@ struct FbsArgs {
     uint32_t* visit;        // per super block: the node the path enters it at (~0: none)
     uint32_t* rstat;        // per region: the walk's terminal
     uint32_t nreg;
+    uint32_t* Jraw;         // FBS_NODES per super block: the chunk map before pointer jumping
+    uint64_t* Jsub;         // FBS_NODES per super block: each node's sub-chunk entries (5 bits each)
+    uint64_t* cbit;         // FBS_K * FBS_SUB per super block: the stream bit the path enters each
+                            // chunk and sub-chunk at (~0: not entered / not recorded)
 };
 
 __global__ __launch_bounds__(FBS_NT) void k_fb_smap(FbsArgs A) {
@@ -2166,16 +2255,23 @@ __global__ __launch_bounds__(FBS_NT) void k_fb_smap(FbsArgs A) {
         const uint64_t cc = lsb * FBS_K + lc;
         const uint64_t p = E + cc * FBS_CH + e;
         uint32_t r0 = FBS_FAIL, r1 = FBS_FAIL;
+        uint64_t sub = FBS_SUB_NONE;
         if (cc == 0) {
-            if (e == 0) fbs_lane(B, S.lut, p, true, E, T, nbits, &r0, &r1);
+            if (e == 0) fbs_lane(B, S.lut, p, true, E, T, nbits, &r0, &r1, &sub);
             r1 = FBS_FAIL;
         } else if (p < T) {
-            fbs_lane(B, S.lut, p, false, E, T, nbits, &r0, &r1);
+            fbs_lane(B, S.lut, p, false, E, T, nbits, &r0, &r1, &sub);
         }
         S.J[lc * 64 + e] = r0;
         S.J[lc * 64 + 32 + e] = r1;
+        uint64_t* const Js = A.Jsub + sb * FBS_NODES + lc * 64;  // (f only matters past an end of block)
+        Js[e] = sub;
+        Js[32 + e] = sub;
     }
     __syncthreads();
+    // the chunk map itself, for k_fb_schunks (every chunk's entry on the true path)
+    uint32_t* const Jr = A.Jraw + sb * FBS_NODES;
+    for (uint32_t i = t; i < FBS_NODES; i += FBS_NT) Jr[i] = S.J[i];
     // pointer jumping inside the super block: a path has at most one node per chunk
     const uint32_t lo = (uint32_t)(lsb * FBS_K);  // region chunk of local chunk 0
     for (int round = 0; round < 7; round++) {
@@ -2208,18 +2304,54 @@ __global__ __launch_bounds__(64) void k_fb_swalk(FbsArgs A) {
     }
 }
 
+// k_fb_schunks: one workgroup per super block follows the true path through its chunks from
+// the node it enters at (k_fb_swalk's visit), in the chunk map staged in LDS; cbit gets the
+// stream bit of every chunk's entry (~0 where the path does not enter), which k_fb_pdecode uses
+// as exact range starts of the region units.
+__global__ __launch_bounds__(64) void k_fb_schunks(FbsArgs A, uint64_t nsb) {
+    __shared__ uint32_t J[FBS_NODES];
+    const uint64_t sb = blockIdx.x;
+    if (sb >= nsb) return;
+    const uint32_t t = threadIdx.x;
+    const uint32_t* const Jr = A.Jraw + sb * FBS_NODES;
+    for (uint32_t i = t; i < FBS_NODES; i += 64) J[i] = Jr[i];
+    uint64_t* const cb = A.cbit + sb * FBS_K * FBS_SUB;
+    for (uint32_t i = t; i < FBS_K * FBS_SUB; i += 64) cb[i] = ~0ull;
+    __syncthreads();
+    if (t != 0) return;
+    const uint32_t r = A.sbreg[sb];
+    const uint64_t E = A.reg[3 * r], lsb = sb - A.reg[3 * r + 2];
+    uint32_t v = A.visit[sb];
+    for (uint32_t k = 0; k < FBS_K && v != ~0u && !(v & FBS_TERM); k++) {
+        const uint32_t c = v >> 6;
+        if (c / FBS_K != lsb) break;  // the path left the super block
+        const uint32_t lc = c % FBS_K;
+        const uint64_t c0 = E + (uint64_t)c * FBS_CH;
+        cb[lc * FBS_SUB] = c0 + (v & 31u);
+        const uint64_t sub = A.Jsub[sb * FBS_NODES + lc * 64 + (v & 63u)];
+        for (uint32_t q = 1; q < FBS_SUB; q++) {
+            const uint32_t o = (uint32_t)(sub >> (5 * (q - 1))) & 31u;
+            if (o < 31) cb[lc * FBS_SUB + q] = c0 + q * FBS_SUBB + o;
+        }
+        v = J[lc * 64 + (v & 63u)];
+    }
+}
+static_assert(FBS_K * FBS_SUB == FBS_XS, "k_fb_pdecode's exact starts");
+
 uint64_t fb_region_super_bits() { return FBS_SB; }
+uint32_t fb_region_entries() { return FBS_K * FBS_SUB; }
 uint64_t fb_region_chunk_bits() { return FBS_CH; }
 uint32_t fb_region_nodes() { return FBS_NODES; }
 
 hipError_t launch_fb_regions(const uint32_t* in_words, uint64_t misalign, uint64_t n, const uint64_t* reg,
                              uint32_t nreg, const uint32_t* sbreg, uint64_t nsb, uint32_t* J, uint32_t* visit,
-                             uint32_t* rstat, hipStream_t st) {
+                             uint32_t* rstat, uint32_t* Jraw, uint64_t* Jsub, uint64_t* cbit, hipStream_t st) {
     if (!nreg || !nsb) return hipSuccess;
-    const FbsArgs A{in_words, misalign, n, reg, sbreg, J, visit, rstat, nreg};
+    const FbsArgs A{in_words, misalign, n, reg, sbreg, J, visit, rstat, nreg, Jraw, Jsub, cbit};
     (void)hipMemsetAsync(visit, 0xFF, nsb * 4, st);
     hipLaunchKernelGGL(k_fb_smap, dim3((uint32_t)nsb), dim3(FBS_NT), 0, st, A);
     hipLaunchKernelGGL(k_fb_swalk, dim3(nreg), dim3(64), 0, st, A);
+    hipLaunchKernelGGL(k_fb_schunks, dim3((uint32_t)nsb), dim3(64), 0, st, A, nsb);
     return hipGetLastError();
 }
 
@@ -2256,9 +2388,11 @@ hipError_t launch_fb_decode(const uint32_t* in_words, uint64_t misalign, uint64_
                             const uint64_t* starts, const uint64_t* stops, const uint8_t* vmode,
                             const uint64_t* vhdr, uint64_t nunits, uint64_t u0, uint64_t count,
                             const uint64_t* tokoff, uint32_t* tok, FbUnit* units, uint32_t flags,
-                            bool parallel, uint32_t* stats, hipStream_t st) {
+                            bool parallel, uint32_t* stats, const uint64_t* cbit, const uint32_t* ucb,
+                            hipStream_t st) {
     if (!count) return hipSuccess;
-    const FbDecodeArgs A{in_words, misalign, n, starts, stops, vmode, vhdr, nunits, u0, tokoff, tok, units, flags, stats};
+    const FbDecodeArgs A{in_words, misalign, n, starts, stops, vmode, vhdr, nunits, u0, tokoff, tok, units, flags, stats,
+                         cbit, ucb};
     if (parallel)
         hipLaunchKernelGGL(k_fb_pdecode, dim3((uint32_t)count), dim3(FBP_NT), 0, st, A);
     else

@@ -33,9 +33,10 @@ struct SegSink {
     uint32_t pos;
     bool stream_start;
     uint32_t err;
+    uint32_t cap = SEG_CAP;  // window bytes (the segment check takes 64 KiB segments)
     __device__ bool full() const { return false; }
     __device__ bool literal(uint32_t b) {
-        if (pos >= SEG_CAP) { err |= SEGF_OVERFLOW; return false; }
+        if (pos >= cap) { err |= SEGF_OVERFLOW; return false; }
         if (lane_id() == 0) win[pos] = (uint8_t)b;
         pos++;
         return true;
@@ -47,14 +48,14 @@ struct SegSink {
             err |= SEGF_XREF;
             return false;
         }
-        if (pos + L > SEG_CAP) { err |= SEGF_OVERFLOW; return false; }
+        if (pos + L > cap) { err |= SEGF_OVERFLOW; return false; }
         lz_copy_lds<0xFFFFFFFFu>(win, pos, L, dist);
         pos += L;
         return true;
     }
     template <class BR>
     __device__ bool stored(const BR& br, uint64_t b0, uint32_t len) {
-        if (pos + len > SEG_CAP) { err |= SEGF_OVERFLOW; return false; }
+        if (pos + len > cap) { err |= SEGF_OVERFLOW; return false; }
         for (uint32_t i = lane_id(); i < len; i += 64) win[pos + i] = br.byte_at(b0 + i);
         pos += len;
         return true;
@@ -1339,13 +1340,15 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_serial(InflateArgs A, int cou
 
 // ---------------------------------------------------------------------------------------
 // dmx_segment_check_device: for each given start, the one segment that begins there, decoded
-// by the exact wave decoder in piece mode (no reference before the start, <= 32 KiB of
-// output); ends[i] = the stream byte after its closing empty stored block (or after its BFINAL
-// block), ~0 when it does not decode.  Validates multi-GPU cut points (shard.py).
+// by the exact wave decoder in piece mode (no reference before the start, <= 64 KiB of
+// output: libdmx's 32 KiB segments and C4's 64 KiB blocks); ends[i] = the stream byte after its
+// closing empty stored block (or after its BFINAL block), ~0 when it does not decode.
+// Validates multi-GPU cut points (shard.py).
 // ---------------------------------------------------------------------------------------
+constexpr uint32_t CHECK_CAP = 65536;
 __global__ __launch_bounds__(IF_NT) void k_segment_check(InflateArgs A, const uint64_t* starts, uint64_t k,
                                                          uint64_t* ends) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[SEG_CAP + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t win[CHECK_CAP + 16];
     __shared__ Tables T;
     const uint64_t i = blockIdx.x;
     if (i >= k) return;
@@ -1354,7 +1357,7 @@ __global__ __launch_bounds__(IF_NT) void k_segment_check(InflateArgs A, const ui
     const uint64_t start = starts[i];
     uint64_t end = ~0ull;
     if (start < A.n) {
-        SegSink sk{win, 0, false, 0};
+        SegSink sk{win, 0, false, 0, CHECK_CAP};
         BitIn br;
         br.init(A.in_words, A.misalign, A.n);
         br.seek((A.misalign + start) * 8);

@@ -325,6 +325,7 @@ __device__ __forceinline__ bool ln_lane_pretab(uint8_t* T, uint64_t pl) {
     return true;
 }
 
+template <uint32_t CAP>
 __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[LN_LANES * (LN_REGION + LN_PRE_BYTES)];
     const uint32_t lane = threadIdx.x;
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             const uint32_t b0 = br.bitpos() >> 3;  // byte of the data (relative)
             if (!bfinal && len == 0 && nlen == 0xFFFF) {
                 end_byte = b0 + cb - off0;  // empty segment: the candidate is itself a marker
-            } else if (b0 + len > br.E || len > LN_OUT_CAP) {
+            } else if (b0 + len > br.E || len > CAP) {
                 flags |= SEGF_EXOTIC;
             } else {
                 push(len);
@@ -420,8 +421,34 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
                     br.align();
                     br.ensure(32);
                     const uint32_t l2 = br.bits(16), n2 = br.bits(16);
-                    if (f2 || t2 != 0 || l2 != 0 || n2 != 0xFFFF) flags |= SEGF_EXOTIC;
-                    end_byte = (br.bitpos() >> 3) + cb - off0;
+                    if (t2 == 0 && l2 != 0 && n2 == (~l2 & 0xFFFFu)) {
+                        // a second stored block: the stored form of a 64 KiB segment (LEN is 16
+                        // bits, so libdmx writes two blocks of 32 KiB), then BFINAL or the marker
+                        const uint32_t c2 = br.bitpos() >> 3;
+                        if (c2 + l2 > br.E || outpos + l2 > CAP) {
+                            flags |= SEGF_EXOTIC;
+                        } else {
+                            push(l2);
+                            push((uint32_t)(c2 + cb - off0 - start));
+                            outpos += l2;
+                            br.seek(c2 + l2);
+                            if (f2) {
+                                fin = true;
+                                end_byte = c2 + l2 + cb - off0;
+                            } else {
+                                br.ensure(3);
+                                const uint32_t f3 = br.bits(1), t3 = br.bits(2);
+                                br.align();
+                                br.ensure(32);
+                                const uint32_t l3 = br.bits(16), n3 = br.bits(16);
+                                if (f3 || t3 != 0 || l3 != 0 || n3 != 0xFFFF) flags |= SEGF_EXOTIC;
+                                end_byte = (br.bitpos() >> 3) + cb - off0;
+                            }
+                        }
+                    } else {
+                        if (f2 || t2 != 0 || l2 != 0 || n2 != 0xFFFF) flags |= SEGF_EXOTIC;
+                        end_byte = (br.bitpos() >> 3) + cb - off0;
+                    }
                 }
             }
         } else if (btype == 3) {
@@ -658,7 +685,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
 #if DMX_LN_PAIR
             const uint32_t sym2 = de & 511, cl2 = (de >> 11) & 15;
             const bool lit2 = !isl & (sym < 256) & ((de & 0x8000u) == 0u) & (sym2 < 256) &
-                              (outpos + 2 <= LN_OUT_CAP);
+                              (outpos + 2 <= CAP);
             const uint32_t c = n1 + (isl ? dcl + dx : (lit2 ? cl2 : 0u));  // 1 .. 33 bits
 #else
             const uint32_t c = n1 + (isl ? dcl + dx : 0u);  // 1 .. 33 bits
@@ -676,8 +703,8 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             const bool far = d > outpos;
             const uint32_t EXO = SEGF_EXOTIC;
             const uint32_t f_far = xref_fl | (((xref_fl == 0u) & (bp > E8)) ? EXO : 0u);
-            const uint32_t f_m = (ds >= 30) ? EXO : (far ? f_far : ((outpos + L > LN_OUT_CAP) ? EXO : 0u));
-            const uint32_t f_o = lit ? ((outpos >= LN_OUT_CAP) ? EXO : 0u) : ((sym != 256) ? EXO : 0u);
+            const uint32_t f_m = (ds >= 30) ? EXO : (far ? f_far : ((outpos + L > CAP) ? EXO : 0u));
+            const uint32_t f_o = lit ? ((outpos >= CAP) ? EXO : 0u) : ((sym != 256) ? EXO : 0u);
             const uint32_t fl = isl ? f_m : f_o;
             const bool ok = fl == 0u;
             const bool mt = isl & !far & ok;
@@ -825,7 +852,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
     }
 }
 
-// token-list capacity per candidate: min(one word per compressed bit, LN_OUT_CAP / 2 + 2) + 16,
+// token-list capacity per candidate: min(one word per compressed bit, cap / 2 + 2) + 16,
 // rounded to whole 16-byte groups.  A segment of at most 32 KiB needs at most 16 Ki + 1 words:
 // a literal-run word holds up to 3 bytes and two consecutive ones hold >= 4 (a short run is
 // followed by a match), a match word >= 3 bytes, so words <= bytes / 2 + 1.
@@ -842,7 +869,7 @@ __device__ __forceinline__ bool ln_dense(const uint8_t* in, uint64_t start, uint
 // for the workgroup decoder (mode 6): a lane decodes ~1 symbol per 1000 cycles, so one dense
 // segment sets the time of a wave.
 __global__ void k_lane_caps(const uint8_t* in, const uint64_t* cands, uint64_t ncand, uint64_t n, uint32_t* caps,
-                            uint32_t heavy, uint32_t limit, uint32_t* hl) {
+                            uint32_t heavy, uint32_t limit, uint32_t* hl, uint32_t ocap) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= ncand) return;
     const uint64_t nxt = j + 1 < ncand ? cands[j + 1] : n;
@@ -853,16 +880,17 @@ __global__ void k_lane_caps(const uint8_t* in, const uint64_t* cands, uint64_t n
         return;
     }
     const uint64_t bits = 8 * span;
-    const uint64_t c = min(bits, (uint64_t)LN_OUT_CAP / 2 + 2) + 16;
+    const uint64_t c = min(bits, (uint64_t)ocap / 2 + 2) + 16;
     caps[j] = (uint32_t)((c + 3) & ~3ull);
 }
 
 // Wave-cooperative copies inside the 32 KiB window.  The body of a copy goes as 16-byte aligned
 // stores, each lane building its quad from five source words with alignbyte.
-constexpr uint32_t LN_WIN_WORDS = LN_OUT_CAP / 4;
 // the 16 bytes at window byte s (the fifth word is needed only when s is not word-aligned, and
 // is clamped into the window for the aligned case)
+template <uint32_t CAP>
 __device__ __forceinline__ uint4 ln_quad_at(const uint8_t* win, uint32_t s) {
+    constexpr uint32_t LN_WIN_WORDS = CAP / 4;
     const uint32_t* const W = reinterpret_cast<const uint32_t*>(win);
     const uint32_t i = s >> 2, sh = s & 3;
     const uint32_t w0 = W[i], w1 = W[i + 1], w2 = W[i + 2], w3 = W[i + 3];
@@ -874,7 +902,9 @@ __device__ __forceinline__ uint4 ln_quad_at(const uint8_t* win, uint32_t s) {
 // ln_copy_plain moves n bytes from s to o with s + n <= o (source wholly before the destination,
 // so every lane copies independently): unaligned head and tail bytes one per lane, the body as
 // aligned quads (one quad per lane and wave-step: these copies are mostly short).
+template <uint32_t CAP>
 __device__ __forceinline__ void ln_copy_plain(uint8_t* win, uint32_t o, uint32_t s, uint32_t n) {
+    constexpr uint32_t LN_WIN_WORDS = CAP / 4;
     const uint32_t lane = lane_id();
     const uint32_t* const W = reinterpret_cast<const uint32_t*>(win);
     const uint32_t end = o + n;
@@ -901,6 +931,7 @@ __device__ __forceinline__ void ln_copy_plain(uint8_t* win, uint32_t o, uint32_t
 // (P >= Q + 16): every source quad lies in that prefix, so the rest of the match is one pass of
 // independent quad copies.  Lane phases advance by 1024 mod Q per wave-step (one division per
 // lane, at the start).
+template <uint32_t CAP>
 __device__ __forceinline__ uint32_t ln_fill_mod(uint8_t* win, uint32_t o, uint32_t P, uint32_t L, uint32_t Q,
                                                 uint8_t* out) {
     const uint32_t lane = lane_id();
@@ -918,8 +949,8 @@ __device__ __forceinline__ uint32_t ln_fill_mod(uint8_t* win, uint32_t o, uint32
     uint32_t k = lane;
     for (; k + 192 < nq; k += 256) {
         const uint32_t r1 = adv(r), r2 = adv(r1), r3 = adv(r2);
-        const uint4 v0 = ln_quad_at(win, o + r), v1 = ln_quad_at(win, o + r1);
-        const uint4 v2 = ln_quad_at(win, o + r2), v3 = ln_quad_at(win, o + r3);
+        const uint4 v0 = ln_quad_at<CAP>(win, o + r), v1 = ln_quad_at<CAP>(win, o + r1);
+        const uint4 v2 = ln_quad_at<CAP>(win, o + r2), v3 = ln_quad_at<CAP>(win, o + r3);
         D[k] = v0;
         D[k + 64] = v1;
         D[k + 128] = v2;
@@ -927,16 +958,17 @@ __device__ __forceinline__ uint32_t ln_fill_mod(uint8_t* win, uint32_t o, uint32
         r = adv(r3);
     }
     for (; k < nq; k += 64) {
-        D[k] = ln_quad_at(win, o + r);
+        D[k] = ln_quad_at<CAP>(win, o + r);
         r = adv(r);
     }
     return a0;
 }
 
-// 8 bytes of the window at byte a (a < LN_OUT_CAP); near the window's end the read is moved
+// 8 bytes of the window at byte a (a < CAP); near the window's end the read is moved
 // back inside it and shifted (only bytes below the end are used)
+template <uint32_t CAP>
 __device__ __forceinline__ uint64_t ln_rd8(const uint8_t* win, uint32_t a) {
-    const uint32_t c = min(a, LN_OUT_CAP - 8);
+    const uint32_t c = min(a, CAP - 8);
     return *reinterpret_cast<const u64_unaligned*>(win + c) >> (8 * (a - c));
 }
 // the low r (1..7) bytes of x at q
@@ -963,14 +995,15 @@ __device__ __forceinline__ void ln_store_tail(uint8_t* q, uint64_t x, uint32_t r
 // for the segment's last token (nothing reads those bytes back) the segment's output in HBM.
 // Returns the window byte from which the output went to `out` (L + o when all of it is in the
 // window).
+template <uint32_t CAP>
 __device__ __forceinline__ uint32_t ln_copy_wave(uint8_t* win, uint32_t o, uint32_t L, uint32_t d, uint8_t* out) {
     if (d >= L) {
-        ln_copy_plain(win, o, o - d, L);
+        ln_copy_plain<CAP>(win, o, o - d, L);
         return o + L;
     }
     uint32_t P;
     if (d >= 64) {
-        ln_copy_plain(win, o, o - d, d);
+        ln_copy_plain<CAP>(win, o, o - d, d);
         P = d;
     } else {
         const uint32_t lane = lane_id();
@@ -984,17 +1017,18 @@ __device__ __forceinline__ uint32_t ln_copy_wave(uint8_t* win, uint32_t o, uint3
     while (P < L && (P < c16 + 16 || L <= 4 * P)) {
         wave_sync();
         const uint32_t n = min(P, L - P);
-        ln_copy_plain(win, o + P, o, n);
+        ln_copy_plain<CAP>(win, o + P, o, n);
         P += n;
     }
     if (P < L) {
         wave_sync();
-        return ln_fill_mod(win, o, P, L, P - c16, out);
+        return ln_fill_mod<CAP>(win, o, P, L, P - c16, out);
     }
     return o + L;
 }
 
 // One segment of k_inflate_resolve: `sf` = its record's {out_size, flags}, n token words at tk.
+template <uint32_t CAP>
 __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j, uint2 sf, uint32_t n,
                                                const uint32_t* tk, uint8_t* win) {
     const uint32_t lane = threadIdx.x;
@@ -1009,23 +1043,31 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
     uint32_t wa = tk[min(lane, n - 1)];
     const uint32_t w0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)wa);  // lane 0 holds word 0
     if ((w0 >> 24) == 0) {  // stored segment: straight from the stream, 16-byte stores
-        const uint8_t* src = reinterpret_cast<const uint8_t*>(A.in_words) + A.misalign + A.cands[j] +
-                           (uint32_t)__builtin_amdgcn_readlane((int)wa, 1);  // word 1 (n = 2)
-        if ((((uintptr_t)dst) & 15) == 0) {
-            // word-aligned source base; the words read stay inside the stream (its last word
-            // holds the last data byte) except the fifth at sh == 0, which is not used then
-            const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3);
-            const uint32_t* sw = reinterpret_cast<const uint32_t*>(src - sh);
-            uint4* d4 = reinterpret_cast<uint4*>(dst);
-            for (uint32_t i = lane; i < nb / 16; i += 64) {
-                const uint32_t w0 = sw[4 * i], w1 = sw[4 * i + 1], w2 = sw[4 * i + 2], w3 = sw[4 * i + 3];
-                const uint32_t w4 = sh ? sw[4 * i + 4] : 0u;
-                d4[i] = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                                   __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+        // one (len, offset) word pair per stored block: one block, or two (a 64 KiB segment)
+        const uint8_t* const sbase = reinterpret_cast<const uint8_t*>(A.in_words) + A.misalign + A.cands[j];
+        uint32_t done = 0;
+        for (uint32_t p = 0; 2 * p + 1 < n && done < nb; p++) {
+            const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)wa, 2 * p);
+            const uint8_t* const src = sbase + (uint32_t)__builtin_amdgcn_readlane((int)wa, 2 * p + 1);
+            const uint32_t m = min(len, nb - done);
+            uint8_t* const d = dst + done;
+            if ((((uintptr_t)d) & 15) == 0) {
+                // word-aligned source base; the words read stay inside the stream (its last word
+                // holds the last data byte) except the fifth at sh == 0, which is not used then
+                const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3);
+                const uint32_t* sw = reinterpret_cast<const uint32_t*>(src - sh);
+                uint4* d4 = reinterpret_cast<uint4*>(d);
+                for (uint32_t i = lane; i < m / 16; i += 64) {
+                    const uint32_t w0 = sw[4 * i], w1 = sw[4 * i + 1], w2 = sw[4 * i + 2], w3 = sw[4 * i + 3];
+                    const uint32_t w4 = sh ? sw[4 * i + 4] : 0u;
+                    d4[i] = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                       __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+                }
+                for (uint32_t i = (m & ~15u) + lane; i < m; i += 64) d[i] = src[i];
+            } else {
+                for (uint32_t i = lane; i < m; i += 64) d[i] = src[i];
             }
-            for (uint32_t i = (nb & ~15u) + lane; i < nb; i += 64) dst[i] = src[i];
-        } else {
-            for (uint32_t i = lane; i < nb; i += 64) dst[i] = src[i];
+            done += m;
         }
         return;
     }
@@ -1062,7 +1104,7 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
                            // per word), store exactly L bytes (neighbouring tokens store beside it)
                 uint64_t v[4];
 #pragma unroll
-                for (uint32_t k = 0; k < 4; k++) v[k] = 8 * k < L ? ln_rd8(win, off - d + 8 * k) : 0ull;
+                for (uint32_t k = 0; k < 4; k++) v[k] = 8 * k < L ? ln_rd8<CAP>(win, off - d + 8 * k) : 0ull;
 #pragma unroll
                 for (uint32_t k = 0; k < 4; k++) {
                     const uint32_t b = 8 * k;
@@ -1095,7 +1137,7 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
             const uint32_t Lk = (uint32_t)__builtin_amdgcn_readlane((int)L, k);
             const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)d, k);
             const bool last = DMX_LN_DIRECT && direct && t0 + (uint32_t)k + 1 == n && ok + Lk == nb;
-            const uint32_t e = ln_copy_wave(win, ok, Lk, dk, last ? dst : win);
+            const uint32_t e = ln_copy_wave<CAP>(win, ok, Lk, dk, last ? dst : win);
             if (last) lim = e;
             wave_sync();
             n_cx++;
@@ -1140,11 +1182,12 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
 
 // one workgroup per segment (a persistent grid with ticket-drawn segments and the next record
 // prefetched measured 5-20% slower on repeat and zeros, equal on text)
+template <uint32_t CAP>
 __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs B) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[LN_OUT_CAP];  // exactly 32 KiB: five per CU
+    __shared__ __attribute__((aligned(16))) uint8_t win[CAP];  // 32 KiB: five per CU; 64 KiB: two
     const uint64_t j = blockIdx.x;
     const SegRecord* const rp = &A.recs[j];
-    ln_resolve_one(A, j, make_uint2(rp->out_size, rp->flags), B.ntok[j], B.tok + B.tokoff[j], win);
+    ln_resolve_one<CAP>(A, j, make_uint2(rp->out_size, rp->flags), B.ntok[j], B.tok + B.tokoff[j], win);
 }
 
 // number of dense candidates (*cnt zeroed by the caller)
@@ -1196,12 +1239,20 @@ hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* t
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_heavy_count, dim3(g), dim3(256), 0, st, in, A.cands, A.ncand, A.n, heavy, hl + 1);
     }
-    hipLaunchKernelGGL(k_lane_caps, dim3(g), dim3(256), 0, st, in, A.cands, A.ncand, A.n, caps, heavy, limit, hl);
+    const bool big = A.slot > LN_OUT_CAP;  // 64 KiB segments (config C4's blocks)
+    hipLaunchKernelGGL(k_lane_caps, dim3(g), dim3(256), 0, st, in, A.cands, A.ncand, A.n, caps, heavy, limit, hl,
+                       big ? 2 * LN_OUT_CAP : LN_OUT_CAP);
     hipError_t e = launch_scan_u32(caps, tokoff, A.ncand, tokoff + A.ncand, st);
     if (e != hipSuccess) return e;
     LaneArgs B{tok, tokoff, ntok, caps};
-    hipLaunchKernelGGL(k_inflate_lanes, dim3((uint32_t)((A.ncand + LN_LANES - 1) / LN_LANES)), dim3(64), 0, st, A, B);
-    hipLaunchKernelGGL(k_inflate_resolve, dim3((uint32_t)A.ncand), dim3(64), 0, st, A, B);
+    const dim3 lg((uint32_t)((A.ncand + LN_LANES - 1) / LN_LANES));
+    if (big) {
+        hipLaunchKernelGGL(k_inflate_lanes<2 * LN_OUT_CAP>, lg, dim3(64), 0, st, A, B);
+        hipLaunchKernelGGL(k_inflate_resolve<2 * LN_OUT_CAP>, dim3((uint32_t)A.ncand), dim3(64), 0, st, A, B);
+    } else {
+        hipLaunchKernelGGL(k_inflate_lanes<LN_OUT_CAP>, lg, dim3(64), 0, st, A, B);
+        hipLaunchKernelGGL(k_inflate_resolve<LN_OUT_CAP>, dim3((uint32_t)A.ncand), dim3(64), 0, st, A, B);
+    }
     if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();
 }

@@ -38,9 +38,14 @@ typedef struct dmx_ctx dmx_ctx;
 
 typedef struct dmx_config {
     int device;             /* HIP device ordinal, -1 = the calling thread's current device  */
-    uint32_t segment_bytes; /* independent deflate segment: 16384 or 32768 (default).
+    uint32_t segment_bytes; /* independent deflate segment: 16384, 32768 (default) or 65536.
                                32768 mirrors the reference's per-chunk LZ77 reset
-                               (deflate.hpp:689-697).                                          */
+                               (deflate.hpp:689-697).  65536 (SURVEY 8(d) config C4's
+                               64 KiB blocks): one DEFLATE block per 64 KiB of input, its
+                               two 32 KiB halves matched independently under one Huffman
+                               code; inflate then places 64 KiB per segment.  Inflate takes
+                               any stream with any setting; the lane decoder's slot follows
+                               this size.                                                      */
     uint32_t flags;         /* DMX_CFG_*                                                        */
     uint32_t n_gpus;        /* 0 or 1: one device.  N > 1: the host-buffer API (dmx_deflate,
                                dmx_inflate, dmx_inflate_alloc, hence deflate::compress and

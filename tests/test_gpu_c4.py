@@ -3,8 +3,9 @@
 offsets through every kernel: segment indices past 2^17, input and output offsets past 4 GiB,
 marker-scan and candidate positions past 4 GiB, token-list offsets past 2^32 bytes.
 
-Block size: C4 names 64 KiB blocks; libdmx's segments are 32 KiB (the reference's chunk,
-deflate.hpp:689-697), which is the unit every test and the bench use."""
+Block size: C4 names 64 KiB blocks (dmx_config.segment_bytes = 65536: one DEFLATE block per
+64 KiB of input, its two 32 KiB halves matched independently under one Huffman code); the
+reference's chunk is 32 KiB (deflate.hpp:689-697), libdmx's default.  Both are run at full size."""
 import gc
 
 import pytest
@@ -98,6 +99,43 @@ def test_c4_full_8GiB_mixed_shards_one_gpu(ctx, oracle):
         assert diff is None, f"shard {r}: first difference at byte {diff}"
     del d_in, stream, out
     _release()
+
+
+def test_c4_64KiB_blocks_8GiB_mixed(oracle):
+    """C4 as stated: 8 GiB of mixed data as 64 KiB DEFLATE blocks in eight 1 GiB shards (NOT_FINAL
+    except the last, concatenated as the RCCL gather does), shard 5 checked by the oracle, the
+    whole stream inflated on the lane path with 64 KiB slots and compared on the device."""
+    import torch
+    c = dmx.Context(segment_bytes=65536)
+    try:
+        world, per = 8, GiB
+        n = world * per
+        d_in = _device_corpus("mixed", n)
+        cap = world * (dmx.deflate_bound(per) + 64)
+        stream = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        offs = [0]
+        for r in range(world):
+            L = c.deflate_device(d_in.data_ptr() + r * per, per, 2, stream.data_ptr() + offs[-1],
+                                 cap - offs[-1], not_final=(r < world - 1))
+            offs.append(offs[-1] + L)
+        total = offs[-1]
+        _log(f"64 KiB blocks: 8 shards deflated, ratio {n / total:.4f}")
+        s5 = stream[offs[5]:offs[6]].cpu().numpy().tobytes() + b"\x03\x00"
+        assert oracle.inflate(s5) == dmx.corpus("mixed", per, offset=5 * per)
+        del s5
+        gc.collect()
+        out = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        olen = c.inflate_device(stream.data_ptr(), total, out.data_ptr(), n + 64)
+        _log(f"inflated {olen} bytes on path {c.stats().path}")
+        assert olen == n
+        assert c.stats().path == 4
+        for r in range(world):
+            diff = _first_diff(out[r * per:(r + 1) * per], d_in[r * per:(r + 1) * per])
+            assert diff is None, f"shard {r}: first difference at byte {diff}"
+        del d_in, stream, out
+    finally:
+        c.close()
+        _release()
 
 
 def test_stream_over_4GiB_random(ctx):
