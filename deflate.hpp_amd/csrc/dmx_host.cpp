@@ -51,6 +51,9 @@ struct DevBuf {
 };
 
 constexpr uint32_t kSegCap = 32768;  // LDS window of k_inflate_segments
+#ifndef DMX_FB_REPAIR_EXACT
+#define DMX_FB_REPAIR_EXACT 0  // path-5 repair units inside fixed-code regions on exact chunk entries
+#endif
 constexpr uint64_t LN_OUT_CAP_BYTES = 32768;  // largest segment output of the lane decoder
 
 }  // namespace
@@ -67,7 +70,7 @@ struct dmx_ctx {
     DevBuf in, out, slots, sizes, offs, scal, cands, tiles, tileoffs, recs, status, dbg;
     DevBuf dtok, dntok;                  // deflate: the front kernel's token words and counts
     DevBuf rtmp, rchain;                 // chain repair: scratch output, chain / offsets / sizes
-    DevBuf ltok, ltokoff, lntok, lcaps;  // lane decoder token lists (mode 4)
+    DevBuf ltok, ltokoff, lntok, lcaps, lsplit;  // lane decoder token lists (mode 4), 64 KiB halves
     DevBuf lheavy;                       // heavy-candidate list for the workgroup decoder (mode 6)
     int ncu = 0;                         // compute units (mode 6 grid)
     // block-parallel path (path 5): scan counts / hits / offsets, hit list, unit starts, token
@@ -506,27 +509,34 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
     };
     if (decode(0, K) != DMX_OK) return DMX_ERR_DEVICE;
     hmark(4);
-    if (dstats) {
+    // DMX_FB_DEBUG: the decode counters so far (cumulative over the first pass, the region units
+    // and the repair rounds; "longest" is the longest unit of each kind so far)
+    auto dump_stats = [&](const char* what, uint64_t Kn) -> int {
+        if (!dstats) return DMX_OK;
         uint32_t hs[16];
         unsigned long long ph[21];
         HIPCHK(hipMemcpyAsync(hs, dstats, 64, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(ph, dstats + 16, sizeof(ph), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        std::fprintf(stderr, "dmx fb: pdecode header cycles per unit: precode %llu, code lengths %llu, trees %llu, "
+        const uint64_t K = std::max<uint64_t>(Kn, 1);
+        std::fprintf(stderr, "dmx fb [%s]: pdecode header cycles per unit: precode %llu, code lengths %llu, trees %llu, "
                      "tables %llu; longest unit: lane-parallel %llu, serial %llu, serial after a block %llu, weak %llu\n",
-                     ph[10] / K, ph[11] / K, ph[12] / K, ph[13] / K, ph[14] >> 24, ph[15] >> 24, ph[16] >> 24, ph[17] >> 24);
-        std::fprintf(stderr, "dmx fb: longest lane-parallel unit: %llu settle rounds, %llu attempts; "
+                     what, ph[10] / K, ph[11] / K, ph[12] / K, ph[13] / K, ph[14] >> 24, ph[15] >> 24, ph[16] >> 24,
+                     ph[17] >> 24);
+        std::fprintf(stderr, "dmx fb [%s]: longest lane-parallel unit: %llu settle rounds, %llu attempts; "
                      "settle re-decodes %llu cycles per unit\n",
-                     (ph[14] >> 4) & 4095, ph[14] & 15, ph[20] / K);
-        std::fprintf(stderr, "dmx fb: pdecode cycles per unit: stage %llu, header %llu, tables %llu, first pass %llu, "
+                     what, (ph[14] >> 4) & 4095, ph[14] & 15, ph[20] / K);
+        std::fprintf(stderr, "dmx fb [%s]: pdecode cycles per unit: stage %llu, header %llu, tables %llu, first pass %llu, "
                      "settle %llu (%.1f rounds, %.1f lane redos), recount %llu, scans %llu, words %llu\n",
-                     ph[0] / K, ph[1] / K, ph[2] / K, ph[3] / K, ph[4] / K, (double)ph[8] / K, (double)ph[9] / K,
+                     what, ph[0] / K, ph[1] / K, ph[2] / K, ph[3] / K, ph[4] / K, (double)ph[8] / K, (double)ph[9] / K,
                      ph[5] / K, ph[6] / K, ph[7] / K);
-        std::fprintf(stderr, "dmx fb: %llu units: %u lane-parallel, %u serial, %u serial after a parallel block, %u weak; "
+        std::fprintf(stderr, "dmx fb [%s]: %llu units: %u lane-parallel, %u serial, %u serial after a parallel block, %u weak; "
                      "serial because: header %u, unsettled %u, no end of block %u, bad end %u, capacity %u, "
                      "stream-start copy %u\n",
-                     (unsigned long long)K, hs[0], hs[1], hs[2], hs[3], hs[4], hs[5], hs[6], hs[7], hs[8], hs[9]);
-    }
+                     what, (unsigned long long)Kn, hs[0], hs[1], hs[2], hs[3], hs[4], hs[5], hs[6], hs[7], hs[8], hs[9]);
+        return DMX_OK;
+    };
+    if (dump_stats("first pass", K) != DMX_OK) return DMX_ERR_DEVICE;
     uint64_t Ku = K;
     uint64_t rep_used = 0;
     // Sorted list of the starts a repair unit stops at: the scanned ones (a weak start inside a
@@ -537,12 +547,12 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         uint8_t kind;  // 0 strong / region head, 1 weak, 2 soft
     };
     std::vector<Prim> prim;
+    struct Reg {
+        uint64_t E, T, sb0, nsb;
+    };
+    std::vector<Reg> regs;  // (kept for the repair units: exact chunk entries inside a region)
     // ---- fixed-code regions ----
     {
-        struct Reg {
-            uint64_t E, T, sb0, nsb;
-        };
-        std::vector<Reg> regs;
         uint64_t nsb = 0;
         for (uint64_t k = 0; k < K; k++) {
             if (!(stops[k] & FB_STOP_REGION)) continue;
@@ -624,6 +634,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
                     in_region[k] = 1;
             }
             if (Ku > k0 && (upload(k0, Ku - k0) != DMX_OK || decode(k0, Ku - k0) != DMX_OK)) return DMX_ERR_DEVICE;
+            if (fb_debug && dump_stats("region units", Ku) != DMX_OK) return DMX_ERR_DEVICE;
         }
         for (uint64_t k = 0; k < K; k++)
             if (!in_region[k]) prim.push_back({starts[k], (uint8_t)(strong[k] ? 0 : 1)});
@@ -746,6 +757,17 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
             vmode[Ku] = br.second == FB_AT_HEADER ? FB_V_HEADER : FB_V_EXACT;
             vhdr[Ku] = br.second == FB_AT_HEADER ? 0 : br.second;
             stops[Ku] = stop_of(e);
+            // inside a fixed-code region (after a stored block there, say): the true path's
+            // chunk entries are known, so the repair unit's ranges start exactly on them too
+            // Off (DMX_FB_REPAIR_EXACT, developer A/B): measured Z_FIXED 64 MiB text 4.7 -> 4.2 ms
+            // but 32 MiB mixed 8.7 -> 13.4 ms (a repair unit after a stored block then ends
+            // serially), also with soft stops only.
+            ucb[Ku] = ~0u;
+            if (DMX_FB_REPAIR_EXACT && dcbit && (stops[Ku] & FB_STOP_SOFT)) {
+                auto rg = std::upper_bound(regs.begin(), regs.end(), e, [](uint64_t v, const Reg& g) { return v < g.E; });
+                if (rg != regs.begin() && e < (--rg)->T)
+                    ucb[Ku] = (uint32_t)((rg->sb0 + (e - rg->E) / kSuper) * 64);
+            }
             const uint64_t w = (stops[Ku] & FB_STOP_SOFT) ? region_words((stops[Ku] & FB_STOP_MASK) - std::min(e, nbits))
                                                           : words_of(e, stops[Ku]);
             if (rep_used + w > rep_words) return chain_break("repair token space", chain.back());
@@ -756,8 +778,10 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         repaired.insert(repaired.end(), breaks.begin(), breaks.end());
         std::sort(repaired.begin(), repaired.end());
         if (upload(k0, Ku - k0) != DMX_OK || decode(k0, Ku - k0) != DMX_OK) return DMX_ERR_DEVICE;
-        if (fb_debug)
+        if (fb_debug) {
             std::fprintf(stderr, "dmx fb: repair round %d: %llu units\n", round, (unsigned long long)(Ku - k0));
+            if (dump_stats("after repair round", Ku) != DMX_OK) return DMX_ERR_DEVICE;
+        }
     }
     // the path's own scratch first: when it does not fit, the stream still decodes on the
     // serial decoder, which needs only the output
@@ -915,7 +939,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
         const uint64_t per = (std::max<uint64_t>(LN_OUT_CAP_BYTES, c->seg) / 2 + 2 + 16 + 3) & ~3ull;
         const uint64_t words = std::min<uint64_t>(ncand * per, 8ull * n + 20ull * ncand);
         if (c->ltok.ensure(words * 4) && c->ltokoff.ensure(scan_words(ncand) * 8) &&
-            c->lntok.ensure(ncand * 4) && c->lcaps.ensure(ncand * 4)) {
+            c->lntok.ensure(ncand * 4) && c->lcaps.ensure(ncand * 4) && c->lsplit.ensure(ncand * 4)) {
             plan[np][0] = 4, plan[np][1] = c->seg, np++;
             // (the workgroup decoder of the heavy route takes segments of <= 32 KiB)
             if (heavy_bytes && c->seg <= 32768 && ncand < 0xFFFFFFF0ull && c->lheavy.ensure((ncand + 2) * 4)) {
@@ -960,7 +984,8 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
             if (mode == 4) {
                 HIPCHK(launch_inflate_lanes(A, c->ltok.as<uint32_t>(), c->ltokoff.as<uint64_t>(),
                                             c->lntok.as<uint32_t>(), c->lcaps.as<uint32_t>(), heavy,
-                                            heavy_limit, c->lheavy.as<uint32_t>(), st, e0, e1));
+                                            heavy_limit, c->lheavy.as<uint32_t>(), c->lsplit.as<uint32_t>(), st, e0,
+                                            e1));
             } else if (mode == 6) {
                 const uint32_t grid = (uint32_t)std::min<uint64_t>(r.exotic, (uint64_t)std::max(c->ncu, 1));
                 HIPCHK(launch_inflate_pj_list(A, A.slot, c->lheavy.as<uint32_t>(), grid, st, e1));

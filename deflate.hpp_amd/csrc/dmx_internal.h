@@ -119,9 +119,10 @@ hipError_t launch_inflate_pj(const InflateArgs& A, uint32_t seg, hipStream_t st,
 // heavy != 0: when at most `limit` candidates span more than `heavy` bytes (counted on the
 // device into hl[1]), those are declined and listed in hl (hl[0] = count, the indices from
 // hl[2] on; ncand + 2 words) for launch_inflate_pj_list.
+// split: ncand words when A.slot is 64 KiB (the halves' split), else unused
 hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* tokoff,
                                 uint32_t* ntok, uint32_t* caps, uint32_t heavy, uint32_t limit,
-                                uint32_t* hl, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+                                uint32_t* hl, uint32_t* split, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 // mode 6: the workgroup decoder over the candidates listed in hl, `grid` persistent workgroups
 hipError_t launch_inflate_pj_list(const InflateArgs& A, uint32_t seg, const uint32_t* hl, uint32_t grid,
                                   hipStream_t st, hipEvent_t ev1);

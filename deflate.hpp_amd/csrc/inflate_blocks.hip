@@ -2181,8 +2181,56 @@ __device__ void fbs_lane(const FbsBits& B, const uint32_t* lut, uint64_t p, bool
             sk++;
             sub_at += FBS_SUBB;
         }
-        const uint32_t e = lut[(uint32_t)w & 511u];
-        const uint32_t cl = e & 15u, ty = (e >> 4) & 3u;
+        // Fast path: tokens until the next event (T, the chunk target, a sub-chunk mark, the
+        // stream end) or an end of block, from the staged words only, without branches: the
+        // next word is always loaded one token ahead and merged by selects.  The general loop
+        // below (one token per trip, every test, HBM words past the staging) takes the rest.
+        {
+            uint64_t ev = min(min(T, target), nbits + 1);
+            if (sk < FBS_SUB - 1) ev = min(ev, sub_at);
+            const uint64_t wb = B.a0 >> 5;  // aligned-image word of stg[0]
+            if (p < ev && wi >= wb && wi - wb + 1 < (uint64_t)(FBS_STG + 2)) {
+                const uint32_t* const stg = B.stg;
+                uint32_t wl = (uint32_t)(wi - wb);
+                uint32_t nxt = stg[wl];
+                const uint32_t rem0 = (uint32_t)min(ev - p, (uint64_t)0x7FFFFFFF);
+                uint32_t used = 0;
+                for (;;) {
+                    const uint32_t x9 = __builtin_bitreverse32((uint32_t)w) >> 23, x8 = x9 >> 1, x7 = x9 >> 2;
+                    const bool c7 = x7 < 0x18u, c8a = (x8 >= 0x30u) & (x8 < 0xC0u), c8b = (x8 >= 0xC0u) & (x8 < 0xC8u);
+                    const uint32_t cl = c7 ? 7u : (c8a | c8b) ? 8u : 9u;
+                    const uint32_t sym = c7 ? 256u + x7 : c8a ? x8 - 0x30u : c8b ? 280u + x8 - 0xC0u : x9 - 256u;
+                    if (sym == 256u) break;  // end of block: the general loop decodes it
+                    const bool m = sym > 256u;
+                    const uint32_t n1 = cl + (m ? len_extra(sym) : 0u);
+                    const uint32_t ds = __builtin_bitreverse32((uint32_t)(w >> n1)) >> 27;
+                    const uint32_t n = m ? n1 + 5 + (ds < 30 ? dist_extra(ds) : 0u) : cl;
+                    used += n;
+                    w >>= n;
+                    nb -= n;
+                    const bool need = nb < 32;
+                    w |= need ? (uint64_t)nxt << nb : 0ull;
+                    nb += need ? 32u : 0u;
+                    wl += need ? 1u : 0u;
+                    nxt = stg[min(wl, FBS_STG + 1)];
+                    if (used >= rem0 || wl + 1 >= FBS_STG + 2) break;
+                }
+                p += used;
+                wi = wb + wl;
+                if (used) {
+                    if (p > nbits) { res = FBS_FAIL; break; }
+                    continue;  // the events at p
+                }
+            }
+        }
+        // the fixed lit/len code (RFC 1951 3.2.6) by arithmetic on the next 9 bits, MSB-first: no
+        // table read on the token's dependency chain (the map is latency-bound)
+        const uint32_t x9 = __builtin_bitreverse32((uint32_t)w) >> 23, x8 = x9 >> 1, x7 = x9 >> 2;
+        const bool c7 = x7 < 0x18u, c8a = (x8 >= 0x30u) & (x8 < 0xC0u), c8b = (x8 >= 0xC0u) & (x8 < 0xC8u);
+        const uint32_t cl = c7 ? 7u : (c8a | c8b) ? 8u : 9u;
+        const uint32_t sym = c7 ? 256u + x7 : c8a ? x8 - 0x30u : c8b ? 280u + x8 - 0xC0u : x9 - 256u;
+        const uint32_t ty = sym < 256u ? 0u : sym == 256u ? 1u : 2u;
+        (void)lut;
         if (ty == 1) {  // end of block
             p += 7;
             w >>= 7;
@@ -2192,7 +2240,7 @@ __device__ void fbs_lane(const FbsBits& B, const uint32_t* lut, uint64_t p, bool
             hdr = true;
         } else {  // literal (ty 0) or length (ty 2) + distance, <= 31 bits of the window
             const bool m = ty == 2;
-            const uint32_t n1 = cl + (m ? (e >> 6) & 15u : 0u);
+            const uint32_t n1 = cl + (m ? len_extra(sym) : 0u);  // (286 / 287: no extra bits)
             const uint32_t ds = __builtin_bitreverse32((uint32_t)(w >> n1)) >> 27;  // 5-bit distance code
             const uint32_t n = m ? n1 + 5 + (ds < 30 ? dist_extra(ds) : 0u) : cl;
             p += n;

@@ -93,6 +93,8 @@ struct LaneArgs {
     const uint64_t* tokoff; // ncand + 1 word offsets (exclusive scan of the capacities)
     uint32_t* ntok;         // ncand token counts
     uint32_t* caps;         // ncand capacities (words)
+    uint32_t* split;        // 64 KiB segments: ncand first-word indices of the second 32 KiB
+                            // half (~0: not split; 0 for a stored segment)
 };
 
 // lit/len table entry: literal / end-of-block  0 | cl(4) << 11 | sym(9)
@@ -325,8 +327,15 @@ __device__ __forceinline__ bool ln_lane_pretab(uint8_t* T, uint64_t pl) {
     return true;
 }
 
-template <uint32_t CAP>
+// CAP: the largest segment output (32 KiB; 64 KiB for config C4's blocks); NL: segments per
+// wavefront (32).  With CAP > 32 KiB the lane also finds the split of its segment into two
+// halves that k_inflate_resolve_half rebuilds in 32 KiB windows (see HALF below).  A lane
+// decodes about one symbol per 1000 cycles whatever the segment size, so a 64 KiB segment
+// takes twice a 32 KiB one's time and a stream has half as many of them: the lane pass of
+// 64 KiB blocks is at best half as fast as that of 32 KiB segments.
+template <uint32_t CAP, uint32_t NL>
 __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B) {
+    constexpr uint32_t LN_LANES = NL;
     __shared__ __attribute__((aligned(16))) uint8_t lds[LN_LANES * (LN_REGION + LN_PRE_BYTES)];
     const uint32_t lane = threadIdx.x;
     const uint64_t j = (uint64_t)blockIdx.x * LN_LANES + lane;
@@ -372,6 +381,13 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
 
     // token output: pending token (merges), 4-word queue, 16-byte stores
     uint32_t ntok = 0, qn = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+    // CAP > 32 KiB: the word index where output byte HALF begins (no token straddles it and no
+    // word merges across it), and whether a match past HALF reaches back before it; a segment
+    // with a split and no such match resolves as two independent 32 KiB halves
+    constexpr uint32_t HALF = 32768;
+    constexpr bool SPLIT = CAP > HALF;
+    uint32_t split = ~0u;
+    bool xhalf = false;
     uint32_t pk = 0, pa = 0, pd = 0;  // pending: kind (1 literal run, 2 match), bytes / L, count / d
     auto push = [&](uint32_t w) {
         q0 = q1;  // shift register (no indexed writes: stays in VGPRs)
@@ -408,6 +424,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             } else if (b0 + len > br.E || len > CAP) {
                 flags |= SEGF_EXOTIC;
             } else {
+                split = 0;  // (a stored segment is copied whole by the half resolve's first item)
                 push(len);
                 push((uint32_t)(b0 + cb - off0 - start));
                 outpos = len;
@@ -685,7 +702,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
 #if DMX_LN_PAIR
             const uint32_t sym2 = de & 511, cl2 = (de >> 11) & 15;
             const bool lit2 = !isl & (sym < 256) & ((de & 0x8000u) == 0u) & (sym2 < 256) &
-                              (outpos + 2 <= CAP);
+                              (outpos + 2 <= CAP) & (!SPLIT | (outpos + 1 != HALF));
             const uint32_t c = n1 + (isl ? dcl + dx : (lit2 ? cl2 : 0u));  // 1 .. 33 bits
 #else
             const uint32_t c = n1 + (isl ? dcl + dx : 0u);  // 1 .. 33 bits
@@ -716,9 +733,14 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
             const bool lt2 = lt & lit2;
             const uint32_t nl = lt2 ? 2u : 1u;
             const uint32_t lb = lt2 ? sym | (sym2 << 8) : sym;
-            const bool lcont = lt & (pk == 1u) & (pd + nl <= 3u);
-            const bool lsplit = lt2 & (pk == 1u) & (pd == 2u);
-            const bool mcont = mt & (pk == 2u) & (pd == d) & (pa + L <= 0xFFFFu);
+            const bool at_half = SPLIT & (outpos == HALF);  // no word merges across HALF
+            const bool lcont = lt & (pk == 1u) & (pd + nl <= 3u) & !at_half;
+            const bool lsplit = lt2 & (pk == 1u) & (pd == 2u) & !at_half;
+            const bool mcont = mt & (pk == 2u) & (pd == d) & (pa + L <= 0xFFFFu) & !at_half;
+            if (SPLIT) {
+                split = (at_half & prod & (split == ~0u)) ? ntok + qn + (pk != 0u ? 1u : 0u) : split;
+                xhalf |= mt & (outpos >= HALF) & (d > outpos - HALF);
+            }
             const bool cont = lcont | mcont;
             const bool emit = prod & !cont & (pk != 0u);
             const uint32_t ew = lsplit ? (3u << 24) | pa | (sym << 16)
@@ -844,6 +866,8 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
     r.flags = flags | (fin ? SEGF_FINAL : 0u);
     A.recs[j] = r;
     B.ntok[j] = ntok;
+    // the split holds only if the output crossed HALF at a token boundary, or never reached it
+    if (SPLIT) B.split[j] = (flags || xhalf || (outpos > HALF && split == ~0u)) ? ~0u : (outpos <= HALF ? ntok : split);
     if (dbg) {  // (slots 5..7 belong to k_inflate_resolve)
         dbg[8] = n_iter;
         dbg[9] = n_top;
@@ -1030,10 +1054,10 @@ __device__ __forceinline__ uint32_t ln_copy_wave(uint8_t* win, uint32_t o, uint3
 // One segment of k_inflate_resolve: `sf` = its record's {out_size, flags}, n token words at tk.
 template <uint32_t CAP>
 __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j, uint2 sf, uint32_t n,
-                                               const uint32_t* tk, uint8_t* win) {
+                                               const uint32_t* tk, uint8_t* win, uint32_t half_off = 0) {
     const uint32_t lane = threadIdx.x;
     if (sf.y & ~SEGF_FINAL) return;
-    const uint64_t dst0 = j * (uint64_t)A.slot;
+    const uint64_t dst0 = j * (uint64_t)A.slot + half_off;
     if (dst0 >= A.cap) return;
     const uint32_t size = sf.x;
     const uint32_t nb = (uint32_t)min((uint64_t)size, A.cap - dst0);
@@ -1186,8 +1210,31 @@ template <uint32_t CAP>
 __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs B) {
     __shared__ __attribute__((aligned(16))) uint8_t win[CAP];  // 32 KiB: five per CU; 64 KiB: two
     const uint64_t j = blockIdx.x;
+    if (CAP > LN_OUT_CAP && B.split[j] != ~0u) return;  // rebuilt by k_inflate_resolve_half
     const SegRecord* const rp = &A.recs[j];
     ln_resolve_one<CAP>(A, j, make_uint2(rp->out_size, rp->flags), B.ntok[j], B.tok + B.tokoff[j], win);
+}
+
+// 64 KiB segments whose two 32 KiB halves are independent (every libdmx 64 KiB block: its halves
+// were matched separately): two items per segment, each rebuilt in a 32 KiB window -- five
+// windows per CU instead of two 64 KiB ones.  Item 2j + h: half h, token words [0, split) or
+// [split, n), written at j * slot + 32768 h; a stored segment is copied whole by item 2j.
+__global__ __launch_bounds__(64) void k_inflate_resolve_half(InflateArgs A, LaneArgs B) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[LN_OUT_CAP];
+    const uint64_t j = blockIdx.x >> 1;
+    const uint32_t h = blockIdx.x & 1;
+    const uint32_t sp = B.split[j];
+    if (sp == ~0u) return;
+    const SegRecord* const rp = &A.recs[j];
+    const uint32_t size = rp->out_size, n = B.ntok[j];
+    const uint32_t* const tk = B.tok + B.tokoff[j];
+    if (sp == 0) {  // stored (or empty): one item copies it
+        if (h == 0) ln_resolve_one<LN_OUT_CAP>(A, j, make_uint2(size, rp->flags), n, tk, win);
+        return;
+    }
+    if (h == 0) ln_resolve_one<LN_OUT_CAP>(A, j, make_uint2(min(size, LN_OUT_CAP), rp->flags), sp, tk, win);
+    else if (size > LN_OUT_CAP)
+        ln_resolve_one<LN_OUT_CAP>(A, j, make_uint2(size - LN_OUT_CAP, rp->flags), n - sp, tk + sp, win, LN_OUT_CAP);
 }
 
 // number of dense candidates (*cnt zeroed by the caller)
@@ -1230,7 +1277,7 @@ hipError_t launch_place_segments(const uint8_t* src, uint32_t slot, const uint64
 
 hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* tokoff,
                                 uint32_t* ntok, uint32_t* caps, uint32_t heavy, uint32_t limit,
-                                uint32_t* hl, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+                                uint32_t* hl, uint32_t* split, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
     if (ev0) (void)hipEventRecord(ev0, st);
     const uint32_t g = (uint32_t)((A.ncand + 255) / 256);
     const uint8_t* const in = reinterpret_cast<const uint8_t*>(A.in_words) + A.misalign;  // stream byte 0
@@ -1244,13 +1291,18 @@ hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* t
                        big ? 2 * LN_OUT_CAP : LN_OUT_CAP);
     hipError_t e = launch_scan_u32(caps, tokoff, A.ncand, tokoff + A.ncand, st);
     if (e != hipSuccess) return e;
-    LaneArgs B{tok, tokoff, ntok, caps};
-    const dim3 lg((uint32_t)((A.ncand + LN_LANES - 1) / LN_LANES));
+    LaneArgs B{tok, tokoff, ntok, caps, split};
     if (big) {
-        hipLaunchKernelGGL(k_inflate_lanes<2 * LN_OUT_CAP>, lg, dim3(64), 0, st, A, B);
+        // (32 segments per wave here too: 16 per wave measured slower at 1 GiB of mixed data,
+        // 17.5 against ~14.5 ms for the lanes, though it puts a wave on every SIMD)
+        constexpr uint32_t NL = LN_LANES;
+        const dim3 lg((uint32_t)((A.ncand + NL - 1) / NL));
+        hipLaunchKernelGGL((k_inflate_lanes<2 * LN_OUT_CAP, NL>), lg, dim3(64), 0, st, A, B);
+        hipLaunchKernelGGL(k_inflate_resolve_half, dim3((uint32_t)(2 * A.ncand)), dim3(64), 0, st, A, B);
         hipLaunchKernelGGL(k_inflate_resolve<2 * LN_OUT_CAP>, dim3((uint32_t)A.ncand), dim3(64), 0, st, A, B);
     } else {
-        hipLaunchKernelGGL(k_inflate_lanes<LN_OUT_CAP>, lg, dim3(64), 0, st, A, B);
+        const dim3 lg((uint32_t)((A.ncand + LN_LANES - 1) / LN_LANES));
+        hipLaunchKernelGGL((k_inflate_lanes<LN_OUT_CAP, LN_LANES>), lg, dim3(64), 0, st, A, B);
         hipLaunchKernelGGL(k_inflate_resolve<LN_OUT_CAP>, dim3((uint32_t)A.ncand), dim3(64), 0, st, A, B);
     }
     if (ev1) (void)hipEventRecord(ev1, st);
