@@ -91,6 +91,8 @@ struct dmx_ctx {
     bool timing = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t ev_df = nullptr;          // end of the last deflate's work (its scratch is reused)
+    hipEvent_t ev_inf = nullptr;         // end of the last asynchronous inflate's work
+    bool inf_pending = false;
     bool df_pending = false;
     dmx_stats stats{};
     uint64_t last_end = 0;               // the last inflate: stream byte just past its final block
@@ -141,6 +143,7 @@ struct Scal {  // small device-side scalars, one allocation
     uint32_t ticket;
     uint32_t fb_err;  // block-parallel path: a copy reached before the stream start
     uint32_t fb_nkeep;  // block-parallel path: accepted unit starts (k_fb_check)
+    uint64_t ncand;     // dmx_inflate_device_async: the candidate count, on the device
     InflateResult res;
     ValidateWords vw;
 };
@@ -855,6 +858,8 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
 int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_out,
                           size_t cap, size_t* total_out, uint8_t** dev_out, hipStream_t st,
                           uint32_t iflags = 0) {
+    // an asynchronous inflate still running uses the same scratch
+    if (c->inf_pending) HIPCHK(hipStreamWaitEvent(st, c->ev_inf, 0));
     begin_timing(c, st);
     *total_out = 0;
     if (n == 0) return DMX_ERR_OVERREAD;  // the reference throws (or faults) on empty input
@@ -876,7 +881,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
         !c->status.ensure(ncand * 8))
         return DMX_ERR_NOMEM;
     HIPCHK(launch_marker_write(words, misalign, n, c->tileoffs.as<uint64_t>(), ntiles,
-                               c->cands.as<uint64_t>(), nullptr, st));
+                               c->cands.as<uint64_t>(), ~0ull, st));
 
     uint8_t* out = fixed_out;
     // The segment-parallel passes place candidate j at j * 32 KiB.  Every 00 00 FF FF inside
@@ -1183,6 +1188,65 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     return r.status;
 }
 
+// dmx_inflate_device_async: the lane path (path 4) of a libdmx-layout stream with no host
+// synchronisation.  The candidate count stays on the device: the scratch is provisioned for
+// cap / segment + 64 candidates (a libdmx stream has one per segment), the grids are sized for
+// that many and every kernel stops at the device-side count.  No heavy route, no patch pass,
+// no chain repair: any stream the lanes do not decode whole -- another layout, a declined
+// segment, more candidates than provisioned, output beyond cap -- ends with status 1 in
+// d_result[1], and the caller decodes it with dmx_inflate_device.
+int inflate_device_async_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* d_out, size_t cap,
+                                uint64_t* d_result, hipStream_t st, uint32_t iflags) {
+    static const uint64_t fail[2] = {0, 1};
+    if (c->inf_pending) HIPCHK(hipStreamWaitEvent(st, c->ev_inf, 0));
+    if (n == 0) {
+        HIPCHK(hipMemcpyAsync(d_result, fail, 16, hipMemcpyHostToDevice, st));
+        return DMX_OK;
+    }
+    if (!c->scal.ensure(sizeof(Scal))) return DMX_ERR_NOMEM;
+    Scal* ds = c->scal.as<Scal>();
+    const uint64_t misalign = (uintptr_t)d_in & 3;
+    const uint32_t* words = reinterpret_cast<const uint32_t*>(d_in - misalign);
+    const uint64_t slot = c->seg;
+    const uint64_t ncap = cap / slot + 64;
+    const uint64_t ntiles = marker_tiles(n, misalign);
+    const uint64_t per = (std::max<uint64_t>(LN_OUT_CAP_BYTES, slot) / 2 + 2 + 16 + 3) & ~3ull;
+    const uint64_t words_tok = std::min<uint64_t>(ncap * per, 8ull * n + 20ull * ncap);
+    if (!c->tiles.ensure(ntiles * 4) || !c->tileoffs.ensure(scan_words(ntiles) * 8) || !c->cands.ensure(ncap * 8) ||
+        !c->recs.ensure(ncap * sizeof(SegRecord)) || !c->status.ensure(ncap * 8) || !c->ltok.ensure(words_tok * 4) ||
+        !c->ltokoff.ensure(scan_words(ncap) * 8) || !c->lntok.ensure(ncap * 4) || !c->lcaps.ensure(ncap * 4) ||
+        !c->lsplit.ensure(ncap * 4))
+        return DMX_ERR_NOMEM;
+    HIPCHK(launch_marker_count(words, misalign, n, c->tiles.as<uint32_t>(), ntiles, st));
+    HIPCHK(launch_scan_u32(c->tiles.as<uint32_t>(), c->tileoffs.as<uint64_t>(), ntiles, &ds->nmarkers, st));
+    HIPCHK(launch_async_prep(&ds->nmarkers, &ds->ncand, st));
+    HIPCHK(launch_marker_write(words, misalign, n, c->tileoffs.as<uint64_t>(), ntiles, c->cands.as<uint64_t>(), ncap,
+                               st));
+    InflateArgs A;
+    A.in_words = words;
+    A.misalign = misalign;
+    A.n = n;
+    A.cands = c->cands.as<uint64_t>();
+    A.ncand = ncap;
+    A.ncand_dev = &ds->ncand;
+    A.out = d_out;
+    A.cap = cap;
+    A.recs = c->recs.as<SegRecord>();
+    A.status = c->status.as<unsigned long long>();
+    A.ticket = &ds->ticket;
+    A.flags = c->flags | iflags;
+    A.mode = 4;
+    A.slot = (uint32_t)slot;
+    A.dbg = nullptr;
+    HIPCHK(launch_inflate_lanes(A, c->ltok.as<uint32_t>(), c->ltokoff.as<uint64_t>(), c->lntok.as<uint32_t>(),
+                                c->lcaps.as<uint32_t>(), 0, 0, nullptr, c->lsplit.as<uint32_t>(), st, nullptr, nullptr));
+    HIPCHK(launch_inflate_validate(A, &ds->vw, &ds->res, st));
+    HIPCHK(launch_async_result(&ds->res, &ds->ncand, ncap, cap, d_result, st));
+    HIPCHK(hipEventRecord(c->ev_inf, st));
+    c->inf_pending = true;
+    return DMX_OK;
+}
+
 // Adler-32 / CRC-32 of a device buffer, computed on the GPU (checksum.hip); the value is
 // returned to the host (the call synchronizes the stream).
 int checksum_locked(dmx_ctx* c, bool crc, const uint8_t* d, size_t n, uint32_t init, uint32_t* out,
@@ -1486,7 +1550,8 @@ int dmx_create(dmx_ctx** out, const dmx_config* cfg) {
         return DMX_ERR_DEVICE;
     }
     for (auto& e : c->ev) (void)hipEventCreate(&e);
-    if (hipEventCreateWithFlags(&c->ev_df, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&c->ev_df, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_inf, hipEventDisableTiming) != hipSuccess) {
         dmx_destroy(c);
         return DMX_ERR_DEVICE;
     }
@@ -1524,6 +1589,7 @@ void dmx_destroy(dmx_ctx* c) {
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_df) (void)hipEventDestroy(c->ev_df);
+    if (c->ev_inf) (void)hipEventDestroy(c->ev_inf);
     if (c->fbkeep_h) (void)hipHostFree(c->fbkeep_h);
     if (c->pin) (void)hipHostFree(c->pin);
     (void)hipStreamDestroy(c->stream);
@@ -1587,6 +1653,17 @@ int dmx_inflate_device(dmx_ctx* c, const void* d_in, size_t n, void* d_out, size
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     return inflate_device_locked(c, (const uint8_t*)d_in, n, (uint8_t*)d_out, cap, out_len,
                                  nullptr, st);
+}
+
+int dmx_inflate_device_async(dmx_ctx* c, const void* d_in, size_t n, void* d_out, size_t cap,
+                             uint64_t* d_result, uint32_t flags, void* stream) {
+    if (!c || (!d_in && n) || !d_out || !d_result || (flags & ~DMX_INFLATE_PIECE)) return DMX_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    DeviceGuard dg(c->device);
+    if (!dg.ok) return DMX_ERR_DEVICE;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return inflate_device_async_locked(c, (const uint8_t*)d_in, n, (uint8_t*)d_out, cap, d_result, st,
+                                       (flags & DMX_INFLATE_PIECE) ? DMX_IFLAG_PIECE : 0u);
 }
 
 int dmx_inflate_piece_device(dmx_ctx* c, const void* d_in, size_t n, void* d_out, size_t cap,
@@ -1718,7 +1795,7 @@ int dmx_segment_starts_device(dmx_ctx* c, const void* d_in, size_t n, uint64_t* 
     HIPCHK(hipStreamSynchronize(st));
     if (!c->cands.ensure((nm + 1) * 8)) return DMX_ERR_NOMEM;
     HIPCHK(launch_marker_write(words, misalign, n, c->tileoffs.as<uint64_t>(), ntiles, c->cands.as<uint64_t>(),
-                               nullptr, st));
+                               ~0ull, st));
     // cands[0] is the stream start; markers follow
     const size_t k = std::min<size_t>(cap, nm);
     if (k) HIPCHK(hipMemcpyAsync(starts, c->cands.as<uint64_t>() + 1, k * 8, hipMemcpyDeviceToHost, st));

@@ -77,7 +77,14 @@ struct InflateArgs {
                                  // 6 = k_inflate_pj_list patching the heavy candidates of mode 4
     uint32_t slot;               // mode 2: segment bytes (16384 or 32768)
     uint64_t* dbg;               // optional per-segment phase timestamps (DMX_PHASES)
+    // dmx_inflate_device_async: the candidate count lives on the device (<= ncand, which is then
+    // the capacity the grids are sized for); nullptr: ncand is the count
+    const uint64_t* ncand_dev = nullptr;
 };
+// the candidate count a kernel works on
+__device__ __forceinline__ uint64_t cand_count(const InflateArgs& A) {
+    return A.ncand_dev ? (*A.ncand_dev < A.ncand ? *A.ncand_dev : A.ncand) : A.ncand;
+}
 
 constexpr int kPhaseSlots = 16;
 #define DMX_PHASE(dbg, idx, slot)                                                   \
@@ -98,9 +105,16 @@ struct InflateResult {
 
 hipError_t launch_marker_count(const uint32_t* in_words, uint64_t misalign, uint64_t n,
                                uint32_t* tile_counts, uint64_t ntiles, hipStream_t st);
+// cands holds cand_cap entries: candidates past them are not written (the async inflate sizes
+// its scratch before the count is known)
 hipError_t launch_marker_write(const uint32_t* in_words, uint64_t misalign, uint64_t n,
                                const uint64_t* tile_offs, uint64_t ntiles, uint64_t* cands,
-                               uint64_t* ncand_out, hipStream_t st);
+                               uint64_t cand_cap, hipStream_t st);
+// dmx_inflate_device_async: *ncand = min(nmarkers + 1, ...) on the device; the result words
+// {decoded bytes, status} from the validation (status 0: decoded; 1: needs the general path)
+hipError_t launch_async_prep(const uint64_t* nmarkers, uint64_t* ncand, hipStream_t st);
+hipError_t launch_async_result(const InflateResult* res, const uint64_t* ncand, uint64_t cand_cap, uint64_t cap,
+                               uint64_t* d_result, hipStream_t st);
 uint64_t marker_tiles(uint64_t n, uint64_t misalign);
 // exclusive scan of n values into offs (64-bit) and *total; offs must hold scan_words(n)
 // entries (the block sums of the multi-workgroup scan follow the n offsets)

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(MK_NT) void k_marker_count(const uint32_t* w, uint6
 
 __global__ __launch_bounds__(MK_NT) void k_marker_write(const uint32_t* w, uint64_t misalign,
                                                         uint64_t n, const uint64_t* tile_offs,
-                                                        uint64_t* cands) {
+                                                        uint64_t* cands, uint64_t cand_cap) {
     __shared__ uint32_t part[MK_NT / 64];
     const uint64_t g = (uint64_t)blockIdx.x * MK_NT + threadIdx.x;
     uint32_t mask = mk_scan16(w, misalign, n, g);
@@ -119,7 +119,8 @@ __global__ __launch_bounds__(MK_NT) void k_marker_write(const uint32_t* w, uint6
     while (mask) {
         const int i = __builtin_ctz(mask);
         mask &= mask - 1;
-        cands[o++] = 16 * g + i - misalign;
+        if (o < cand_cap) cands[o] = 16 * g + i - misalign;
+        o++;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) cands[0] = 0;
 }
@@ -137,9 +138,9 @@ hipError_t launch_marker_count(const uint32_t* in_words, uint64_t misalign, uint
 
 hipError_t launch_marker_write(const uint32_t* in_words, uint64_t misalign, uint64_t n,
                                const uint64_t* tile_offs, uint64_t ntiles, uint64_t* cands,
-                               uint64_t*, hipStream_t st) {
+                               uint64_t cand_cap, hipStream_t st) {
     hipLaunchKernelGGL(k_marker_write, dim3((uint32_t)ntiles), dim3(MK_NT), 0, st, in_words,
-                       misalign, n, tile_offs, cands);
+                       misalign, n, tile_offs, cands, cand_cap);
     return hipGetLastError();
 }
 
@@ -886,7 +887,8 @@ __global__ __launch_bounds__(256) void k_inflate_validate_scan(InflateArgs A, Va
     // mode 2 / 4 placed segment j at j * slot
     const uint32_t size0 = A.mode >= 2 ? A.slot : A.recs[0].out_size;
     const uint64_t j = (uint64_t)blockIdx.x * 256 + t;
-    if (j < A.ncand) {
+    const uint64_t nc = cand_count(A);
+    if (j < nc) {
         const SegRecord r = A.recs[j];
         if (r.flags & SEGF_EXOTIC) {  // the pass declined this candidate
             atomicMin(&xmin, (unsigned long long)j);
@@ -894,7 +896,7 @@ __global__ __launch_bounds__(256) void k_inflate_validate_scan(InflateArgs A, Va
         } else {
             const bool fin = (r.flags & SEGF_FINAL) != 0;
             const bool err = (r.flags & ~SEGF_FINAL) != 0;
-            const bool chain = (j + 1 < A.ncand) && r.end_byte == A.cands[j + 1];
+            const bool chain = (j + 1 < nc) && r.end_byte == A.cands[j + 1];
             if (fin) atomicMin(&kmin, (unsigned long long)j);
             if (err || (!fin && !chain)) atomicMin(&bmin, (unsigned long long)j);
             if (!fin && r.out_size != size0) atomicMin(&umin, (unsigned long long)j);
@@ -915,10 +917,11 @@ __global__ void k_inflate_validate(InflateArgs A, const ValidateWords* W, Inflat
     const uint64_t k = unmax(W->kmin), bmin = unmax(W->bmin), umin = unmax(W->umin), xmin = unmax(W->xmin);
     res->fin_index = (uint32_t)k;
     res->exotic = W->xcnt;
-    if (xmin < A.ncand) {
+    const uint64_t nc = cand_count(A);
+    if (xmin < nc) {
         res->status = 1;
         res->total = 0;
-    } else if (k < A.ncand && bmin > k) {
+    } else if (k < nc && bmin > k) {
         if (A.mode != 1 && umin < k) {
             res->status = 1;
             res->total = 0;
@@ -1380,6 +1383,26 @@ hipError_t launch_inflate_segments(const InflateArgs& A, hipStream_t st, hipEven
     if (ev0) (void)hipEventRecord(ev0, st);
     hipLaunchKernelGGL(k_inflate_segments, dim3((uint32_t)A.ncand), dim3(IF_NT), 0, st, A);
     if (ev1) (void)hipEventRecord(ev1, st);
+    return hipGetLastError();
+}
+
+__global__ void k_async_prep(const uint64_t* nmarkers, uint64_t* ncand) { *ncand = *nmarkers + 1; }
+// status 0 only when the lane pass decoded the whole chain up to BFINAL, every candidate fit the
+// provisioned scratch and the output fits cap; anything else is the general path's (the caller's
+// synchronous dmx_inflate_device)
+__global__ void k_async_result(const InflateResult* res, const uint64_t* ncand, uint64_t cand_cap, uint64_t cap,
+                               uint64_t* d_result) {
+    const bool ok = res->status == 0 && *ncand <= cand_cap && res->total <= cap;
+    d_result[0] = ok ? res->total : 0;
+    d_result[1] = ok ? 0 : 1;
+}
+hipError_t launch_async_prep(const uint64_t* nmarkers, uint64_t* ncand, hipStream_t st) {
+    hipLaunchKernelGGL(k_async_prep, dim3(1), dim3(1), 0, st, nmarkers, ncand);
+    return hipGetLastError();
+}
+hipError_t launch_async_result(const InflateResult* res, const uint64_t* ncand, uint64_t cand_cap, uint64_t cap,
+                               uint64_t* d_result, hipStream_t st) {
+    hipLaunchKernelGGL(k_async_result, dim3(1), dim3(1), 0, st, res, ncand, cand_cap, cap, d_result);
     return hipGetLastError();
 }
 

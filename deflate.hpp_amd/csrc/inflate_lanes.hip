@@ -340,7 +340,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
     const uint32_t lane = threadIdx.x;
     const uint64_t j = (uint64_t)blockIdx.x * LN_LANES + lane;
     // lanes 0 .. LN_LANES-1 decode one segment each; the whole wave builds the tables
-    const bool seg_lane = lane < LN_LANES && j < A.ncand;
+    const bool seg_lane = lane < LN_LANES && j < cand_count(A);
     uint8_t* const R = lds + min(lane, LN_LANES - 1) * LN_REGION;
     uint8_t* const SH = lds + LN_LANES * LN_REGION;  // shared area
     uint8_t* const PRE = SH + min(lane, LN_LANES - 1) * LN_PRE_BYTES;
@@ -893,9 +893,14 @@ __device__ __forceinline__ bool ln_dense(const uint8_t* in, uint64_t start, uint
 // for the workgroup decoder (mode 6): a lane decodes ~1 symbol per 1000 cycles, so one dense
 // segment sets the time of a wave.
 __global__ void k_lane_caps(const uint8_t* in, const uint64_t* cands, uint64_t ncand, uint64_t n, uint32_t* caps,
-                            uint32_t heavy, uint32_t limit, uint32_t* hl, uint32_t ocap) {
+                            uint32_t heavy, uint32_t limit, uint32_t* hl, uint32_t ocap, const uint64_t* ncand_dev) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= ncand) return;
+    if (ncand_dev && j >= *ncand_dev) {  // (async: past the device-side count)
+        caps[j] = 0;
+        return;
+    }
+    if (ncand_dev && *ncand_dev < ncand) ncand = *ncand_dev;
     const uint64_t nxt = j + 1 < ncand ? cands[j + 1] : n;
     const uint64_t span = nxt - cands[j];
     if (heavy && ln_dense(in, cands[j], n, span, heavy) && hl[1] <= limit) {
@@ -1210,6 +1215,7 @@ template <uint32_t CAP>
 __global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs B) {
     __shared__ __attribute__((aligned(16))) uint8_t win[CAP];  // 32 KiB: five per CU; 64 KiB: two
     const uint64_t j = blockIdx.x;
+    if (j >= cand_count(A)) return;
     if (CAP > LN_OUT_CAP && B.split[j] != ~0u) return;  // rebuilt by k_inflate_resolve_half
     const SegRecord* const rp = &A.recs[j];
     ln_resolve_one<CAP>(A, j, make_uint2(rp->out_size, rp->flags), B.ntok[j], B.tok + B.tokoff[j], win);
@@ -1223,6 +1229,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve_half(InflateArgs A, Lane
     __shared__ __attribute__((aligned(16))) uint8_t win[LN_OUT_CAP];
     const uint64_t j = blockIdx.x >> 1;
     const uint32_t h = blockIdx.x & 1;
+    if (j >= cand_count(A)) return;
     const uint32_t sp = B.split[j];
     if (sp == ~0u) return;
     const SegRecord* const rp = &A.recs[j];
@@ -1288,7 +1295,7 @@ hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* t
     }
     const bool big = A.slot > LN_OUT_CAP;  // 64 KiB segments (config C4's blocks)
     hipLaunchKernelGGL(k_lane_caps, dim3(g), dim3(256), 0, st, in, A.cands, A.ncand, A.n, caps, heavy, limit, hl,
-                       big ? 2 * LN_OUT_CAP : LN_OUT_CAP);
+                       big ? 2 * LN_OUT_CAP : LN_OUT_CAP, A.ncand_dev);
     hipError_t e = launch_scan_u32(caps, tokoff, A.ncand, tokoff + A.ncand, st);
     if (e != hipSuccess) return e;
     LaneArgs B{tok, tokoff, ntok, caps, split};

@@ -37,6 +37,7 @@ EXPORTS = [
     "dmx_framed_bound", "dmx_deflate_zlib", "dmx_deflate_gzip", "dmx_inflate_zlib", "dmx_inflate_gzip",
     "dmx_deflate_file", "dmx_inflate_file", "dmx_segment_starts_device", "dmx_inflate_piece_device",
     "dmx_segment_check_device", "dmx_set_default_config", "dmx_deflate_device_async",
+    "dmx_inflate_device_async",
 ]
 
 
@@ -93,6 +94,7 @@ def lib():
     L.dmx_deflate_device_async.argtypes = [vp, vp, sz, ctypes.c_int, ctypes.c_uint32, vp, sz, vp, vp]
     L.dmx_set_default_config.argtypes = [ctypes.POINTER(Config)]
     L.dmx_inflate_device.argtypes = [vp, vp, sz, vp, sz, ctypes.POINTER(sz), vp]
+    L.dmx_inflate_device_async.argtypes = [vp, vp, sz, vp, sz, vp, ctypes.c_uint32, vp]
     L.dmx_set_timing.argtypes = [vp, ctypes.c_int]
     L.dmx_last_stats.argtypes = [vp, ctypes.POINTER(Stats)]
     L.dmx_corpus_generate.argtypes = [ctypes.c_int, ctypes.c_uint64, sz, vp]
@@ -325,6 +327,14 @@ class Context:
                                       ctypes.byref(out_len), ctypes.c_void_p(stream) if stream else None)
         _check(rc, "inflate_device")
         return out_len.value
+
+    def inflate_device_async(self, d_in, n, d_out, cap, d_result, stream=None, piece=False):
+        """Enqueue the lane-path inflate of a libdmx-layout stream; d_result (16 device bytes)
+        receives {decoded bytes, status}; status 1: decode it with inflate_device instead."""
+        rc = lib().dmx_inflate_device_async(self.h, ctypes.c_void_p(d_in), n, ctypes.c_void_p(d_out), cap,
+                                            ctypes.c_void_p(d_result), 1 if piece else 0,
+                                            ctypes.c_void_p(stream) if stream else None)
+        _check(rc, "inflate_device_async")
 
     def inflate_piece_device(self, d_in, n, d_out, cap, stream=None):
         """inflate_device for one piece of a larger stream: a reference before the piece start

@@ -158,6 +158,22 @@ int dmx_deflate_device_async(dmx_ctx* ctx, const void* d_in, size_t n, int level
 int dmx_inflate_device(dmx_ctx* ctx, const void* d_in, size_t n, void* d_out, size_t cap,
                        size_t* out_len, void* stream);
 
+/* Device-resident inflate without any host synchronisation, for streams in libdmx's segment
+ * layout (its own deflate output, or any stream of independent marker-delimited segments of at
+ * most segment_bytes each): every step is enqueued on `stream` and the call returns at once
+ * (graph-capturable; a multi-GPU caller keeps every device busy from one thread).  When the
+ * work completes, d_result (16 bytes of DEVICE memory) holds {decoded bytes, status}: status 0
+ * = decoded into d_out; status 1 = this fast path does not take the stream (another layout, a
+ * segment it declines, more segments than cap / segment_bytes + 64, output beyond cap) and
+ * nothing is promised about d_out -- decode it with dmx_inflate_device, which takes any stream.
+ * flags: DMX_INFLATE_PIECE for one piece of a larger stream (a back-reference before the piece
+ * is an error, as in dmx_inflate_piece_device).  Calls on one context are ordered even across
+ * streams.  Replaces nothing in the reference (whose inflate is synchronous, inflate.hpp:
+ * 338-408); it is the asynchronous form of the same decode (multi-GPU pieces). */
+#define DMX_INFLATE_PIECE 1u
+int dmx_inflate_device_async(dmx_ctx* ctx, const void* d_in, size_t n, void* d_out, size_t cap,
+                             uint64_t* d_result, uint32_t flags, void* stream);
+
 /* Byte offsets just past every "00 00 FF FF" (empty stored block) in a device-resident stream:
  * the candidate segment starts of libdmx's layout, in order (at most cap written, *count = all).
  * Multi-GPU inflate splits a stream at these (deflate.hpp_amd/shard.py scatter_inflate); a

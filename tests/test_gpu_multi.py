@@ -116,3 +116,59 @@ def test_n_gpus_bound():
     with pytest.raises(dmx.DmxError) as e:
         dmx.Context(n_gpus=1 << 20)
     assert e.value.code == dmx.DMX_ERR_ARG
+
+
+@pytest.mark.parametrize("seg", [32768, 65536])
+def test_inflate_device_async(oracle, seg):
+    """dmx_inflate_device_async: libdmx-layout streams decode with no host
+    synchronisation -- the candidate count stays on the device -- and give the synchronous
+    call's bytes; a stream of another layout (zlib's), a too-small cap or a piece whose first
+    segment reaches back report status 1 for the caller's synchronous fallback.  Two calls on
+    different streams are ordered by the context."""
+    import zlib
+    import torch
+    c = dmx.Context(segment_bytes=seg)
+    try:
+        data = dmx.corpus("mixed", (24 << 20) + 777, offset=3)
+        s = c.compress(data, 2)
+        d_in = torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda()
+        d_o = torch.zeros(len(data) + 64, dtype=torch.uint8, device="cuda")
+        d_r = torch.full((2,), 7, dtype=torch.int64, device="cuda")
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        c.inflate_device_async(d_in.data_ptr(), len(s), d_o.data_ptr(), d_o.numel(), d_r.data_ptr(),
+                               stream=s1.cuda_stream)
+        # a second call on another stream into another buffer: ordered behind the first
+        d_o2 = torch.zeros_like(d_o)
+        d_r2 = torch.full((2,), 7, dtype=torch.int64, device="cuda")
+        c.inflate_device_async(d_in.data_ptr(), len(s), d_o2.data_ptr(), d_o2.numel(), d_r2.data_ptr(),
+                               stream=s2.cuda_stream)
+        torch.cuda.synchronize()
+        for r, o in ((d_r, d_o), (d_r2, d_o2)):
+            n, st = (int(x) for x in r.tolist())
+            assert (n, st) == (len(data), 0)
+            assert o[:n].cpu().numpy().tobytes() == data
+        # another layout: status 1, and the synchronous call decodes it
+        z = zlib.compressobj(1, zlib.DEFLATED, -15)
+        zs = z.compress(data) + z.flush()
+        d_z = torch.frombuffer(bytearray(zs), dtype=torch.uint8).cuda()
+        c.inflate_device_async(d_z.data_ptr(), len(zs), d_o.data_ptr(), d_o.numel(), d_r.data_ptr())
+        torch.cuda.synchronize()
+        assert int(d_r[1]) == 1
+        assert c.inflate_device(d_z.data_ptr(), len(zs), d_o.data_ptr(), d_o.numel()) == len(data)
+        # output beyond cap: status 1
+        c.inflate_device_async(d_in.data_ptr(), len(s), d_o.data_ptr(), len(data) // 2, d_r.data_ptr())
+        torch.cuda.synchronize()
+        assert int(d_r[1]) == 1
+        # a piece cut at a proven segment start, closed with an empty final block, piece mode
+        starts = c.segment_starts_device(d_in.data_ptr(), len(s))
+        cut = starts[len(starts) // 2]
+        piece = s[cut:]
+        d_p = torch.frombuffer(bytearray(piece), dtype=torch.uint8).cuda()
+        c.inflate_device_async(d_p.data_ptr(), len(piece), d_o.data_ptr(), d_o.numel(), d_r.data_ptr(), piece=True)
+        torch.cuda.synchronize()
+        n, st = (int(x) for x in d_r.tolist())
+        assert st == 0
+        want = oracle.inflate(piece)
+        assert d_o[:n].cpu().numpy().tobytes() == want == data[len(data) - len(want):]
+    finally:
+        c.close()
