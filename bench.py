@@ -54,7 +54,7 @@ REF_NOTES = {"text": "reference L2 stream is lossy (SURVEY A-1)",
              "mixed": "reference L2 stream is invalid (SURVEY A-3)",
              "bmp": "reference L2 stream is invalid (SURVEY A-3)"}
 REF_RATIO_L3_TEXT = 2.5741  # reference L3 on the 1 MiB text prefix
-PROFILE_TAG = "r05"  # tools/profile_all.sh writes profiles/<tag>_kstats_*.csv and traffic.json
+PROFILE_TAG = "r06"  # tools/profile_all.sh writes profiles/<tag>_kstats_*.csv and traffic.json
 
 
 def profile_path(name):
@@ -331,7 +331,7 @@ def corpus_record(run, kind, level, steps, tag=None):
     run.torch.cuda.synchronize(run.dev)
     s = summarize(recs, run.n)
     n = run.n
-    inf_k = ["k_inflate_lanes", "k_inflate_resolve", "k_inflate_pj_list"]
+    inf_k = ["k_inflate_lanes", "k_inflate_resolve", "k_inflate_resolve_half", "k_inflate_pj_list"]
     return {"bytes": n, "level": level, "roundtrip_ok": ok,
             "roundtrip_GBps": round(n / ((s["t_def"] + s["t_inf"]) * 1e-3) / 1e9, 3),
             "deflate_GBps": round(n / (s["t_def"] * 1e-3) / 1e9, 3),

@@ -456,6 +456,10 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
         return (w + 63) & ~63ull;
     };
     auto region_words = [](uint64_t span) -> uint64_t { return ((span / 3 + 4096) + 63) & ~63ull; };
+    // a repair unit (or the last unit of a failed region walk) whose stop is far: at most this
+    // many words (>= 6 Mbit of the densest code); when they fill, it stops softly and the next
+    // repair round continues it, instead of reserving 2/3 of a word per bit up to the stop
+    constexpr uint64_t kOpenWords = (1ull << 22) + 4096;
     // region budget: every long gap could become one region of units, each with a repair
     uint64_t reg_budget = 0, reg_units_max = 0;
     for (uint64_t k = 0; k < K; k++)
@@ -602,9 +606,13 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
                     std::fprintf(stderr, "dmx fb: region %llu: bits %llu..%llu, %llu super blocks, walk %s\n",
                                  (unsigned long long)r, (unsigned long long)regs[r].E, (unsigned long long)regs[r].T,
                                  (unsigned long long)regs[r].nsb,
-                                 rs == FB_REGION_END ? "end" : rs == FB_REGION_LINK ? "link" : "fail");
-                // no token path through the region: the serial decoder reports what is wrong
-                if (rs != FB_REGION_END && rs != FB_REGION_LINK) return DMX_OK;
+                                 rs == FB_REGION_END ? "end" : rs == FB_REGION_LINK ? "link" : "fail (cut there)");
+                // A failed walk (the map met a dynamic header that was not a listed start, a
+                // stored block past T, ...): the super blocks it visited before failing are still
+                // on the true path, so they keep their units; the last one decodes on towards T
+                // (through the unlisted block, as far as its token space goes) and repair units
+                // take the rest -- only that span loses parallelism, not the stream.
+                const bool walked = rs == FB_REGION_END || rs == FB_REGION_LINK;
                 const uint64_t first = Ku;
                 for (uint64_t j = 0; j < regs[r].nsb; j++) {
                     const uint32_t v = vis[regs[r].sb0 + j];
@@ -619,7 +627,9 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
                 }
                 for (uint64_t k = first; k < Ku; k++) {
                     stops[k] = k + 1 < Ku ? (starts[k + 1] | FB_STOP_SOFT) : regs[r].T;
-                    const uint64_t w = region_words(std::min(stops[k] & FB_STOP_MASK, nbits) - starts[k]);
+                    const uint64_t w = k + 1 < Ku || walked
+                                           ? region_words(std::min(stops[k] & FB_STOP_MASK, nbits) - starts[k])
+                                           : std::min(words_of(starts[k], stops[k]), kOpenWords);
                     if (rep_used + w > rep_words) {
                         if (fb_debug)  // (say so instead of a silent serial decode)
                             std::fprintf(stderr, "dmx fb: region token space (%llu words) exhausted at unit %llu: "
@@ -772,7 +782,7 @@ int inflate_fb_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fixed_
                     ucb[Ku] = (uint32_t)((rg->sb0 + (e - rg->E) / kSuper) * 64);
             }
             const uint64_t w = (stops[Ku] & FB_STOP_SOFT) ? region_words((stops[Ku] & FB_STOP_MASK) - std::min(e, nbits))
-                                                          : words_of(e, stops[Ku]);
+                                                          : std::min(words_of(e, stops[Ku]), kOpenWords);
             if (rep_used + w > rep_words) return chain_break("repair token space", chain.back());
             tokoff[Ku + 1] = tokoff[Ku] + w;
             rep_used += w;

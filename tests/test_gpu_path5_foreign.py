@@ -187,3 +187,53 @@ def test_path5_truncated_stream_reports_error_from_chain(ctx, oracle):
         if ref is not None:
             assert raised
             assert ms < ref, (cut, ms, ref)
+
+
+def _fixed_bits(data, final):
+    """One fixed-code block of literals as a bit array (sending order), not byte-padded."""
+    import numpy as np
+    a = np.frombuffer(bytes(data), dtype=np.uint8).astype(np.uint32)
+    code = np.where(a < 144, 0x30 + a, 0x190 + a - 144)
+    ln = np.where(a < 144, 8, 9)
+    j = np.arange(9, dtype=np.uint32)
+    bits = ((code[:, None] >> np.maximum(ln[:, None] - 1 - j[None, :], 0)) & 1).astype(np.uint8)
+    body = bits[j[None, :] < ln[:, None]]
+    head = np.array([1 if final else 0, 1, 0], dtype=np.uint8)
+    return np.concatenate([head, body, np.zeros(7, dtype=np.uint8)])
+
+
+def test_path5_unlisted_dynamic_header_inside_fixed_run(ctx, oracle):
+    """A dynamic block inside a long fixed-code run whose header the scan's check rejects (its
+    lit/len code is incomplete -- valid for the reference's decoder, inflate.hpp:136-224, but
+    not a candidate the check accepts): the region map meets a dynamic header that is not a
+    listed start, so the region has no token path.  That region's span is decoded by repair
+    units on the block-parallel path (it used to send the whole stream to the serial
+    decoder); the bytes are the oracle's."""
+    import numpy as np
+    from golden.quirk_streams import BitWriter, canonical, rle_ops, write_dynamic_header
+    a = dmx.corpus("mixed", 1 << 20, offset=11)
+    b = dmx.corpus("text", 1 << 20, offset=22)
+    # the dynamic block: 16 literals 'a'..'p' and end of block at 5 bits -- 17/32 of the code
+    # space (incomplete); two distance codes of one bit
+    L = [0] * 257
+    for s in list(range(ord("a"), ord("a") + 16)) + [256]:
+        L[s] = 5
+    lc = canonical(L)
+    payload = bytes((ord("a") + (i * 7) % 16) for i in range(5000))
+    bw = BitWriter()
+    bw.put(0, 1)
+    bw.put(2, 2)
+    write_dynamic_header(bw, rle_ops(L) + rle_ops([1, 1]), 257, 2)
+    for ch in payload:
+        bw.put_code(*lc[ch])
+    bw.put_code(*lc[256])
+    nbits = 8 * len(bw.out) + bw.n
+    dyn = np.unpackbits(np.frombuffer(bytes(bw.out) + bytes([bw.acc & 0xFF]), dtype=np.uint8),
+                        bitorder="little")[:nbits]
+    allbits = np.concatenate([_fixed_bits(a, False), dyn, _fixed_bits(b, True)])
+    s = np.packbits(allbits, bitorder="little").tobytes()
+    want = oracle.inflate(s)
+    assert want == a + payload + b
+    out, path, ms = _gpu_inflate(ctx, s, len(want), reps=1)
+    assert out == want
+    assert path == 5

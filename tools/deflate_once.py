@@ -12,7 +12,7 @@ kind = sys.argv[1] if len(sys.argv) > 1 else "repeat"
 n = (int(sys.argv[2]) if len(sys.argv) > 2 else 256) << 20
 lvl = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 inf = len(sys.argv) > 4 and sys.argv[4] == "1"
-ctx = dmx.Context()
+ctx = dmx.Context(segment_bytes=int(os.environ.get("DMX_SEG", "32768")))
 host = torch.empty(n, dtype=torch.uint8).pin_memory()
 dmx.corpus_into(kind, n, host.data_ptr())
 d_in = host.cuda()
