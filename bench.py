@@ -400,6 +400,51 @@ def c3_record(torch, ctx, dev, stream):
     return res
 
 
+FOREIGN_REF_MBPS = {"text": 35.1, "mixed": 48.2, "zeros": 227.6}  # reference inflate of zlib-1, 1 GiB
+
+
+def foreign_record(torch, ctx, dev, stream, kind="text", nbytes=GiB, pieces=8):
+    """A third-party stream at BASELINE scale on path 5: zlib level 1 of
+    the 1 GiB corpus, compressed on `pieces` host threads (zlib releases the GIL) as one raw
+    stream -- every piece primed with the previous 32 KiB as its dictionary, joined at sync
+    flushes (an empty stored block each) -- so matches cross the joins as in one zlib run.  The
+    output's SHA-256 is checked against SURVEY Appendix B (tests/test_gpu_foreign_1GiB.py runs
+    the whole-stream zlib-1 of text, mixed and zeros)."""
+    from concurrent.futures import ThreadPoolExecutor
+    data = dmx.corpus(kind, nbytes)
+    step = -(-nbytes // pieces)
+
+    def comp(i):
+        b = i * step
+        z = zlib.compressobj(1, zlib.DEFLATED, -15, zdict=data[max(b - 32768, 0):b]) if b else \
+            zlib.compressobj(1, zlib.DEFLATED, -15)
+        out = z.compress(data[b:b + step])
+        return out + (z.flush() if b + step >= nbytes else z.flush(zlib.Z_SYNC_FLUSH))
+
+    with ThreadPoolExecutor(pieces) as ex:
+        s = b"".join(ex.map(comp, range(pieces)))
+    sha = hashlib.sha256(data).hexdigest()
+    del data
+    d_s = torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev)
+    out = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
+    ms = []
+    for it in range(4):
+        olen = ctx.inflate_device(d_s.data_ptr(), len(s), out.data_ptr(), nbytes + 64, stream=stream.cuda_stream)
+        if it >= 1:
+            ms.append(ctx.stats().ms_device_total)
+    path = int(ctx.stats().path)
+    ok = olen == nbytes and hashlib.sha256(out[:nbytes].cpu().numpy().tobytes()).hexdigest() == sha
+    med = sorted(ms)[len(ms) // 2]
+    ref = FOREIGN_REF_MBPS.get(kind)
+    return {"corpus": kind, "bytes": nbytes, "stream": f"zlib level 1, {pieces} pieces joined at sync flushes, "
+                                                       "each primed with the previous 32 KiB",
+            "stream_bytes": len(s), "inflate_ms": round(med, 3), "inflate_GBps": round(nbytes / (med * 1e-3) / 1e9, 3),
+            "path": path, "sha256_ok": ok,
+            "roofline_frac": round((nbytes + len(s)) / (med * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
+            "ref_inflate_MBps_survey6": ref,
+            "vs_reference_1core": round(nbytes / (med * 1e-3) / 1e6 / ref, 1) if ref else None}
+
+
 def main():
     a = parse()
     import torch
@@ -562,6 +607,7 @@ def main():
                                  "zlib6_ratio_32KiB_chunks_16MiB": zlib_ratio("text", 6, chunk=32768)})
         res["c3_inflate"] = c3_record(torch, ctx, dev, stream)
         res["c4_64k"] = c4_record(run, dev, a.level, 3)
+        res["foreign_1GiB"] = foreign_record(torch, ctx, dev, stream)
     if rank == 0:
         if world == 1 and not a.no_cpu_baseline:
             try:
