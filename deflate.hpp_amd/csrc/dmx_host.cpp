@@ -1188,9 +1188,13 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
     }
     end_timing(c, st);
     if (c->diag & DIAG_FB)
-        std::fprintf(stderr, "dmx serial: cycles decode %llu walk %llu offsets %llu writes %llu flush %llu, steps %llu\n",
+        std::fprintf(stderr, "dmx serial: cycles %llu %llu %llu %llu %llu, regions %llu; walk phases %llu %llu %llu %llu %llu, "
+                     "rounds %llu (k_inflate_serial_wg: doubling, members+scan+cuts, parallel writes, wave-0 copies + "
+                     "flush, decode + walks; walks: first pass, rounds, output sums, writes, dependent copies)\n",
                      (unsigned long long)r.cycles[0], (unsigned long long)r.cycles[1], (unsigned long long)r.cycles[2],
-                     (unsigned long long)r.cycles[3], (unsigned long long)r.cycles[4], (unsigned long long)r.cycles[5]);
+                     (unsigned long long)r.cycles[3], (unsigned long long)r.cycles[4], (unsigned long long)r.cycles[5],
+                     (unsigned long long)r.cycles[6], (unsigned long long)r.cycles[7], (unsigned long long)r.cycles[8],
+                     (unsigned long long)r.cycles[9], (unsigned long long)r.cycles[10], (unsigned long long)r.cycles[11]);
     *total_out = r.total;
     c->last_end = r.end_byte;
     c->stats.out_bytes = r.total;

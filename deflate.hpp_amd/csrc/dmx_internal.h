@@ -99,7 +99,7 @@ struct InflateResult {
     uint32_t fin_index;
     uint64_t exotic;  // candidates flagged SEGF_EXOTIC by the pass
     uint64_t end_byte;  // status 0: the stream byte just past the final block (relative to the stream)
-    uint64_t cycles[6];  // serial decoder (DMX_FB_DEBUG): s_memtime per phase -- decode, walk,
+    uint64_t cycles[12];  // serial decoder (DMX_FB_DEBUG): s_memtime per phase -- decode, walk,
                          // offsets, literals + copies, flush + refill, steps
 };
 

@@ -1049,10 +1049,13 @@ __device__ __noinline__ void sk_slow_dist(const LdsTables* T, uint32_t dv, uint3
     uint32_t ds, dl;
     *de = slow_decode(T->dm, T->dsorted, dv & 0x7FFF, LUT_D + 1, &ds, &dl) ? dist_entry(ds, dl) : 0u;
 }
+// LIN: `ring` is a plain array of stream words (sw_walk's staging), not the FB_RW ring
+template <bool LIN = false>
 __device__ __forceinline__ uint32_t sk_token(const LdsU32* ring, const LdsTables* T, uint32_t b, uint32_t* L,
                                              uint32_t* d) {
     const uint32_t wi = b >> 5, sh = b & 31;
-    const uint32_t x0 = ring[wi % FB_RW], x1 = ring[(wi + 1) % FB_RW], x2 = ring[(wi + 2) % FB_RW];
+    const uint32_t x0 = ring[LIN ? wi : wi % FB_RW], x1 = ring[LIN ? wi + 1 : (wi + 1) % FB_RW],
+                   x2 = ring[LIN ? wi + 2 : (wi + 2) % FB_RW];
     const uint32_t v = __builtin_amdgcn_alignbit(x1, x0, sh);
     const uint64_t W = (uint64_t)v | ((uint64_t)__builtin_amdgcn_alignbit(x2, x1, sh) << 32);
     uint32_t e = T->llut[v & ((1u << LUT_L) - 1)];
@@ -1069,6 +1072,37 @@ __device__ __forceinline__ uint32_t sk_token(const LdsU32* ring, const LdsTables
     }
     const uint32_t dl = de & 15, dx = (de >> 6) & 15;
     const uint32_t lenv = (e >> 16) + ((v >> cl) & ((1u << ex) - 1u));  // literal byte or match length
+    *L = ty == 1 ? 0u : lenv;
+    *d = ism ? (de >> 16) + ((dv >> dl) & ((1u << dx) - 1u)) : 0u;
+    const uint32_t kind = !e || (ism && !de) ? SK_BAD : ty == 0 ? SK_LIT : ty == 1 ? SK_EOB : SK_MATCH;
+    const uint32_t tl = ism ? q + dl + dx : cl;
+    return tl | (kind << 8);
+}
+
+// sk_token for sw_walk: stream words in a plain array, wider primary tables (SW_LL / SW_LD bits,
+// built per walk region) -- a walk from a wrong offset meets long codes often, and every lane of
+// the wave then waits for the slow path
+constexpr int SW_LL = 11, SW_LD = 10;
+__device__ __forceinline__ uint32_t sw_wtok(const LdsU32* win, const LdsTables* T, const LdsU32* llut,
+                                            const LdsU32* dlut, uint32_t b, uint32_t* L, uint32_t* d) {
+    const uint32_t wi = b >> 5, sh = b & 31;
+    const uint32_t x0 = win[wi], x1 = win[wi + 1], x2 = win[wi + 2];
+    const uint32_t v = __builtin_amdgcn_alignbit(x1, x0, sh);
+    const uint64_t W = (uint64_t)v | ((uint64_t)__builtin_amdgcn_alignbit(x2, x1, sh) << 32);
+    uint32_t e = llut[v & ((1u << SW_LL) - 1)];
+    if (__ballot(e == 0)) {
+        if (!e) sk_slow_lit(T, v, &e);
+    }
+    const uint32_t cl = e & 15, ty = (e >> 4) & 3, ex = (e >> 6) & 15;
+    const uint32_t q = cl + ex;
+    const uint32_t dv = (uint32_t)(W >> q);
+    const bool ism = ty == 2;
+    uint32_t de = dlut[dv & ((1u << SW_LD) - 1)];
+    if (__ballot(ism && de == 0)) {
+        if (ism && !de) sk_slow_dist(T, dv, &de);
+    }
+    const uint32_t dl = de & 15, dx = (de >> 6) & 15;
+    const uint32_t lenv = (e >> 16) + ((v >> cl) & ((1u << ex) - 1u));
     *L = ty == 1 ? 0u : lenv;
     *d = ism ? (de >> 16) + ((dv >> dl) & ((1u << dx) - 1u)) : 0u;
     const uint32_t kind = !e || (ism && !de) ? SK_BAD : ty == 0 ? SK_LIT : ty == 1 ? SK_EOB : SK_MATCH;
@@ -1338,7 +1372,764 @@ __global__ __launch_bounds__(IF_NT) void k_inflate_serial(InflateArgs A, int cou
         res->fin_index = 0;
         res->end_byte = fin ? end_byte - A.misalign : 0;
     }
-    if (threadIdx.x < 6) res->cycles[threadIdx.x] = cyc[threadIdx.x];
+    if (threadIdx.x < 12) res->cycles[threadIdx.x] = threadIdx.x < 6 ? cyc[threadIdx.x] : 0ull;
+}
+
+// ---------------------------------------------------------------------------------------
+// Workgroup serial decoder (k_inflate_serial_wg, the default serial path): the same
+// realDecompress (inflate.hpp:277-322) and output ring as k_inflate_serial, but each Huffman
+// block is decoded 2048 bit offsets at a time by 1024 threads (16 wavefronts):
+//   1. every thread decodes the token that would start at two of the region's bit offsets
+//      (sk_token) and its successor offset J0 (end-of-block / bad codes end a chain);
+//   2. pointer doubling, J_k = J_{k-1} o J_{k-1}, up to the chain length the block's shortest
+//      lit/len code allows (one barrier per level);
+//   3. the chain's i-th member is J_{b_m} o .. o J_{b_0}(0) for the bits of i -- every thread
+//      finds two members with no barrier in between, and the members come out in order;
+//   4. one workgroup scan of their output lengths gives each token's output offset; the region
+//      is cut at 16 KiB of output, at a distance reaching before the stream start (the
+//      reference copies nothing there: the token is skipped; an error in piece mode) and at an
+//      over-read (the reference's error, nothing of the region written);
+//   5. literals and matches whose source lies before the region go to the ring in parallel
+//      (short ones one thread each, long ones one wave each), then wave 0 copies the matches
+//      that read the region's own output, in token order.
+// Headers, stored blocks and the block loop stay on wave 0 (inflate_blocks); the other waves
+// wait at the workgroup barrier and join every Huffman block (decode_block below).
+// ---------------------------------------------------------------------------------------
+#ifndef DMX_SW_DIAG
+#define DMX_SW_DIAG 0  // developer aid: the cycle slots 0-3 count walk attempts / successes / rounds / failures
+#endif
+constexpr int SW_NT = 1024;
+constexpr uint32_t SW_R = 2048;        // bit offsets per region
+constexpr uint32_t SW_LMAX = 11;       // doubling levels for 2048 one-bit tokens
+constexpr uint32_t SW_OUTCAP = 16384;  // output bytes per region (the 64 KiB ring: window + unflushed)
+enum : uint32_t { SW_CMD_DECODE = 1, SW_CMD_EXIT = 2 };
+
+// walk regions (sw_walk): one 32-bit slice of the stream per thread
+constexpr uint32_t SW_WS = 64;                 // bits per slice
+constexpr uint32_t SW_NS = 512;                // slices (threads that walk)
+constexpr uint32_t SW_RW = SW_NS * SW_WS;      // 32768 bits per walk region
+constexpr uint32_t SW_WW = SW_RW / 32 + 4;     // staged stream words
+constexpr uint32_t SW_KMAX = 24;               // synchronisation rounds before the doubling fallback
+constexpr uint32_t SW_WARM = 128;              // bits each slice's first walk starts before it
+constexpr uint32_t SW_TERM = 1u << 31, SW_BADT = 1u << 30;
+struct SwWalk {
+    uint32_t win[SW_WW];                // the region's stream words
+    uint32_t ex[2][SW_NS];              // each slice's exit (first token start past it; SW_TERM: a
+                                        // path that ended in the slice, SW_BADT: at a bad code)
+    uint16_t R[SW_OUTCAP];              // dependent output bytes: the byte they copy, + 32768
+    uint32_t llut[1 << SW_LL];          // the block's codes, wider primary tables
+    uint32_t dlut[1 << SW_LD];
+    uint32_t cutq, cutxo, term;
+};
+
+struct SwSmem {
+    uint8_t oring[65536];
+    uint32_t inring[FB_RW];
+    Tables T;
+    union {
+        struct {  // a doubling region
+            uint32_t E[SW_R];               // tl | kind << 6 | L << 8 | (d & 0x7FFF) << 17
+            uint16_t J[SW_LMAX][SW_R + 2];  // successors after 2^k tokens; SW_R = out of the chain
+            uint16_t node[SW_R + 2];        // the chain's members in order
+            uint32_t X[SW_R];               // their output offsets in the region
+        };
+        SwWalk W;  // a walk region
+    };
+    uint32_t DB[SW_R / 32];             // members whose match reads the region's own output
+    uint16_t DL[SW_R];                  // those members, in order
+    uint32_t PB[SW_OUTCAP / 32];        // the output bytes of those matches
+    uint32_t wsum[SW_NT / 64];
+    uint32_t more[3];
+    uint8_t flag[128];                  // (k_inflate_serial's sk_loop marks; unused here)
+    uint64_t p, pos, flushed, rb;
+    uint32_t cmd, err, nmem, cut, cutx, cutov;
+    uint64_t cyc[12];  // phase cycles (DMX_FB_DEBUG): sw_block's 6, then sw_walk's 5 and its rounds
+};
+
+__device__ __forceinline__ uint32_t sw_len(uint32_t e) {
+    const uint32_t k = (e >> 6) & 3;
+    return k == SK_LIT ? 1u : k == SK_MATCH ? (e >> 8) & 0x1FFu : 0u;
+}
+__device__ __forceinline__ uint32_t sw_dist(uint32_t e) {
+    const uint32_t d = e >> 17;
+    return d ? d : 32768u;
+}
+
+// short copy by one thread, source wholly before the destination (d >= L): reads first, then
+// exact-size stores (neighbouring tokens store beside it); byte loop across the ring's end
+__device__ __forceinline__ void sw_copy_short(LdsU8* ring, uint32_t dst, uint32_t d, uint32_t L) {
+    const uint32_t s = (dst - d) & 0xFFFFu, o = dst & 0xFFFFu;
+    if (s + 32 > 65536u || o + 32 > 65536u) {
+        for (uint32_t i = 0; i < L; i++) ring[(o + i) & 0xFFFFu] = ring[(s + i) & 0xFFFFu];
+        return;
+    }
+    typedef __attribute__((address_space(3))) uint64_t __attribute__((aligned(1))) LdsU64u;
+    typedef __attribute__((address_space(3))) uint32_t __attribute__((aligned(1))) LdsU32u;
+    typedef __attribute__((address_space(3))) uint16_t __attribute__((aligned(1))) LdsU16u;
+    uint64_t v[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) v[k] = 8 * k < L ? *reinterpret_cast<LdsU64u*>(ring + s + 8 * k) : 0ull;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t b = 8 * k;
+        if (b + 8 <= L) {
+            *reinterpret_cast<LdsU64u*>(ring + o + b) = v[k];
+        } else if (b < L) {
+            uint32_t r = L - b, q = o + b;
+            uint64_t x = v[k];
+            if (r & 4) {
+                *reinterpret_cast<LdsU32u*>(ring + q) = (uint32_t)x;
+                q += 4;
+                x >>= 32;
+            }
+            if (r & 2) {
+                *reinterpret_cast<LdsU16u*>(ring + q) = (uint16_t)x;
+                q += 2;
+                x >>= 16;
+            }
+            if (r & 1) ring[q] = (uint8_t)x;
+        }
+    }
+}
+
+// Wave 0, one batch of up to 64 matches that read their region's own output (lane: have, output
+// offset xo in the region, length ln, distance d), in output order: those whose source (the first
+// period of a periodic one) holds no such match's output (PB) copy first, side by side; then the
+// rest, one after the other.
+__device__ __forceinline__ void sw_deps(LdsU8* ring, const uint32_t* PB, uint32_t pos, bool have, uint32_t xo,
+                                        uint32_t ln, uint32_t d) {
+    const uint32_t lane = lane_id();
+    bool chained = false;
+    const uint32_t a0 = xo > d ? xo - d : 0u, a1 = d >= ln ? xo - d + ln : xo;
+    for (uint32_t b = a0; have && b < a1 && !chained;) {
+        const uint32_t n = min(32u - (b & 31), a1 - b);
+        chained = (PB[b >> 5] >> (b & 31)) & (n == 32 ? ~0u : ((1u << n) - 1u));
+        b += n;
+    }
+    const bool freec = have && !chained;
+    const bool lanec = freec && ln <= 32 && d >= ln;  // one lane copies it
+    if (lanec) sw_copy_short(ring, pos + xo, d, ln);
+    // then the long or periodic free ones, then the chained ones in order
+    for (int pass = 0; pass < 2; pass++) {
+        for (uint64_t q = __ballot(pass ? have && chained : freec && !lanec); q; q &= q - 1) {
+            const int k = __builtin_ctzll(q);
+            const uint32_t ko = pos + (uint32_t)__builtin_amdgcn_readlane((int)xo, k);
+            const uint32_t kd = (uint32_t)__builtin_amdgcn_readlane((int)d, k);
+            const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)ln, k);
+            if (kd >= kl) {
+                for (uint32_t b = lane; b < kl; b += 64) ring[(ko + b) & 0xFFFFu] = ring[(ko - kd + b) & 0xFFFFu];
+            } else {  // periodic: byte b repeats byte b mod d of the first period
+                for (uint32_t b = lane; b < kl; b += 64) ring[(ko + b) & 0xFFFFu] = ring[(ko - kd + b % kd) & 0xFFFFu];
+            }
+            if (pass) wave_sync();
+        }
+        wave_sync();
+    }
+}
+
+// One walk region of SW_RW bits from stream bit p (output position pos >= 32 KiB, the region
+// inside the stream): thread t walks the tokens of its 32-bit slice from the slice start (thread
+// 0 from p); then, in rounds, every thread whose entry -- its predecessor's exit -- differs from
+// the one it walked from walks again from there until its path meets a token start of its old
+// path (Huffman codes resynchronise within a few tokens: from there on the paths are the same).
+// When no exit changes, every slice holds the stream's true tokens.  A second walk sums each
+// slice's output (workgroup scan: output offsets), a third writes literals and the matches whose
+// source precedes the region and lists the others for wave 0 (sw_deps), in output order.
+// Returns 0 (region done: *np, *ntot), 1 (the block's end of block was in it: *np after it) or
+// 2 (not converged in SW_KMAX rounds, a bad code on the path, too many dependent matches: the
+// caller decodes the same span as doubling regions, which also rewrite anything written here).
+__device__ __attribute__((noinline)) uint32_t sw_walk(SwSmem& S, GlbU32* w, uint64_t nwords, uint64_t end_bytes,
+                                                      uint64_t p, uint64_t pos, uint64_t* np, uint32_t* ntot,
+                                                      uint32_t* rounds, bool timed, uint32_t warm, uint32_t kmax) {
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint64_t tc = timed ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int k) {  // (thread 0 adds the phase to S.cyc[6 + k])
+        if (timed && t == 0) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            S.cyc[6 + k] += t1 - tc;
+            tc = t1;
+        }
+    };
+    SwWalk& W = S.W;
+    LdsU8* const ring = (LdsU8*)S.oring;
+    const LdsTables* const T = (const LdsTables*)&S.T;
+    const LdsU32* const win = (const LdsU32*)W.win;
+    const uint64_t w0 = p >> 5;
+    const uint32_t q0 = (uint32_t)(p & 31);
+    for (uint32_t i = t; i < SW_WW; i += SW_NT) {
+        uint32_t v = 0;
+        if (w0 + i < nwords) {
+            v = w[w0 + i];
+            const uint64_t lm = end_bytes - 4 * (w0 + i);
+            if (lm < 4) v &= (1u << (8 * lm)) - 1u;
+        }
+        W.win[i] = v;
+    }
+    if (t == 0) {
+        W.cutq = ~0u;
+        W.term = ~0u;
+        S.more[0] = 0;
+    }
+    if (t < SW_OUTCAP / 32) S.PB[t] = 0;
+    fill_lut32_wg<SW_LL, false>(W.llut, S.T.lm, S.T.lsorted, (int)t, SW_NT);
+    fill_lut32_wg<SW_LD, true>(W.dlut, S.T.dm, S.T.dsorted, (int)t, SW_NT);
+    const LdsU32* const wl = (const LdsU32*)W.llut;
+    const LdsU32* const wd = (const LdsU32*)W.dlut;
+    __syncthreads();
+    const bool walker = t < SW_NS;
+    const uint32_t lo = SW_WS * t, hi = walker ? lo + SW_WS : lo;
+    uint32_t Lv, dv;
+    // the path from en through the slice: bw = its token starts, ex = its exit
+    // (the first walk starts SW_WARM bits early: by its slice's start it has most likely met
+    // the stream's true tokens, so the rounds below seldom have anything to do)
+    uint32_t en = ~0u, ex = ~0u;
+    uint64_t bw = 0;
+    {
+        uint32_t q = t ? (lo >= warm ? lo - warm : 0u) : q0;
+        while (q < hi) {
+            if (q >= lo) {
+                if (en == ~0u) en = q;
+                bw |= 1ull << (q - lo);
+            }
+            const uint32_t info = sw_wtok(win, T, wl, wd, q, &Lv, &dv);
+            const uint32_t kind = info >> 8;
+            q += info & 255;
+            if (kind >= SK_EOB) {
+                ex = q | SW_TERM | (kind == SK_BAD ? SW_BADT : 0u);
+                break;
+            }
+        }
+        if (ex == ~0u) ex = q;
+        if (en == ~0u) {
+            if (ex & SW_TERM) {  // ended before the slice: (its mark is not the slice's) walk from lo
+                ex = ~0u;
+                bw = 0;
+                en = lo;
+                for (q = lo; q < hi;) {
+                    bw |= 1ull << (q - lo);
+                    const uint32_t info = sw_wtok(win, T, wl, wd, q, &Lv, &dv);
+                    const uint32_t kind = info >> 8;
+                    q += info & 255;
+                    if (kind >= SK_EOB) {
+                        ex = q | SW_TERM | (kind == SK_BAD ? SW_BADT : 0u);
+                        break;
+                    }
+                }
+                if (ex == ~0u) ex = q;
+            } else {
+                en = q;  // (a token crossed the whole slice)
+            }
+        }
+    }
+    if (walker) W.ex[0][t] = ex;
+    __syncthreads();
+    stamp(0);
+    uint32_t cur = 0;
+    bool conv = false;
+    for (uint32_t k = 0; k < kmax; k++) {
+        if (t == 0) S.more[(k + 1) % 3] = 0;
+        bool ch = false;
+        if (t > 0 && walker) {
+            const uint32_t pe = W.ex[cur][t - 1];
+            uint32_t nex = ex;
+            // (a predecessor's path that ends -- an end of block or a bad code -- leaves this
+            // slice as it is: on the true path that is the block's end, and the slice is unused)
+            if (!(pe & SW_TERM) && pe != en) {
+                uint32_t q = pe;
+                uint64_t nb = 0;
+                nex = ~0u;
+                while (q < hi) {
+                    if ((bw >> (q - lo)) & 1u) {  // met the old path: the same tokens from here
+                        nb |= bw & (~0ull << (q - lo));
+                        nex = ex;
+                        break;
+                    }
+                    nb |= 1ull << (q - lo);
+                    const uint32_t info = sw_wtok(win, T, wl, wd, q, &Lv, &dv);
+                    const uint32_t kind = info >> 8;
+                    q += info & 255;
+                    if (kind >= SK_EOB) {
+                        nex = q | SW_TERM | (kind == SK_BAD ? SW_BADT : 0u);
+                        break;
+                    }
+                }
+                if (nex == ~0u) nex = q;
+                en = pe;
+                bw = nb;
+            }
+            ch = nex != ex;
+            ex = nex;
+        }
+        if (walker) W.ex[cur ^ 1][t] = ex;
+        if (ch) S.more[k % 3] = 1;
+        __syncthreads();
+        cur ^= 1;
+        if (!S.more[k % 3]) {
+            conv = true;
+            *rounds = k + 1;
+            break;
+        }
+    }
+    stamp(1);
+    if (!conv) {
+        *rounds = 1000u;
+        return 2;
+    }
+    if (timed && t == 0) S.cyc[11] += *rounds;
+    // the slice whose path ends the block: the first with SW_TERM (every slice before it holds
+    // the true path, each starting at its predecessor's exit)
+    if (walker && (ex & SW_TERM)) atomicMin(&W.term, t);
+    __syncthreads();
+    const uint32_t tterm = W.term;
+    if (tterm != ~0u && (W.ex[cur][tterm] & SW_BADT)) return 2;  // (the doubling region reports it)
+    const bool live = walker && t <= tterm;
+    // output bytes of each slice
+    uint32_t ol = 0;
+    if (live)
+        for (uint32_t q = en; q < hi;) {
+            const uint32_t info = sw_wtok(win, T, wl, wd, q, &Lv, &dv);
+            const uint32_t kind = info >> 8;
+            q += info & 255;
+            if (kind >= SK_EOB) break;
+            ol += kind == SK_LIT ? 1u : (Lv && dv) ? Lv : 0u;
+        }
+    const uint32_t incl = wave_incl_scan(ol);
+    if (lane == 63) S.wsum[wv] = incl;
+    __syncthreads();
+    const uint32_t wpre = wave_incl_scan(lane < SW_NT / 64 ? S.wsum[lane] : 0u);
+    const uint32_t base = (wv ? (uint32_t)__builtin_amdgcn_readlane((int)wpre, (int)wv - 1) : 0u) + incl - ol;
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)wpre, SW_NT / 64 - 1);
+    stamp(2);
+    if (t == 0) S.more[0] = 0;  // (for the dependent-byte rounds; the last read of it is behind a barrier)
+    // writes
+    if (live && base <= SW_OUTCAP) {  // (base == cap: the crossing token may be this slice's first)
+        uint32_t xo = base;
+        for (uint32_t q = en; q < hi;) {
+            const uint32_t info = sw_wtok(win, T, wl, wd, q, &Lv, &dv);
+            const uint32_t kind = info >> 8;
+            if (kind >= SK_EOB) break;
+            const uint32_t ln = kind == SK_LIT ? 1u : (Lv && dv) ? Lv : 0u;
+            if (xo + ln > SW_OUTCAP) {  // (one token crosses the cap)
+                W.cutq = q;
+                W.cutxo = xo;
+                break;
+            }
+            const uint32_t dst = (uint32_t)pos + xo;
+            if (kind == SK_LIT) {
+                ring[dst & 0xFFFFu] = (uint8_t)Lv;
+            } else if (ln) {
+                if (dv >= xo + ln) {  // the source precedes the region
+                    for (uint32_t b = 0; b < ln; b += 32) sw_copy_short(ring, dst + b, dv, min(32u, ln - b));
+                } else {  // reads the region's own output: resolved below, byte by byte
+                    for (uint32_t b = xo; b < xo + ln; b++) W.R[b] = (uint16_t)(b + 32768u - dv);
+                    for (uint32_t b = xo; b < xo + ln;) {
+                        const uint32_t n = min(32u - (b & 31), xo + ln - b);
+                        atomicOr(&S.PB[b >> 5], (n == 32 ? ~0u : ((1u << n) - 1u)) << (b & 31));
+                        b += n;
+                    }
+                }
+            }
+            xo += ln;
+            q += info & 255;
+        }
+    }
+    __syncthreads();
+    stamp(3);
+    // dependent bytes: R[b] = R[R[b]] until every R[b] is a byte no dependent match writes (a
+    // literal, a match reading before the region, or a byte before the region): the
+    // reference's byte-serial copy out[b] = out[b - d], in log2(chain length) rounds
+    const uint32_t cutq = W.cutq;
+    const uint32_t tot = cutq != ~0u ? W.cutxo : total;
+    auto dep_byte = [&](int v) -> bool { return v >= 0 && ((S.PB[(uint32_t)v >> 5] >> ((uint32_t)v & 31)) & 1u); };
+    for (uint32_t r = 0;; r++) {
+        if (t == 0) S.more[(r + 1) % 3] = 0;
+        bool more = false;
+        for (uint32_t b = t; b < tot; b += SW_NT) {
+            if (!dep_byte((int)b)) continue;
+            const int v = (int)W.R[b] - 32768;
+            if (!dep_byte(v)) continue;
+            const uint32_t w2 = W.R[v];
+            W.R[b] = (uint16_t)w2;
+            more |= dep_byte((int)w2 - 32768);
+        }
+        if (more) S.more[r % 3] = 1;
+        __syncthreads();
+        if (!S.more[r % 3]) break;
+    }
+    for (uint32_t b = t; b < tot; b += SW_NT)
+        if (dep_byte((int)b)) ring[((uint32_t)pos + b) & 0xFFFFu] = ring[((uint32_t)pos + (uint32_t)W.R[b] - 32768u) & 0xFFFFu];
+    stamp(4);
+    uint32_t r = 0;
+    if (cutq != ~0u) {
+        *np = w0 * 32 + cutq;
+        *ntot = W.cutxo;
+    } else if (tterm != ~0u) {
+        *np = w0 * 32 + (W.ex[cur][tterm] & ~(SW_TERM | SW_BADT));
+        *ntot = total;
+        r = 1;
+    } else {
+        *np = w0 * 32 + W.ex[cur][SW_NS - 1];
+        *ntot = total;
+    }
+    __syncthreads();
+    return r;
+}
+
+// One Huffman block by the whole workgroup, from S.p / S.pos / S.flushed / S.rb; results back in
+// S (err, p after the block, pos, flushed, rb), published by the final barrier.
+__device__ __attribute__((noinline)) void sw_block(SwSmem& S, GlbU32* w, uint64_t nwords, uint64_t end_bytes,
+                                                   GlbU8* out, uint64_t cap, bool piece, bool timed, uint32_t walk) {
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint64_t endb = end_bytes * 8;
+    LdsU8* const ring = (LdsU8*)S.oring;
+    const LdsTables* const T = (const LdsTables*)&S.T;
+    // the shortest lit/len code bounds the chain length, hence the doubling levels
+    uint32_t minb = 0;
+    for (uint32_t k = 1; k < 16 && !minb; k++)
+        if (S.T.lm.cnt[k]) minb = k;
+    if (!minb) minb = 1;
+    const uint32_t maxn = (SW_R - 1) / minb + 1;                        // chain members at most
+    const uint32_t L = maxn <= 1 ? 1u : 32u - (uint32_t)__clz(maxn - 1);  // 2^L >= maxn
+    const uint32_t lim = min(1u << L, SW_R);
+    uint64_t p = S.p, pos = S.pos, flushed = S.flushed, rb = S.rb;
+    uint32_t err = 0;
+    uint64_t tc = timed ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t cy[6] = {0, 0, 0, 0, 0, 0};
+    auto stamp = [&](int k) {
+        if (timed && (!DMX_SW_DIAG || k >= 4)) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            cy[k] += t1 - tc;
+            tc = t1;
+        }
+    };
+    auto flush_if = [&]() {
+        if (pos - flushed >= 32768) {
+            const uint64_t hi = pos < cap ? pos : cap;
+            for (uint64_t i = flushed + t; i < hi; i += SW_NT) out[i] = ring[i & 0xFFFF];
+            flushed = pos;
+        }
+    };
+    uint32_t wait = 0, backoff = 8;  // doubling regions before the next walk attempt
+    const bool fixed = S.T.fixed_loaded != 0;
+    for (;;) {
+        // walk regions where they apply: past the first 32 KiB of output (no distance can reach
+        // before the stream start) and SW_RW + 64 bits before the stream end (no over-read)
+        // (dynamic-code blocks only: walks through fixed-code literal runs seldom resynchronise)
+        if (walk && !fixed && !wait && pos >= 32768 && p + SW_RW + 64 <= endb) {
+            uint64_t np = 0;
+            uint32_t nt = 0, rounds = 0;
+            const uint32_t r = sw_walk(S, w, nwords, end_bytes, p, pos, &np, &nt, &rounds, timed, walk & 0xFFFFu,
+                                       walk >> 16);
+            stamp(4);
+#ifdef DMX_SW_TRACE
+            if (t == 0 && pos + 40000 > DMX_SW_TRACE && pos < DMX_SW_TRACE + 1000)
+                printf("walk p %llu pos %llu -> r %u np %llu nt %u rounds %u\n", (unsigned long long)p,
+                       (unsigned long long)pos, r, (unsigned long long)np, nt, rounds);
+#endif
+#if DMX_SW_DIAG
+            cy[0] += 1;                           // attempts
+            cy[1] += r != 2;                      // successes
+            cy[2] += rounds < 1000 ? rounds : 0;  // rounds of the converged ones
+            cy[3] += rounds >= 1000;              // not converged
+#endif
+            if (r != 2) {
+                pos += nt;
+                p = np;
+                flush_if();
+                cy[5]++;
+                backoff = 8;
+                if (r == 1) break;
+                continue;
+            }
+            // no convergence (long runs of codes that do not resynchronise, e.g. literal-only
+            // fixed-code data): doubling regions for a while, longer after each failure
+            wait = backoff;
+            backoff = min(backoff * 2, 512u);
+        }
+        if (wait) wait--;
+        const uint64_t w0 = p >> 5;
+        if (w0 < rb || w0 + SW_R / 32 + 4 > rb + FB_RW) {  // (uniform: every thread holds p, rb)
+            rb = w0;
+            for (uint64_t i = w0 + t; i < w0 + FB_RW; i += SW_NT) {
+                uint32_t v = 0;
+                if (i < nwords) {
+                    v = w[i];
+                    const uint64_t lm = end_bytes - 4 * i;
+                    if (lm < 4) v &= (1u << (8 * lm)) - 1u;
+                }
+                S.inring[i % FB_RW] = v;
+            }
+            __syncthreads();
+        }
+        if (t == 0) {
+            S.cut = S.cutx = S.cutov = ~0u;
+        }
+        if (t < L) S.J[t][SW_R] = (uint16_t)SW_R;
+        if (t < SW_R / 32) S.DB[t] = 0;
+        if (t < SW_OUTCAP / 32) S.PB[t] = 0;
+        // 1. tokens at every offset
+#pragma unroll
+        for (uint32_t h = 0; h < 2; h++) {
+            const uint32_t o = t + h * SW_NT;
+            uint32_t Lv, dv;
+            const uint32_t info = sk_token((const LdsU32*)S.inring, T, (uint32_t)p + o, &Lv, &dv);
+            const uint32_t kind = info >> 8, tl = info & 255;
+            uint32_t e = min(tl, 63u) | (kind << 6);
+            if (kind == SK_LIT) e |= Lv << 8;
+            else if (kind == SK_MATCH && Lv && dv) e |= (Lv << 8) | ((dv & 0x7FFFu) << 17);
+            S.E[o] = e;
+            S.J[0][o] = (uint16_t)(kind <= SK_MATCH ? min(o + tl, SW_R) : SW_R);
+        }
+        __syncthreads();
+        stamp(4);
+        // 2. doubling
+        for (uint32_t k = 1; k < L; k++) {
+            const uint32_t a = S.J[k - 1][S.J[k - 1][t]], b = S.J[k - 1][S.J[k - 1][t + SW_NT]];
+            S.J[k][t] = (uint16_t)a;
+            S.J[k][t + SW_NT] = (uint16_t)b;
+            __syncthreads();
+        }
+        stamp(0);
+        // 3. members 2t, 2t + 1
+        uint32_t x[2];
+#pragma unroll
+        for (uint32_t h = 0; h < 2; h++) {
+            const uint32_t i = 2 * t + h;
+            uint32_t v = SW_R;
+            if (i < lim) {
+                v = 0;
+                for (uint32_t k = 0; k < L; k++) {
+                    const uint32_t nv = S.J[k][v];
+                    v = ((i >> k) & 1u) ? nv : v;
+                }
+            }
+            x[h] = v;
+            S.node[i] = (uint16_t)v;
+        }
+        if (t == 0) S.node[SW_R] = (uint16_t)SW_R;
+        // 4. output offsets
+        const uint32_t e0 = x[0] < SW_R ? S.E[x[0]] : 0u, e1 = x[1] < SW_R ? S.E[x[1]] : 0u;
+        const uint32_t l0 = x[0] < SW_R ? sw_len(e0) : 0u, l1 = x[1] < SW_R ? sw_len(e1) : 0u;
+        const uint32_t incl = wave_incl_scan(l0 + l1);
+        if (lane == 63) S.wsum[wv] = incl;
+        __syncthreads();
+        // (the last member: the one whose successor is out of the chain)
+        if (x[0] < SW_R && x[1] == SW_R) S.nmem = 2 * t + 1;
+        if (x[1] < SW_R && (2 * t + 2 >= lim || S.node[2 * t + 2] == SW_R)) S.nmem = 2 * t + 2;
+        const uint32_t wpre = wave_incl_scan(lane < SW_NT / 64 ? S.wsum[lane] : 0u);
+        const uint32_t base = wv ? (uint32_t)__builtin_amdgcn_readlane((int)wpre, (int)wv - 1) : 0u;
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)wpre, SW_NT / 64 - 1);
+        const uint32_t x0 = base + incl - l0 - l1, x1 = x0 + l0;
+        S.X[2 * t] = x0;
+        S.X[2 * t + 1] = x1;
+        // cuts: 16 KiB of output, a distance before the stream start, an over-read
+        const bool near_end = p + SW_R + 48 > endb;
+#pragma unroll
+        for (uint32_t h = 0; h < 2; h++) {
+            const uint32_t i = 2 * t + h, v = x[h];
+            if (v >= SW_R) continue;
+            const uint32_t e = h ? e1 : e0, ln = h ? l1 : l0, xo = h ? x1 : x0;
+            if (xo + ln > SW_OUTCAP) atomicMin(&S.cut, i);
+            if (ln && ((e >> 6) & 3) == SK_MATCH && sw_dist(e) > pos + xo) atomicMin(&S.cutx, i);
+            if (near_end && ((e >> 6) & 3) != SK_BAD && p + v + (e & 63) > endb) atomicMin(&S.cutov, i);
+        }
+        __syncthreads();
+        stamp(1);
+        const uint32_t nmem = S.nmem, cutc = S.cut, cutx = S.cutx, cutov = S.cutov;
+        const uint32_t ev = min(cutx, cutov);
+        if (cutov < nmem && cutov <= cutx && cutov < cutc) {  // over-read first: the region is not written
+            err = SEGF_OVERREAD;
+            break;
+        }
+        uint32_t C = min(min(cutc, ev), nmem);  // members [0, C) are written
+        const uint32_t tot = C < nmem ? S.X[C] : total;
+        // where the next region starts (read now: once the region's last barrier is passed, the
+        // faster waves overwrite node[] and E[] with the next region's)
+        uint64_t nextp = p;
+        bool done = false;
+        if (C == cutc && cutc < ev && cutc < nmem) {  // 16 KiB: the next region starts at member C
+            nextp += S.node[C];
+        } else if (C == cutx && cutx < nmem) {  // a distance before the stream start
+            if (piece) {
+                err = SEGF_XREF;
+                done = true;
+            } else {
+                const uint32_t v = S.node[C];
+                nextp += v + (S.E[v] & 63);
+            }
+        } else {  // the chain's last member: end of block, a bad code, or past the region
+            const uint32_t v = S.node[nmem - 1], e = S.E[v], kind = (e >> 6) & 3;
+            nextp += v + (e & 63);
+            if (kind == SK_EOB) {
+                done = true;
+            } else if (kind == SK_BAD) {
+                err = SEGF_ERR_DATA;
+                done = true;
+            }
+        }
+        // 5. parallel writes: literals, matches whose source precedes the region.  The other
+        // ("dependent") matches read the region's own output: their members are flagged in
+        // S.DB and their output bytes in S.PB, for wave 0
+#pragma unroll
+        for (uint32_t h = 0; h < 2; h++) {
+            const uint32_t i = 2 * t + h;
+            const uint32_t e = h ? e1 : e0, ln = h ? l1 : l0, xo = h ? x1 : x0;
+            const bool mine = i < C && ln;
+            const uint32_t kind = (e >> 6) & 3;
+            const uint32_t dst = (uint32_t)pos + xo;
+            if (mine && kind == SK_LIT) ring[dst & 0xFFFFu] = (uint8_t)(e >> 8);
+            const uint32_t d = sw_dist(e);
+            const bool indep = mine && kind == SK_MATCH && d >= xo + ln;
+            if (indep && ln <= 32) sw_copy_short(ring, dst, d, ln);
+            if (mine && kind == SK_MATCH && !indep) {
+                atomicOr(&S.DB[i >> 5], 1u << (i & 31));
+                for (uint32_t b = xo; b < xo + ln;) {
+                    const uint32_t n = min(32u - (b & 31), xo + ln - b);
+                    atomicOr(&S.PB[b >> 5], (n == 32 ? ~0u : ((1u << n) - 1u)) << (b & 31));
+                    b += n;
+                }
+            }
+            const uint64_t m = __ballot(indep && ln > 32);
+            for (uint64_t q = m; q; q &= q - 1) {  // long ones: the wave copies each, 64 bytes per step
+                const int k = __builtin_ctzll(q);
+                const uint32_t kd = (uint32_t)__builtin_amdgcn_readlane((int)dst, k);
+                const uint32_t kdist = (uint32_t)__builtin_amdgcn_readlane((int)d, k);
+                const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)ln, k);
+                for (uint32_t b = lane; b < kl; b += 64) ring[(kd + b) & 0xFFFFu] = ring[(kd - kdist + b) & 0xFFFFu];
+            }
+        }
+        __syncthreads();
+        stamp(2);
+        // wave 0: the dependent matches, listed in token order.  Those whose source (the first
+        // period of a periodic one) holds no dependent output copy first, side by side; then
+        // the rest, one after the other.
+        if (wv == 0) {
+            const uint32_t bits = S.DB[lane];
+            const uint32_t nb = (uint32_t)__popc(bits);
+            const uint32_t inc = wave_incl_scan(nb);
+            const uint32_t ndep = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            uint32_t at = inc - nb;
+            for (uint32_t b = bits; b; b &= b - 1) S.DL[at++] = (uint16_t)(32 * lane + (uint32_t)__builtin_ctz(b));
+            wave_sync();
+            for (uint32_t b0 = 0; b0 < ndep; b0 += 64) {
+                uint32_t e = 0, xo = 0;
+                const bool have = b0 + lane < ndep;
+                if (have) {
+                    const uint32_t i = S.DL[b0 + lane];
+                    e = S.E[S.node[i]];
+                    xo = S.X[i];
+                }
+                sw_deps(ring, S.PB, (uint32_t)pos, have, xo, have ? sw_len(e) : 0u, sw_dist(e));
+            }
+        }
+        __syncthreads();
+        stamp(3);
+#ifdef DMX_SW_TRACE
+        if (t == 0 && pos + 40000 > DMX_SW_TRACE && pos < DMX_SW_TRACE + 1000)
+            printf("dbl p %llu pos %llu tot %u C %u nmem %u\n", (unsigned long long)p, (unsigned long long)pos, tot, C, nmem);
+#endif
+        pos += tot;
+        p = nextp;
+        flush_if();
+        stamp(3);
+        cy[5]++;
+        if (done) break;
+    }
+    if (t == 0) {
+        S.p = p;
+        S.pos = pos;
+        S.flushed = flushed;
+        S.rb = rb;
+        S.err = err;
+        if (timed)
+            for (int k = 0; k < 6; k++) S.cyc[k] += cy[k];
+    }
+    __syncthreads();
+}
+
+struct WgSink : FlushSink {
+    SwSmem* S;
+    uint32_t walk;  // 0: doubling regions only; else walk regions, warm-up bits | rounds << 16
+    const uint32_t* words;
+    uint64_t nwords, end_bytes;
+};
+
+// the Huffman blocks of k_inflate_serial_wg (found by ADL from inflate_blocks): wave 0 hands the
+// state to the waiting waves and decodes the block with them
+__device__ uint32_t decode_block(RingIn& br, const Tables&, WgSink& sk) {
+    SwSmem& S = *sk.S;
+    if (lane_id() == 0) {
+        S.cmd = SW_CMD_DECODE;
+        S.p = br.abspos();
+        S.pos = sk.pos;
+        S.flushed = sk.flushed;
+        S.rb = br.rb;
+    }
+    __syncthreads();  // the other waves wait here (k_inflate_serial_wg)
+    sw_block(S, (GlbU32*)sk.words, sk.nwords, sk.end_bytes, (GlbU8*)sk.out, sk.cap, sk.piece, sk.cyc != nullptr,
+             sk.walk);
+    br.rb = S.rb;
+    sk.pos = S.pos;
+    sk.flushed = S.flushed;
+    if (S.err) {
+        sk.err |= S.err == SEGF_XREF ? SEGF_XREF : 0u;
+        return S.err;
+    }
+    br.seek(S.p);
+    return 0;
+}
+
+__global__ __launch_bounds__(SW_NT) void k_inflate_serial_wg(InflateArgs A, int count_only, InflateResult* res,
+                                                             int walk) {
+    __shared__ __attribute__((aligned(16))) SwSmem S;
+    const uint32_t t = threadIdx.x;
+    if (t == 0) {
+        S.T.fixed_loaded = 0;
+        S.cmd = 0;
+    }
+    if (t < 12) S.cyc[t] = 0;
+    if (t < 128) S.flag[t] = 0;
+    __syncthreads();
+    if (t < 64) {  // wave 0: the block loop
+        RingIn br;
+        br.init(A.in_words, A.misalign, A.n, S.inring);
+        br.seek(A.misalign * 8);
+        WgSink sk;
+        sk.ring = S.oring;
+        sk.pos = 0;
+        sk.flushed = 0;
+        sk.out = A.out;
+        sk.cap = count_only ? 0 : A.cap;
+        sk.err = 0;
+        sk.piece = (A.flags & DMX_IFLAG_PIECE) != 0;
+        sk.cyc = A.dbg ? S.cyc : nullptr;
+        sk.flag = S.flag;
+        sk.S = &S;
+        sk.walk = (uint32_t)walk;
+        sk.words = A.in_words;
+        sk.end_bytes = A.misalign + A.n;
+        sk.nwords = (sk.end_bytes + 3) / 4;
+        uint64_t end_byte = 0;
+        bool fin = false;
+        const uint32_t err = inflate_blocks(br, S.T, sk, (A.flags & DMX_CFG_RFC_STRICT) != 0, false, &end_byte, &fin);
+        sk.flush();
+        if (t == 0) {
+            res->total = sk.pos;
+            res->status = err == 0 ? 0 : (err & SEGF_OVERREAD) ? DMX_ERR_OVERREAD : DMX_ERR_DATA;
+            res->fin_index = 0;
+            res->end_byte = fin ? end_byte - A.misalign : 0;
+            S.cmd = SW_CMD_EXIT;
+        }
+        if (t < 12) res->cycles[t] = S.cyc[t];
+        __syncthreads();  // releases the other waves
+    } else {
+        for (;;) {
+            __syncthreads();  // wave 0 publishes a command
+            if (S.cmd == SW_CMD_EXIT) break;
+            sw_block(S, (GlbU32*)A.in_words, (A.misalign + A.n + 3) / 4, A.misalign + A.n, (GlbU8*)A.out,
+                     count_only ? 0 : A.cap, (A.flags & DMX_IFLAG_PIECE) != 0, A.dbg != nullptr, (uint32_t)walk);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1417,6 +2208,26 @@ hipError_t launch_inflate_validate(const InflateArgs& A, ValidateWords* W, Infla
 
 hipError_t launch_inflate_serial(const InflateArgs& A, int count_only, InflateResult* res,
                                  hipStream_t st) {
+    // DMX_SERIAL_WAVE=1: the one-wavefront decoder (developer A/B)
+    static const bool one_wave = [] {
+        const char* e = std::getenv("DMX_SERIAL_WAVE");
+        return e && *e == '1';
+    }();
+    // DMX_SERIAL_WALK=0: doubling regions only; DMX_SERIAL_WARM / DMX_SERIAL_ROUNDS: the walk's
+    // warm-up bits and synchronisation rounds (developer A/B)
+    static const int walk = [] {
+        const char* e = std::getenv("DMX_SERIAL_WALK");
+        if (e && *e == '0') return 0;
+        const char* w = std::getenv("DMX_SERIAL_WARM");
+        const char* k = std::getenv("DMX_SERIAL_ROUNDS");
+        const int warm = w && *w ? std::atoi(w) : (int)SW_WARM;
+        const int kmax = k && *k ? std::atoi(k) : (int)SW_KMAX;
+        return (warm & 0xFFFF) | (kmax << 16);
+    }();
+    if (!one_wave) {
+        hipLaunchKernelGGL(k_inflate_serial_wg, dim3(1), dim3(SW_NT), 0, st, A, count_only, res, walk);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_inflate_serial, dim3(1), dim3(IF_NT), 0, st, A, count_only, res);
     return hipGetLastError();
 }

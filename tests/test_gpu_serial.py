@@ -1,10 +1,11 @@
-"""The serial decoder (k_inflate_serial), the safety net for every stream the parallel paths
+"""The serial decoder (k_inflate_serial_wg), the safety net for every stream the parallel paths
 decline: forced with dev_inflate_pass (7 = the serial decoder alone), it must
 give the oracle's bytes -- realDecompress, /root/reference/include/inflate.hpp:277-322 -- and
 errors.  Speed bar: faster than the reference's own inflate::decompress of
 the same stream on one core of the same host (the rule of test_gpu_path5_foreign.py), not a
-floor taken from the decoder's own measurements.  The two cases the one-wavefront decoder does
-not win yet are expected failures with the measured rates, not passes."""
+floor taken from the decoder's own measurements.  The one case the decoder does not win clearly
+(zlib-6 of the mixed corpus: about the reference's rate) is a non-strict expected failure with
+the measured rates, not a pass."""
 import time
 import zlib
 
@@ -36,16 +37,18 @@ def _run(c, s, n):
     return d_o[:olen].cpu().numpy().tobytes(), path, ms
 
 
-# The decoder is one wavefront (the stream is one dependency chain): it decodes the token at 128
-# consecutive bit offsets at once and walks the true chain four tokens per scalar step.  Round 6 on
-# one MI355X against the reference on one core of the box's EPYC 9575F (16 MiB, MB/s GPU / ref):
-# mixed zlib-6 29.7 / 127, text zlib-1 13.8 / 76, one literal-only fixed block 10.8 / 26, bmp
-# Z_FIXED 35.9 / 84.  The one-wavefront decoder loses every case, so each is an expected failure
-# (non-strict: an XPASS shows the day it wins) instead of a floor that certifies it.  Streams the
-# parallel paths take never reach it; a truncated or corrupt stream now gets its error from the
-# block-parallel chain (test_gpu_path5_foreign.py), not from this decoder.
-SLOW = pytest.mark.xfail(reason="one-wavefront serial decoder below the reference's one-core rate "
-                                "(round 6: 2.3-5.5x slower on the EPYC 9575F)", strict=False)
+# The decoder is one 1024-thread workgroup (k_inflate_serial_wg): each Huffman block goes in
+# regions -- 32 Kbit walk regions (512 threads walk 64-bit slices with a 128-bit warm-up and
+# resynchronise in rounds) for dynamic-code blocks, 2 Kbit doubling regions (pointer doubling over
+# the token at every bit offset) for fixed-code blocks and wherever a walk does not converge.
+# Round 6 on one MI355X against the reference on one core of the box's EPYC 9575F (16 MiB, MB/s
+# GPU / ref): mixed zlib-6 127 / 125-134, text zlib-1 115 / 76, one literal-only fixed block
+# 39 / 26, bmp Z_FIXED 108 / 81 (the round-5 one-wavefront decoder: 29.7, 13.8, 10.8, 35.9).
+# The mixed zlib-6 case is at parity, so it stays a non-strict expected failure; the others must
+# beat the reference.  Streams the parallel paths take never reach this decoder; a truncated or
+# corrupt stream gets its error from the block-parallel chain (test_gpu_path5_foreign.py).
+SLOW = pytest.mark.xfail(reason="mixed zlib-6: the workgroup serial decoder is at the reference's "
+                                "one-core rate (127 vs 125-134 MB/s), not clearly above it", strict=False)
 
 
 def _ref_ms(s):
@@ -63,9 +66,12 @@ def _ref_ms(s):
 
 
 @pytest.mark.parametrize("kind,shape", [("mixed", "zlib6"), ("text", "zlib1"), ("mixed", "single"),
-                                        ("bmp", "zfixed")])
+                                        ("bmp", "zfixed"), ("repeat", "zlib6"), ("zeros", "zlib6"),
+                                        ("text", "zlib9")])
 def test_serial_16MiB_bytes(sctx, oracle, kind, shape):
-    """Bit-exact against the oracle on the forced serial decoder (parity: always required)."""
+    """Bit-exact against the oracle on the forced serial decoder (parity: always required).  The
+    high-ratio shapes (repeat, zeros) cut the walk and doubling regions at 16 KiB of output and
+    resolve long chains of matches that read each other."""
     data = dmx.corpus(kind, 16 << 20)
     s = _STREAMS[shape](data)
     out, path, ms = _run(sctx, s, len(data))
@@ -74,12 +80,12 @@ def test_serial_16MiB_bytes(sctx, oracle, kind, shape):
 
 
 _STREAMS = {"zlib6": lambda d: streams.zlib_raw(d, 6), "zlib1": lambda d: streams.zlib_raw(d, 1),
+            "zlib9": lambda d: streams.zlib_raw(d, 9),
             "single": lambda d: streams.single_fixed_block(d), "zfixed": lambda d: streams.zfixed(d)}
 
 
-@SLOW
-@pytest.mark.parametrize("kind,shape", [("mixed", "zlib6"), ("text", "zlib1"), ("mixed", "single"),
-                                        ("bmp", "zfixed")])
+@pytest.mark.parametrize("kind,shape", [pytest.param("mixed", "zlib6", marks=SLOW), ("text", "zlib1"),
+                                        ("mixed", "single"), ("bmp", "zfixed")])
 def test_serial_16MiB_speed(sctx, oracle, kind, shape):
     data = dmx.corpus(kind, 16 << 20)
     s = _STREAMS[shape](data)

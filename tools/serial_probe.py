@@ -18,10 +18,12 @@ for kind, shape in [("mixed", "zlib6"), ("text", "zlib1"), ("mixed", "single"), 
          "single": lambda: streams.single_fixed_block(data), "zfixed": lambda: streams.zfixed(data)}[shape]()
     d_in = torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda()
     d_o = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    n = c.inflate_device(d_in.data_ptr(), len(s), d_o.data_ptr(), len(data) + 64)
-    ms = (time.perf_counter() - t) * 1e3
+    ms = 1e30
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        n = c.inflate_device(d_in.data_ptr(), len(s), d_o.data_ptr(), len(data) + 64)
+        ms = min(ms, (time.perf_counter() - t) * 1e3)
     ok = d_o[:n].cpu().numpy().tobytes() == data
     print(f"{kind} {shape}: {len(s)} B -> {n} B in {ms:.1f} ms = {len(data) / ms / 1e3:.1f} MB/s ok {ok}", flush=True)
     sys.stderr.flush()
