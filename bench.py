@@ -254,11 +254,23 @@ def dist_step(torch, ctx, dev, run, level, gathered, sub, stream):
         got[0] = olen
         return run.d_out[:olen]
 
+    # the pieces decode with no host sync (dmx_inflate_device_async): their {bytes, status} words
+    # ride in the ranks' one all_gather; a piece the lane path does not take decodes again
+    # synchronously (decode above)
+    d_res = torch.zeros(2, dtype=torch.int64, device=dev)
+
+    def decode_async(piece, first):
+        ctx.inflate_device_async(piece.data_ptr(), piece.numel(), run.d_out.data_ptr(), run.out_cap,
+                                 d_res.data_ptr(), stream=sh, piece=not first)
+        return d_res, run.d_out
+
     src = gathered if rank == 0 else torch.empty(0, dtype=torch.uint8, device=dev)
     _, ok = shard.scatter_inflate(src, total if rank == 0 else 0, decode, starts=starts,
                                   out=run.d_out if rank == 0 else None, check=check, gather=False,
-                                  balance="count")
+                                  balance="count", decode_async=decode_async if dev.type == "cuda" else None)
     ev[2].record(stream)
+    if dev.type == "cuda" and not got[0]:  # decoded by decode_async: this rank's bytes
+        got[0] = int(d_res[0].item()) if int(d_res[1].item()) == 0 else got[0]
     return ev, total, got[0], ok
 
 

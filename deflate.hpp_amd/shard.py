@@ -308,7 +308,8 @@ def pick_cuts(starts, total, world, check=None, balance="bytes"):
     return split_points(starts, total, world, valid=lambda s: s in ok, balance=balance)
 
 
-def scatter_inflate(stream, clen, decode, starts=None, out=None, check=None, gather=True, balance="bytes"):
+def scatter_inflate(stream, clen, decode, starts=None, out=None, check=None, gather=True, balance="bytes",
+                    decode_async=None):
     """Inflate one stream held by rank 0 (stream[:clen]) on all ranks.
 
     decode(piece, first) -> 1-D uint8 tensor of decoded bytes, raising on a decode error; first
@@ -323,6 +324,10 @@ def scatter_inflate(stream, clen, decode, starts=None, out=None, check=None, gat
     (decode's own buffer; bench.py at N > 1): no byte goes back to rank 0 and out is unused
     except for the whole-stream fallback.  balance: cut targets by stream bytes, or by
     candidate count ("count": equal output for libdmx's equal-size segments).
+    decode_async(piece, first) -> (res, buf): the same decode enqueued without a host sync
+    (libdmx's dmx_inflate_device_async): res is a device int64 pair {bytes, status}, buf the
+    output tensor.  The statuses travel in the one all_gather the ranks need anyway; a rank whose
+    status is 1 (a piece the lane path does not take) decodes it again with decode().
     """
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = stream.device
@@ -349,13 +354,34 @@ def scatter_inflate(stream, clen, decode, starts=None, out=None, check=None, gat
         piece[plen: plen + 2].copy_(torch.tensor(FINAL_EMPTY, dtype=torch.uint8))
         plen += 2
     dec, ok = None, 1
-    if plen:
+    cap = out.numel() if (rank == 0 and out is not None) else -1
+    st = None
+    if decode_async is not None:
+        # {ok, bytes, cap, status} per rank from device values: no host read before the gather
+        res, buf = decode_async(piece[:plen], rank == 0) if plen else (None, None)
+        mine = torch.tensor([1, 0, cap, 0], dtype=torch.int64, device=dev)
+        if res is not None:
+            mine[1:2].copy_(res[0:1])
+            mine[3:4].copy_(res[1:2])
+        parts = [torch.zeros(4, dtype=torch.int64, device=dev) for _ in range(world)]
+        dist.all_gather(parts, mine)
+        st = [[int(x) for x in p.tolist()] for p in parts]
+        if st[rank][3] == 0 and res is not None:
+            dec = buf[: st[rank][1]]
+        if any(x[3] != 0 for x in st):  # some rank needs the synchronous decode of its piece
+            if st[rank][3] != 0:
+                try:
+                    dec = decode(piece[:plen], rank == 0)
+                except Exception:
+                    ok = 0
+            st = _all_gather_ints([ok, 0 if dec is None else dec.numel(), cap], dev)
+    elif plen:
         try:
             dec = decode(piece[:plen], rank == 0)
         except Exception:
             ok = 0
-    cap = out.numel() if (rank == 0 and out is not None) else -1
-    st = _all_gather_ints([ok, 0 if dec is None else dec.numel(), cap], dev)
+    if st is None:
+        st = _all_gather_ints([ok, 0 if dec is None else dec.numel(), cap], dev)
     oks = [s[0] for s in st]
     sizes = [s[1] for s in st]
     if not all(oks):

@@ -122,6 +122,23 @@ def _oracle_decode(orc):
     return decode
 
 
+def _oracle_decode_async(orc, refuse_rank=None):
+    """Stand-in for Context.inflate_device_async: {bytes, status} in a tensor, status 1 when the
+    piece does not decode (or, refuse_rank, always on that rank: the synchronous retry runs)."""
+    def decode_async(piece, first):
+        buf = torch.zeros(8 << 20, dtype=torch.uint8)
+        res = torch.tensor([0, 1], dtype=torch.int64)
+        if dist.get_rank() != refuse_rank:
+            try:
+                b = orc.inflate(piece.numpy().tobytes(), piece=not first)
+                buf[:len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8) if b else buf[:0]
+                res = torch.tensor([len(b), 0], dtype=torch.int64)
+            except Exception:
+                pass
+        return res, buf
+    return decode_async
+
+
 def _oracle_check(orc, s):
     """Stand-in for Context.segment_check_device: the segment at c must decode in piece mode up
     to the first 00 00 FF FF after it (or to the stream end, as the final segment)."""
@@ -165,7 +182,7 @@ def _scatter_case(name):
     return s, _markers(s)
 
 
-def _scatter_worker(rank, world, port, name, use_check, out_cap, q):
+def _scatter_worker(rank, world, port, name, use_check, out_cap, q, mode=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -175,9 +192,14 @@ def _scatter_worker(rank, world, port, name, use_check, out_cap, q):
     stream = torch.frombuffer(bytearray(s), dtype=torch.uint8) if rank == 0 else torch.empty(0, dtype=torch.uint8)
     out = torch.empty(out_cap, dtype=torch.uint8) if rank == 0 else None
     try:
+        da = None
+        if mode == "async":
+            da = _oracle_decode_async(orc)
+        elif mode == "async-refuse":
+            da = _oracle_decode_async(orc, refuse_rank=world - 1)
         total, ok = shard.scatter_inflate(stream, len(s) if rank == 0 else 0, _oracle_decode(orc),
                                           starts=starts if rank == 0 else None, out=out,
-                                          check=_oracle_check(orc, s) if use_check else None)
+                                          check=_oracle_check(orc, s) if use_check else None, decode_async=da)
         res = (bytes(out[:total].numpy()), ok)
     except Exception as e:  # every rank reports (a rank that hung would time the test out)
         res = ("raised", type(e).__name__)
@@ -230,6 +252,29 @@ def test_scatter_inflate_libdmx_stream(oracle, world, use_check):
     dec, ok = res[0]
     assert ok
     assert hashlib.sha256(dec).hexdigest() == full["out_sha256"]
+
+
+def _scatter_worker_mode(rank, world, port, name, use_check, out_cap, mode, q):
+    _scatter_worker(rank, world, port, name, use_check, out_cap, q, mode)
+
+
+@pytest.mark.parametrize("mode", ["async", "async-refuse"])
+def test_scatter_inflate_async_decode(oracle, mode):
+    """the pieces decode through decode_async (dmx_inflate_device_async on a
+    GPU) with their statuses in the ranks' one all_gather; a rank whose status says "not the lane
+    path" decodes its piece again synchronously.  Same bytes either way; a corrupt split still
+    falls back to rank 0's whole decode."""
+    import hashlib
+    m = _dmx_manifest()
+    full = next(s for s in m["streams"] if s["file"] == "mixed1M_L2.deflate")
+    res = _run(_scatter_worker_mode, 3, "mixed1M_L2.deflate", True, 4 << 20, mode, all_ranks=True)
+    dec, ok = res[0]
+    assert ok
+    assert hashlib.sha256(dec).hexdigest() == full["out_sha256"]
+    s = _read("mixed1M_L0_shard0.deflate") + _read("mixed1M_L0_shard1.deflate")
+    dec, ok = _run(_scatter_worker_mode, 2, "corrupt-split", False, 4 << 20, mode, all_ranks=True)[0]
+    assert not ok
+    assert dec == oracle.inflate(s)
 
 
 def test_scatter_inflate_false_marker_falls_back(oracle):
