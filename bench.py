@@ -267,9 +267,9 @@ def dist_step(torch, ctx, dev, run, level, gathered, sub, stream):
     src = gathered if rank == 0 else torch.empty(0, dtype=torch.uint8, device=dev)
     _, ok = shard.scatter_inflate(src, total if rank == 0 else 0, decode, starts=starts,
                                   out=run.d_out if rank == 0 else None, check=check, gather=False,
-                                  balance="count", decode_async=decode_async if dev.type == "cuda" else None)
+                                  balance="count", decode_async=decode_async if hasattr(ctx, "inflate_device_async") else None)
     ev[2].record(stream)
-    if dev.type == "cuda" and not got[0]:  # decoded by decode_async: this rank's bytes
+    if not got[0]:  # decoded by decode_async: this rank's bytes
         got[0] = int(d_res[0].item()) if int(d_res[1].item()) == 0 else got[0]
     return ev, total, got[0], ok
 

@@ -425,6 +425,16 @@ class _HostCodec(_HostDeflate):
     def inflate_piece_device(self, d_in, n, d_out, cap, stream=None):
         return self._inflate(d_in, n, d_out, cap, True)
 
+    def inflate_device_async(self, d_in, n, d_out, cap, d_result, stream=None, piece=False):
+        """{bytes, status} at d_result (int64 pair); status 1 when the piece does not decode here,
+        so dist_step's synchronous retry runs (as on the GPU for a stream the lane path declines)."""
+        import ctypes
+        res = (ctypes.c_int64 * 2).from_address(d_result)
+        try:
+            res[0], res[1] = self._inflate(d_in, n, d_out, cap, piece), 0
+        except Exception:
+            res[0], res[1] = 0, 1
+
     def segment_starts_device(self, d_in, n, stream=None):
         import ctypes
         return _markers(ctypes.string_at(d_in, n))
