@@ -1528,16 +1528,17 @@ __device__ __forceinline__ void sw_deps(LdsU8* ring, const uint32_t* PB, uint32_
 }
 
 // One walk region of SW_RW bits from stream bit p (output position pos >= 32 KiB, the region
-// inside the stream): thread t walks the tokens of its 32-bit slice from the slice start (thread
-// 0 from p); then, in rounds, every thread whose entry -- its predecessor's exit -- differs from
-// the one it walked from walks again from there until its path meets a token start of its old
-// path (Huffman codes resynchronise within a few tokens: from there on the paths are the same).
-// When no exit changes, every slice holds the stream's true tokens.  A second walk sums each
-// slice's output (workgroup scan: output offsets), a third writes literals and the matches whose
-// source precedes the region and lists the others for wave 0 (sw_deps), in output order.
+// inside the stream): thread t < SW_NS walks the tokens of its 64-bit slice, starting SW_WARM
+// bits before it (thread 0 from p); then, in rounds, every thread whose entry -- its
+// predecessor's exit -- differs from the token it started at walks again from there until its
+// path meets a token start of its old path (from there on the paths are the same).  When no exit
+// changes, every slice holds the stream's true tokens.  A second walk sums each slice's output
+// (workgroup scan: output offsets), a third writes literals and the matches whose source precedes
+// the region; the bytes of the other matches are resolved by pointer jumping over the region's
+// output (R[b] = b - d, then R[b] = R[R[b]]) and copied side by side.
 // Returns 0 (region done: *np, *ntot), 1 (the block's end of block was in it: *np after it) or
-// 2 (not converged in SW_KMAX rounds, a bad code on the path, too many dependent matches: the
-// caller decodes the same span as doubling regions, which also rewrite anything written here).
+// 2 (not converged in kmax rounds, or a bad code on the path: the caller decodes the same span
+// as doubling regions, which also rewrite anything written here).
 __device__ __attribute__((noinline)) uint32_t sw_walk(SwSmem& S, GlbU32* w, uint64_t nwords, uint64_t end_bytes,
                                                       uint64_t p, uint64_t pos, uint64_t* np, uint32_t* ntot,
                                                       uint32_t* rounds, bool timed, uint32_t warm, uint32_t kmax) {
