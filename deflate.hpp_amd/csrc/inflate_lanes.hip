@@ -27,12 +27,13 @@
 // (decompressHuffmanBlock inflate.hpp:226-275, readDynamicTreeCodes :166-206, realDecompress
 // :277-322), including "distance beyond the output so far copies nothing" at the stream start.
 //
-// Phase B, k_inflate_resolve: one wavefront per segment rebuilds the output in a 32 KiB LDS
-// window from the token list, 64 tokens per step (wave prefix sum of token lengths):
-// literal runs and short matches whose source lies before the step go in parallel (4 bytes
-// per iteration when d >= 4), long or self-dependent matches are copied by the whole wave in
-// token order (periodic copy out[o + i] = out[o - d + (i mod d)], as the reference's
-// byte-serial copy inflate.hpp:268-270), then 16-byte stores put the window at j * slot.
+// Phase B, k_inflate_resolve: one workgroup per segment rebuilds the output in a 32 KiB LDS
+// window from the token list; its first wavefront takes 64 tokens per step (wave prefix sum of
+// token lengths): literal runs and short matches whose source lies before the step go in
+// parallel (4 bytes per iteration when d >= 4), long or self-dependent matches are copied by the
+// whole wave in token order (periodic copy out[o + i] = out[o - d + (i mod d)], as the
+// reference's byte-serial copy inflate.hpp:268-270); then all waves put the window at j * slot
+// with 16-byte stores (a long periodic copy at the segment's end goes straight to HBM).
 #include "../../include/dmx.h"
 #include "dmx_device.h"
 #include "dmx_internal.h"
@@ -79,11 +80,32 @@ constexpr uint32_t LN_LANES = DMX_LN_LANES;
 #ifndef DMX_LN_PRETAB
 #define DMX_LN_PRETAB 1
 #endif
-// resolve: the segment's last token, a periodic copy, written straight to HBM (1) or through the
-// window (0; measured faster: repeat inflate 0.629 vs 0.655 ms, zeros 0.468 vs 0.495 ms)
+// resolve workgroup: RS_NT threads around one window.  Wave 0 runs the token steps, the
+// workgroup fills periodic copies of >= RS_BIG bytes (repeat, zeros, image rows: segments of at
+// most RS_FOLLOW token words) and copies the window out.  A 32 KiB window allows five workgroups
+// per CU: with one wave each, those copies ran at 1.25 waves per SIMD, latency-bound.
+#ifndef DMX_RS_NT
+#define DMX_RS_NT 256
+#endif
+#ifndef DMX_RS_BIG
+#define DMX_RS_BIG 2048
+#endif
+#ifndef DMX_RS_FOLLOW
+#define DMX_RS_FOLLOW 1024
+#endif
+constexpr uint32_t RS_FOLLOW = DMX_RS_FOLLOW;
+#ifndef DMX_RS_SPLIT
+#define DMX_RS_SPLIT 1
+#endif
+// (NT = 64) the segment's last token, a periodic copy, written straight to HBM (1) or through
+// the window (0; measured faster: repeat inflate 0.629 vs 0.655 ms, zeros 0.468 vs 0.495 ms)
 #ifndef DMX_LN_DIRECT
 #define DMX_LN_DIRECT 0
 #endif
+constexpr uint32_t RS_NT = DMX_RS_NT;
+constexpr uint32_t RS_BIG = DMX_RS_BIG;
+static_assert(RS_NT % 64 == 0 && RS_NT <= 1024, "resolve workgroup");
+constexpr bool kRsSplit = DMX_RS_SPLIT && RS_NT > 64;
 
 __constant__ const uint8_t kLnPerm[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5,
                                           11, 4,  12, 3, 13, 2, 14, 1, 15};
@@ -1056,11 +1078,90 @@ __device__ __forceinline__ uint32_t ln_copy_wave(uint8_t* win, uint32_t o, uint3
     return o + L;
 }
 
-// One segment of k_inflate_resolve: `sf` = its record's {out_size, flags}, n token words at tk.
+// smallest multiple of d >= 16 (d < 16: d * ceil(16 / d), no division)
+__device__ __forceinline__ uint32_t ln_c16(uint32_t d) {
+    return d >= 16 ? d : d * (d == 1 ? 16u : d == 2 ? 8u : d == 3 ? 6u : d <= 5 ? 4u : d <= 7 ? 3u : 2u);
+}
+// the prefix length ln_copy_wave builds before its fill pass (L if none): the first period (or
+// for d < 64 the largest multiple of d that fits one byte per lane), doubled while the rest is
+// short (at most two more rounds: no divisions) or until it holds c16 + 16 bytes
+__device__ __forceinline__ uint32_t ln_prefix_len(uint32_t L, uint32_t d) {
+    uint32_t P = d >= 64 ? d : d * (64 / d);
+    const uint32_t c16 = ln_c16(d);
+    while (P < L && (P < c16 + 16 || L <= 4 * P)) P += min(P, L - P);
+    return min(P, L);
+}
+// builds [o, o + P) of the periodic copy (the wave; the caller syncs before reading it)
 template <uint32_t CAP>
+__device__ __forceinline__ void ln_build_prefix(uint8_t* win, uint32_t o, uint32_t L, uint32_t d, uint32_t Pend) {
+    uint32_t P;
+    if (d >= 64) {
+        ln_copy_plain<CAP>(win, o, o - d, d);
+        P = d;
+    } else {
+        const uint32_t lane = lane_id();
+        P = d * (64 / d);  // 33..64 bytes, a multiple of d
+        if (lane < min(P, L)) win[o + lane] = win[o - d + lane % d];
+    }
+    while (P < Pend) {
+        wave_sync();
+        const uint32_t n = min(P, Pend - P);
+        ln_copy_plain<CAP>(win, o + P, o, n);
+        P += n;
+    }
+}
+
+// A periodic copy of L >= RS_BIG bytes at o with distance d < L: wave 0 builds its prefix
+// [o, o + P) and the bytes up to the next 16-byte boundary a0 (the caller syncs the workgroup),
+// then ln_fill_wg has every thread of the workgroup write [a0, o + L) from that prefix (period
+// Q = P - c16, a multiple Q >= 16 of d; the prefix holds Q + 16 bytes).
+template <uint32_t CAP>
+__device__ __forceinline__ void ln_fill_head(uint8_t* win, uint32_t o, uint32_t L, uint32_t d, uint32_t P) {
+    ln_build_prefix<CAP>(win, o, L, d, P);
+    wave_sync();
+    const uint32_t beg = o + P, a0 = (beg + 15) & ~15u, Q = P - ln_c16(d);
+    if (lane_id() < a0 - beg) win[beg + lane_id()] = win[o + (P + lane_id()) % Q];
+}
+template <uint32_t CAP, uint32_t NT>
+__device__ __forceinline__ void ln_fill_wg(uint8_t* win, uint32_t o, uint32_t L, uint32_t d, uint32_t P) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t Q = P - ln_c16(d), end = o + L, a0 = (o + P + 15) & ~15u, a1 = end & ~15u;
+    const uint32_t nq = (a1 - a0) >> 4;
+    const uint32_t R = (16 * NT) % Q;
+    auto adv = [&](uint32_t r) { r += R; return r >= Q ? r - Q : r; };
+    uint32_t r = (a0 - o + 16 * t) % Q;
+    uint4* const D = reinterpret_cast<uint4*>(win + a0);
+    uint32_t k = t;
+    for (; k + 3 * NT < nq; k += 4 * NT) {
+        const uint32_t r1 = adv(r), r2 = adv(r1), r3 = adv(r2);
+        const uint4 v0 = ln_quad_at<CAP>(win, o + r), v1 = ln_quad_at<CAP>(win, o + r1);
+        const uint4 v2 = ln_quad_at<CAP>(win, o + r2), v3 = ln_quad_at<CAP>(win, o + r3);
+        D[k] = v0;
+        D[k + NT] = v1;
+        D[k + 2 * NT] = v2;
+        D[k + 3 * NT] = v3;
+        r = adv(r3);
+    }
+    for (; k < nq; k += NT) {
+        D[k] = ln_quad_at<CAP>(win, o + r);
+        r = adv(r);
+    }
+    if (t < end - a1) win[a1 + t] = win[o + (a1 - o + t) % Q];
+}
+
+// One segment of k_inflate_resolve: `sf` = its record's {out_size, flags}, n token words at tk.
+// All NT threads call it.  NT = 64: one wave does everything.  NT > 64 (token lists of at most
+// RS_FOLLOW words): wave 0 steps through the token words and writes the window; the other waves
+// step through the words and their scan too and join the fills of long periodic copies (they
+// reach the same copies in the same order: workgroup barriers in uniform control flow), the
+// stored copies and the copy-out.
+template <uint32_t CAP, uint32_t NT>
 __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j, uint2 sf, uint32_t n,
                                                const uint32_t* tk, uint8_t* win, uint32_t half_off = 0) {
-    const uint32_t lane = threadIdx.x;
+    constexpr bool GRP = NT > 64;
+    const uint32_t lane = GRP ? lane_id() : threadIdx.x;
+    const uint32_t t = threadIdx.x;  // (= lane when NT = 64)
+    const bool wz = !GRP || t < 64;  // the stepping wave
     if (sf.y & ~SEGF_FINAL) return;
     const uint64_t dst0 = j * (uint64_t)A.slot + half_off;
     if (dst0 >= A.cap) return;
@@ -1086,21 +1187,21 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
                 const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3);
                 const uint32_t* sw = reinterpret_cast<const uint32_t*>(src - sh);
                 uint4* d4 = reinterpret_cast<uint4*>(d);
-                for (uint32_t i = lane; i < m / 16; i += 64) {
+                for (uint32_t i = t; i < m / 16; i += NT) {
                     const uint32_t w0 = sw[4 * i], w1 = sw[4 * i + 1], w2 = sw[4 * i + 2], w3 = sw[4 * i + 3];
                     const uint32_t w4 = sh ? sw[4 * i + 4] : 0u;
                     d4[i] = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
                                        __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
                 }
-                for (uint32_t i = (m & ~15u) + lane; i < m; i += 64) d[i] = src[i];
+                for (uint32_t i = (m & ~15u) + t; i < m; i += NT) d[i] = src[i];
             } else {
-                for (uint32_t i = lane; i < m; i += 64) d[i] = src[i];
+                for (uint32_t i = t; i < m; i += NT) d[i] = src[i];
             }
             done += m;
         }
         return;
     }
-    uint64_t* const dbg = (A.dbg && lane == 0) ? A.dbg + j * kPhaseSlots : nullptr;
+    uint64_t* const dbg = (A.dbg && t == 0) ? A.dbg + j * kPhaseSlots : nullptr;
     if (dbg) dbg[5] = __builtin_amdgcn_s_memtime();
     uint32_t pos = 0, n_cx = 0;
     // the window holds the output below lim; the rest went straight to dst (see ln_copy_wave)
@@ -1118,7 +1219,7 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
         const uint32_t inc = wave_incl_scan(L);
         const uint32_t off = pos + inc - L;
         const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        if (!ism) {  // literal run of 1..3 bytes: exact-size stores
+        if (wz && !ism) {  // literal run of 1..3 bytes: exact-size stores
             if (L & 2) {
                 *reinterpret_cast<u16_unaligned*>(win + off) = (uint16_t)w;
                 if (L & 1) win[off + 2] = (uint8_t)(w >> 16);
@@ -1128,7 +1229,7 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
         }
         // short matches whose source lies before this step: each lane copies its own
         const bool simple = ism && L <= 32 && off + min(L, d) <= pos + d;
-        if (simple) {
+        if (wz && simple) {
             if (d >= L) {  // the whole source is final: read it at once (one LDS latency, not one
                            // per word), store exactly L bytes (neighbouring tokens store beside it)
                 uint64_t v[4];
@@ -1165,10 +1266,23 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
             const uint32_t ok = (uint32_t)__builtin_amdgcn_readlane((int)off, k);
             const uint32_t Lk = (uint32_t)__builtin_amdgcn_readlane((int)L, k);
             const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)d, k);
-            const bool last = DMX_LN_DIRECT && direct && t0 + (uint32_t)k + 1 == n && ok + Lk == nb;
-            const uint32_t e = ln_copy_wave<CAP>(win, ok, Lk, dk, last ? dst : win);
-            if (last) lim = e;
-            wave_sync();
+            if constexpr (GRP) {
+                const uint32_t P = dk < Lk && Lk >= RS_BIG ? ln_prefix_len(Lk, dk) : Lk;
+                if (P + 64 <= Lk) {  // the workgroup fills it
+                    if (wz) ln_fill_head<CAP>(win, ok, Lk, dk, P);
+                    __syncthreads();
+                    ln_fill_wg<CAP, NT>(win, ok, Lk, dk, P);
+                    __syncthreads();
+                } else if (wz) {
+                    ln_copy_wave<CAP>(win, ok, Lk, dk, win);
+                    wave_sync();
+                }
+            } else {
+                const bool last = DMX_LN_DIRECT && direct && t0 + (uint32_t)k + 1 == n && ok + Lk == nb;
+                const uint32_t e = ln_copy_wave<CAP>(win, ok, Lk, dk, last ? dst : win);
+                if (last) lim = e;
+                wave_sync();
+            }
             n_cx++;
         }
         if (dbg) {
@@ -1189,43 +1303,54 @@ __device__ __forceinline__ void ln_resolve_one(const InflateArgs& A, uint64_t j,
         dbg[13] = c_simple;
         dbg[14] = c_cx;
     }
+    if (GRP) __syncthreads();
     if ((((uintptr_t)dst) & 15) == 0) {
         const uint32_t nv = lim / 16;  // (lim < nb: a 16-byte boundary)
         const uint4* s4 = reinterpret_cast<const uint4*>(win);
         uint4* d4 = reinterpret_cast<uint4*>(dst);
-        uint32_t i = lane;
-        for (; i + 192 < nv; i += 256) {  // four 16-byte LDS reads in flight per lane
-            const uint4 v0 = s4[i], v1 = s4[i + 64], v2 = s4[i + 128], v3 = s4[i + 192];
+        uint32_t i = t;
+        for (; i + 3 * NT < nv; i += 4 * NT) {  // four 16-byte LDS reads in flight per lane
+            const uint4 v0 = s4[i], v1 = s4[i + NT], v2 = s4[i + 2 * NT], v3 = s4[i + 3 * NT];
             d4[i] = v0;
-            d4[i + 64] = v1;
-            d4[i + 128] = v2;
-            d4[i + 192] = v3;
+            d4[i + NT] = v1;
+            d4[i + 2 * NT] = v2;
+            d4[i + 3 * NT] = v3;
         }
-        for (; i < nv; i += 64) d4[i] = s4[i];
-        for (uint32_t i = nv * 16 + lane; i < lim; i += 64) dst[i] = win[i];
+        for (; i < nv; i += NT) d4[i] = s4[i];
+        for (uint32_t i = nv * 16 + t; i < lim; i += NT) dst[i] = win[i];
     } else {
-        for (uint32_t i = lane; i < nb; i += 64) dst[i] = win[i];
+        for (uint32_t i = t; i < nb; i += NT) dst[i] = win[i];
     }
     if (dbg) dbg[7] = __builtin_amdgcn_s_memtime();
 }
 
 // one workgroup per segment (a persistent grid with ticket-drawn segments and the next record
-// prefetched measured 5-20% slower on repeat and zeros, equal on text)
-template <uint32_t CAP>
-__global__ __launch_bounds__(64) void k_inflate_resolve(InflateArgs A, LaneArgs B) {
+// prefetched measured 5-20% slower on repeat and zeros, equal on text).  Two launches split the
+// segments by token count: NT = RS_NT takes lists of at most RS_FOLLOW words (and stored
+// segments), NT = 64 the longer ones -- one-wave workgroups step text faster (a 256-thread
+// workgroup whose other waves leave at once still measured 5 % slower on 1 GiB of text).
+template <uint32_t NT>
+__device__ __forceinline__ bool rs_mine(uint32_t n) {
+    return !kRsSplit || ((n <= RS_FOLLOW) == (NT > 64));
+}
+template <uint32_t CAP, uint32_t NT>
+__global__ __launch_bounds__(NT) void k_inflate_resolve(InflateArgs A, LaneArgs B) {
     __shared__ __attribute__((aligned(16))) uint8_t win[CAP];  // 32 KiB: five per CU; 64 KiB: two
     const uint64_t j = blockIdx.x;
     if (j >= cand_count(A)) return;
     if (CAP > LN_OUT_CAP && B.split[j] != ~0u) return;  // rebuilt by k_inflate_resolve_half
+    const uint32_t n = B.ntok[j];
+    if (!rs_mine<NT>(n)) return;
     const SegRecord* const rp = &A.recs[j];
-    ln_resolve_one<CAP>(A, j, make_uint2(rp->out_size, rp->flags), B.ntok[j], B.tok + B.tokoff[j], win);
+    ln_resolve_one<CAP, NT>(A, j, make_uint2(rp->out_size, rp->flags), n, B.tok + B.tokoff[j], win);
 }
 
 // 64 KiB segments whose two 32 KiB halves are independent (every libdmx 64 KiB block: its halves
 // were matched separately): two items per segment, each rebuilt in a 32 KiB window -- five
 // windows per CU instead of two 64 KiB ones.  Item 2j + h: half h, token words [0, split) or
 // [split, n), written at j * slot + 32768 h; a stored segment is copied whole by item 2j.
-__global__ __launch_bounds__(64) void k_inflate_resolve_half(InflateArgs A, LaneArgs B) {
+template <uint32_t NT>
+__global__ __launch_bounds__(NT) void k_inflate_resolve_half(InflateArgs A, LaneArgs B) {
     __shared__ __attribute__((aligned(16))) uint8_t win[LN_OUT_CAP];
     const uint64_t j = blockIdx.x >> 1;
     const uint32_t h = blockIdx.x & 1;
@@ -1236,12 +1361,14 @@ __global__ __launch_bounds__(64) void k_inflate_resolve_half(InflateArgs A, Lane
     const uint32_t size = rp->out_size, n = B.ntok[j];
     const uint32_t* const tk = B.tok + B.tokoff[j];
     if (sp == 0) {  // stored (or empty): one item copies it
-        if (h == 0) ln_resolve_one<LN_OUT_CAP>(A, j, make_uint2(size, rp->flags), n, tk, win);
+        if (h == 0 && rs_mine<NT>(n)) ln_resolve_one<LN_OUT_CAP, NT>(A, j, make_uint2(size, rp->flags), n, tk, win);
         return;
     }
-    if (h == 0) ln_resolve_one<LN_OUT_CAP>(A, j, make_uint2(min(size, LN_OUT_CAP), rp->flags), sp, tk, win);
-    else if (size > LN_OUT_CAP)
-        ln_resolve_one<LN_OUT_CAP>(A, j, make_uint2(size - LN_OUT_CAP, rp->flags), n - sp, tk + sp, win, LN_OUT_CAP);
+    if (h == 0) {
+        if (rs_mine<NT>(sp)) ln_resolve_one<LN_OUT_CAP, NT>(A, j, make_uint2(min(size, LN_OUT_CAP), rp->flags), sp, tk, win);
+    } else if (size > LN_OUT_CAP && rs_mine<NT>(n - sp)) {
+        ln_resolve_one<LN_OUT_CAP, NT>(A, j, make_uint2(size - LN_OUT_CAP, rp->flags), n - sp, tk + sp, win, LN_OUT_CAP);
+    }
 }
 
 // number of dense candidates (*cnt zeroed by the caller)
@@ -1305,12 +1432,18 @@ hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* t
         constexpr uint32_t NL = LN_LANES;
         const dim3 lg((uint32_t)((A.ncand + NL - 1) / NL));
         hipLaunchKernelGGL((k_inflate_lanes<2 * LN_OUT_CAP, NL>), lg, dim3(64), 0, st, A, B);
-        hipLaunchKernelGGL(k_inflate_resolve_half, dim3((uint32_t)(2 * A.ncand)), dim3(64), 0, st, A, B);
-        hipLaunchKernelGGL(k_inflate_resolve<2 * LN_OUT_CAP>, dim3((uint32_t)A.ncand), dim3(64), 0, st, A, B);
+        hipLaunchKernelGGL(k_inflate_resolve_half<RS_NT>, dim3((uint32_t)(2 * A.ncand)), dim3(RS_NT), 0, st, A, B);
+        hipLaunchKernelGGL((k_inflate_resolve<2 * LN_OUT_CAP, RS_NT>), dim3((uint32_t)A.ncand), dim3(RS_NT), 0, st, A, B);
+        if (kRsSplit) {
+            hipLaunchKernelGGL(k_inflate_resolve_half<64>, dim3((uint32_t)(2 * A.ncand)), dim3(64), 0, st, A, B);
+            hipLaunchKernelGGL((k_inflate_resolve<2 * LN_OUT_CAP, 64>), dim3((uint32_t)A.ncand), dim3(64), 0, st, A, B);
+        }
     } else {
         const dim3 lg((uint32_t)((A.ncand + LN_LANES - 1) / LN_LANES));
         hipLaunchKernelGGL((k_inflate_lanes<LN_OUT_CAP, LN_LANES>), lg, dim3(64), 0, st, A, B);
-        hipLaunchKernelGGL(k_inflate_resolve<LN_OUT_CAP>, dim3((uint32_t)A.ncand), dim3(64), 0, st, A, B);
+        hipLaunchKernelGGL((k_inflate_resolve<LN_OUT_CAP, RS_NT>), dim3((uint32_t)A.ncand), dim3(RS_NT), 0, st, A, B);
+        if (kRsSplit)
+            hipLaunchKernelGGL((k_inflate_resolve<LN_OUT_CAP, 64>), dim3((uint32_t)A.ncand), dim3(64), 0, st, A, B);
     }
     if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();
