@@ -954,7 +954,7 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
         const uint64_t per = (std::max<uint64_t>(LN_OUT_CAP_BYTES, c->seg) / 2 + 2 + 16 + 3) & ~3ull;
         const uint64_t words = std::min<uint64_t>(ncand * per, 8ull * n + 20ull * ncand);
         if (c->ltok.ensure(words * 4) && c->ltokoff.ensure(scan_words(ncand) * 8) &&
-            c->lntok.ensure(ncand * 4) && c->lcaps.ensure(ncand * 4) && c->lsplit.ensure(ncand * 4)) {
+            c->lntok.ensure(ncand * 4) && c->lcaps.ensure(ncand * 4) && c->lsplit.ensure(ncand * 4 + 8)) {
             plan[np][0] = 4, plan[np][1] = c->seg, np++;
             // (the workgroup decoder of the heavy route takes segments of <= 32 KiB)
             if (heavy_bytes && c->seg <= 32768 && ncand < 0xFFFFFFF0ull && c->lheavy.ensure((ncand + 2) * 4)) {
@@ -1229,7 +1229,7 @@ int inflate_device_async_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8
     if (!c->tiles.ensure(ntiles * 4) || !c->tileoffs.ensure(scan_words(ntiles) * 8) || !c->cands.ensure(ncap * 8) ||
         !c->recs.ensure(ncap * sizeof(SegRecord)) || !c->status.ensure(ncap * 8) || !c->ltok.ensure(words_tok * 4) ||
         !c->ltokoff.ensure(scan_words(ncap) * 8) || !c->lntok.ensure(ncap * 4) || !c->lcaps.ensure(ncap * 4) ||
-        !c->lsplit.ensure(ncap * 4))
+        !c->lsplit.ensure(ncap * 4 + 8))
         return DMX_ERR_NOMEM;
     HIPCHK(launch_marker_count(words, misalign, n, c->tiles.as<uint32_t>(), ntiles, st));
     HIPCHK(launch_scan_u32(c->tiles.as<uint32_t>(), c->tileoffs.as<uint64_t>(), ntiles, &ds->nmarkers, st));

@@ -106,6 +106,10 @@ constexpr uint32_t RS_NT = DMX_RS_NT;
 constexpr uint32_t RS_BIG = DMX_RS_BIG;
 static_assert(RS_NT % 64 == 0 && RS_NT <= 1024, "resolve workgroup");
 constexpr bool kRsSplit = DMX_RS_SPLIT && RS_NT > 64;
+#ifndef DMX_RS_TICKET_WG
+#define DMX_RS_TICKET_WG 5
+#endif
+constexpr uint32_t RS_TICKET_WG = DMX_RS_TICKET_WG;  // one-wave resolve workgroups per CU
 
 __constant__ const uint8_t kLnPerm[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5,
                                           11, 4,  12, 3, 13, 2, 14, 1, 15};
@@ -116,7 +120,9 @@ struct LaneArgs {
     uint32_t* ntok;         // ncand token counts
     uint32_t* caps;         // ncand capacities (words)
     uint32_t* split;        // 64 KiB segments: ncand first-word indices of the second 32 KiB
-                            // half (~0: not split; 0 for a stored segment)
+                            // half (~0: not split; 0 for a stored segment).  32 KiB segments:
+                            // [0] a count, [1] a ticket, then the candidates whose token lists
+                            // the one-wave resolve takes (ncand + 2 words)
 };
 
 // lit/len table entry: literal / end-of-block  0 | cl(4) << 11 | sym(9)
@@ -888,6 +894,9 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
     r.flags = flags | (fin ? SEGF_FINAL : 0u);
     A.recs[j] = r;
     B.ntok[j] = ntok;
+    // 32 KiB segments: a long token list goes on the one-wave resolve's list (the rest: the
+    // workgroup resolve, launched over every candidate)
+    if (!SPLIT && kRsSplit && !(r.flags & ~SEGF_FINAL) && ntok > RS_FOLLOW) B.split[2 + atomicAdd(B.split, 1u)] = (uint32_t)j;
     // the split holds only if the output crossed HALF at a token boundary, or never reached it
     if (SPLIT) B.split[j] = (flags || xhalf || (outpos > HALF && split == ~0u)) ? ~0u : (outpos <= HALF ? ntok : split);
     if (dbg) {  // (slots 5..7 belong to k_inflate_resolve)
@@ -914,9 +923,12 @@ __device__ __forceinline__ bool ln_dense(const uint8_t* in, uint64_t start, uint
 // lane declines it: SEGF_EXOTIC) and is appended to the list hl[2..] (hl[0] = its length)
 // for the workgroup decoder (mode 6): a lane decodes ~1 symbol per 1000 cycles, so one dense
 // segment sets the time of a wave.
+// (rsl: the one-wave resolve's count and ticket, zeroed here for the lanes that follow)
 __global__ void k_lane_caps(const uint8_t* in, const uint64_t* cands, uint64_t ncand, uint64_t n, uint32_t* caps,
-                            uint32_t heavy, uint32_t limit, uint32_t* hl, uint32_t ocap, const uint64_t* ncand_dev) {
+                            uint32_t heavy, uint32_t limit, uint32_t* hl, uint32_t ocap, const uint64_t* ncand_dev,
+                            uint32_t* rsl) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (rsl && j < 2) rsl[j] = 0;
     if (j >= ncand) return;
     if (ncand_dev && j >= *ncand_dev) {  // (async: past the device-side count)
         caps[j] = 0;
@@ -1337,6 +1349,21 @@ template <uint32_t CAP, uint32_t NT>
 __global__ __launch_bounds__(NT) void k_inflate_resolve(InflateArgs A, LaneArgs B) {
     __shared__ __attribute__((aligned(16))) uint8_t win[CAP];  // 32 KiB: five per CU; 64 KiB: two
     const uint64_t j = blockIdx.x;
+    if constexpr (CAP == LN_OUT_CAP && NT == 64 && kRsSplit) {
+        // the long token lists listed by the lanes, drawn by ticket (a grid over every candidate
+        // kept a 32 KiB window per empty workgroup: ~15 us on 1 GiB of repeat, which has none)
+        const uint32_t cnt = B.split[0];
+        for (;;) {
+            uint32_t i = 0;
+            if (threadIdx.x == 0) i = atomicAdd(B.split + 1, 1u);
+            i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
+            if (i >= cnt) break;
+            const uint32_t jj = B.split[2 + i];
+            const SegRecord* const rp = &A.recs[jj];
+            ln_resolve_one<CAP, NT>(A, jj, make_uint2(rp->out_size, rp->flags), B.ntok[jj], B.tok + B.tokoff[jj], win);
+        }
+        return;
+    }
     if (j >= cand_count(A)) return;
     if (CAP > LN_OUT_CAP && B.split[j] != ~0u) return;  // rebuilt by k_inflate_resolve_half
     const uint32_t n = B.ntok[j];
@@ -1422,7 +1449,7 @@ hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* t
     }
     const bool big = A.slot > LN_OUT_CAP;  // 64 KiB segments (config C4's blocks)
     hipLaunchKernelGGL(k_lane_caps, dim3(g), dim3(256), 0, st, in, A.cands, A.ncand, A.n, caps, heavy, limit, hl,
-                       big ? 2 * LN_OUT_CAP : LN_OUT_CAP, A.ncand_dev);
+                       big ? 2 * LN_OUT_CAP : LN_OUT_CAP, A.ncand_dev, !big && kRsSplit ? split : nullptr);
     hipError_t e = launch_scan_u32(caps, tokoff, A.ncand, tokoff + A.ncand, st);
     if (e != hipSuccess) return e;
     LaneArgs B{tok, tokoff, ntok, caps, split};
@@ -1442,8 +1469,17 @@ hipError_t launch_inflate_lanes(const InflateArgs& A, uint32_t* tok, uint64_t* t
         const dim3 lg((uint32_t)((A.ncand + LN_LANES - 1) / LN_LANES));
         hipLaunchKernelGGL((k_inflate_lanes<LN_OUT_CAP, LN_LANES>), lg, dim3(64), 0, st, A, B);
         hipLaunchKernelGGL((k_inflate_resolve<LN_OUT_CAP, RS_NT>), dim3((uint32_t)A.ncand), dim3(RS_NT), 0, st, A, B);
-        if (kRsSplit)
-            hipLaunchKernelGGL((k_inflate_resolve<LN_OUT_CAP, 64>), dim3((uint32_t)A.ncand), dim3(64), 0, st, A, B);
+        if (kRsSplit) {
+            static int ncu = 0;
+            if (!ncu) {
+                int dev = 0;
+                (void)hipGetDevice(&dev);
+                if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+                    ncu = 256;
+            }
+            const uint32_t g = (uint32_t)std::min<uint64_t>(A.ncand, (uint64_t)RS_TICKET_WG * (uint64_t)ncu);
+            if (g) hipLaunchKernelGGL((k_inflate_resolve<LN_OUT_CAP, 64>), dim3(g), dim3(64), 0, st, A, B);
+        }
     }
     if (ev1) (void)hipEventRecord(ev1, st);
     return hipGetLastError();
