@@ -1364,12 +1364,18 @@ __global__ __launch_bounds__(NT) void k_inflate_resolve(InflateArgs A, LaneArgs 
         }
         return;
     }
-    if (j >= cand_count(A)) return;
-    if (CAP > LN_OUT_CAP && B.split[j] != ~0u) return;  // rebuilt by k_inflate_resolve_half
-    const uint32_t n = B.ntok[j];
-    if (!rs_mine<NT>(n)) return;
+    // (j < A.ncand: the record, count and offset loads go out together, before the tests -- the
+    // compiler otherwise sinks each below the test before it, a chain of scalar-load latencies)
     const SegRecord* const rp = &A.recs[j];
-    ln_resolve_one<CAP, NT>(A, j, make_uint2(rp->out_size, rp->flags), n, B.tok + B.tokoff[j], win);
+    const uint32_t n = B.ntok[j];
+    const uint2 sf = make_uint2(rp->out_size, rp->flags);
+    const uint64_t to = B.tokoff[j];
+    const uint64_t cc = cand_count(A);
+    asm volatile("" ::"s"(n), "s"(sf.x), "s"(sf.y), "s"(to), "s"(cc));
+    if (j >= cc) return;
+    if (CAP > LN_OUT_CAP && B.split[j] != ~0u) return;  // rebuilt by k_inflate_resolve_half
+    if (!rs_mine<NT>(n)) return;
+    ln_resolve_one<CAP, NT>(A, j, sf, n, B.tok + to, win);
 }
 
 // 64 KiB segments whose two 32 KiB halves are independent (every libdmx 64 KiB block: its halves
