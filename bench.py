@@ -343,7 +343,8 @@ def corpus_record(run, kind, level, steps, tag=None):
     run.torch.cuda.synchronize(run.dev)
     s = summarize(recs, run.n)
     n = run.n
-    inf_k = ["k_inflate_lanes", "k_inflate_resolve", "k_inflate_resolve_half", "k_inflate_pj_list"]
+    inf_k = ["k_inflate_lanes", "k_inflate_resolve", "k_inflate_resolve_wave", "k_inflate_resolve_half",
+             "k_inflate_resolve_half_wave", "k_inflate_pj_list"]
     return {"bytes": n, "level": level, "roundtrip_ok": ok,
             "roundtrip_GBps": round(n / ((s["t_def"] + s["t_inf"]) * 1e-3) / 1e9, 3),
             "deflate_GBps": round(n / (s["t_def"] * 1e-3) / 1e9, 3),

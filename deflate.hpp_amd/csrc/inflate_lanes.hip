@@ -1352,15 +1352,16 @@ __global__ __launch_bounds__(NT) void k_inflate_resolve(InflateArgs A, LaneArgs 
     if constexpr (CAP == LN_OUT_CAP && NT == 64 && kRsSplit) {
         // the long token lists listed by the lanes, drawn by ticket (a grid over every candidate
         // kept a 32 KiB window per empty workgroup: ~15 us on 1 GiB of repeat, which has none)
+        // (the first item is the workgroup's own index: no ticket traffic when the list is
+        // short or empty -- 1280 tickets drawn on one word took ~15 us)
         const uint32_t cnt = B.split[0];
-        for (;;) {
-            uint32_t i = 0;
-            if (threadIdx.x == 0) i = atomicAdd(B.split + 1, 1u);
-            i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
+        for (uint32_t i = blockIdx.x;;) {
             if (i >= cnt) break;
             const uint32_t jj = B.split[2 + i];
             const SegRecord* const rp = &A.recs[jj];
             ln_resolve_one<CAP, NT>(A, jj, make_uint2(rp->out_size, rp->flags), B.ntok[jj], B.tok + B.tokoff[jj], win);
+            if (threadIdx.x == 0) i = gridDim.x + atomicAdd(B.split + 1, 1u);
+            i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
         }
         return;
     }

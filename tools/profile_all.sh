@@ -23,16 +23,21 @@ if [ "$mode" = collect ]; then
     for k in k_deflate_segments k_deflate_emit k_inflate_lanes k_inflate_pj_list; do
       python3 tools/traffic.py $P/f_$c$l $P/w_$c$l $c:$N:$l:$k $k profiles/traffic.json || true
     done
-    # (templated name: not the 64 KiB half resolve)
-    python3 tools/traffic.py $P/f_$c$l $P/w_$c$l $c:$N:$l:k_inflate_resolve "k_inflate_resolve<" profiles/traffic.json || true
+    # (templated names: the workgroup resolve and the one-wave resolve of long token lists, two
+    # launches per call, each averaged over its own dispatches; not the 64 KiB half resolve)
+    python3 tools/traffic.py $P/f_$c$l $P/w_$c$l $c:$N:$l:k_inflate_resolve "k_inflate_resolve<32768u, 256u>" profiles/traffic.json || true
+    python3 tools/traffic.py $P/f_$c$l $P/w_$c$l $c:$N:$l:k_inflate_resolve_wave "k_inflate_resolve<32768u, 64u>" profiles/traffic.json || true
   done
   # config C4's 64 KiB blocks (bench sub-record c4_64k): the mixed corpus at segment_bytes 65536
   if [ -d $P/s_c4 ]; then
     cp $(ls -t $(find $P/s_c4 -name "*kernel_stats.csv") | head -1) profiles/${tag}_kstats_c4_64k_L2.csv
-    for k in k_deflate_segments k_deflate_emit k_inflate_lanes k_inflate_resolve_half; do
+    for k in k_deflate_segments k_deflate_emit k_inflate_lanes; do
       python3 tools/traffic.py $P/f_c4 $P/w_c4 c4_64k:$N:2:$k $k profiles/traffic.json || true
     done
-    python3 tools/traffic.py $P/f_c4 $P/w_c4 c4_64k:$N:2:k_inflate_resolve "k_inflate_resolve<" profiles/traffic.json || true
+    python3 tools/traffic.py $P/f_c4 $P/w_c4 c4_64k:$N:2:k_inflate_resolve_half "k_inflate_resolve_half<256u>" profiles/traffic.json || true
+    python3 tools/traffic.py $P/f_c4 $P/w_c4 c4_64k:$N:2:k_inflate_resolve_half_wave "k_inflate_resolve_half<64u>" profiles/traffic.json || true
+    python3 tools/traffic.py $P/f_c4 $P/w_c4 c4_64k:$N:2:k_inflate_resolve "k_inflate_resolve<65536u, 256u>" profiles/traffic.json || true
+    python3 tools/traffic.py $P/f_c4 $P/w_c4 c4_64k:$N:2:k_inflate_resolve_wave "k_inflate_resolve<65536u, 64u>" profiles/traffic.json || true
   fi
   if [ -d $P/s_c3 ]; then
     cp $(ls -t $(find $P/s_c3 -name "*kernel_stats.csv") | head -1) profiles/${tag}_kstats_c3_zlib1.csv
