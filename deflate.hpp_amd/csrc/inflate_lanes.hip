@@ -75,6 +75,10 @@ constexpr uint32_t LN_LANES = DMX_LN_LANES;
 #ifndef DMX_LN_PAIR
 #define DMX_LN_PAIR 1
 #endif
+// lane tables: the code-length words read ahead of their use (1) or at it (0)
+#ifndef DMX_LN_PREF
+#define DMX_LN_PREF 1
+#endif
 // precode tables: one per lane, all segments at once (1), or built by the whole wave one segment
 // after the other (0, ln_coop_table)
 #ifndef DMX_LN_PRETAB
@@ -244,8 +248,17 @@ __device__ __forceinline__ bool ln_lane_table(uint16_t* T, const Pk9& cnt, uint3
 #pragma unroll 4
     for (uint32_t w = 0; w < NW / 2; w++) T64w[(w + lane) & (NW / 2 - 1)] = m4;
     // symbols below NL (a multiple of 8, < nsym): entry (L << lsh) | sym, no bound test
+    // (DMX_LN_PREF: each word read one iteration ahead, its LDS latency behind the 8 symbols)
+#if DMX_LN_PREF
+    uint32_t xn = word(0);
+#endif
     for (uint32_t k = 0; 8 * k < (uint32_t)NL; k++) {
+#if DMX_LN_PREF
+        const uint32_t x = xn;
+        xn = word(k + 1);  // (k + 1 <= NL / 8: the next loop's first word)
+#else
         const uint32_t x = word(k);
+#endif
 #pragma unroll
         for (uint32_t i = 0; i < 8; i++) {
             const uint32_t sym = 8 * k + i, L = (x >> (4 * i)) & 15u;
@@ -257,7 +270,11 @@ __device__ __forceinline__ bool ln_lane_table(uint16_t* T, const Pk9& cnt, uint3
         }
     }
     for (uint32_t k = NL / 8; 8 * k < nsym; k++) {
+#if DMX_LN_PREF
+        const uint32_t x = k == NL / 8 && NL > 0 ? xn : word(k);
+#else
         const uint32_t x = word(k);
+#endif
 #pragma unroll
         for (uint32_t i = 0; i < 8; i++) {
             const uint32_t sym = 8 * k + i, L = (x >> (4 * i)) & 15u;
@@ -623,6 +640,9 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(InflateArgs A, LaneArgs B)
         uint32_t* const PD = reinterpret_cast<uint32_t*>(R + LN_DIST);             // words 32..39
         const uint32_t* const LW = reinterpret_cast<const uint32_t*>(R + LN_LENS);
         Pk9 cl = {0ull, 0u}, cd = {0ull, 0u};
+#if DMX_LN_PREF
+#pragma unroll 8
+#endif
         for (uint32_t k = 0; k < 40; k++) {
             // fixed code (RFC 1951 3.2.6): 8 (0..143), 9 (144..255), 7 (256..279), 8 (280..287), 5
             const uint32_t fw = k < 18 ? 0x88888888u : k < 32 ? 0x99999999u : k < 35 ? 0x77777777u
