@@ -953,8 +953,21 @@ int inflate_device_locked(dmx_ctx* c, const uint8_t* d_in, size_t n, uint8_t* fi
         // k_lane_caps: min(8 bits, slot / 2 + 2) + 16 words per candidate, in groups of four
         const uint64_t per = (std::max<uint64_t>(LN_OUT_CAP_BYTES, c->seg) / 2 + 2 + 16 + 3) & ~3ull;
         const uint64_t words = std::min<uint64_t>(ncand * per, 8ull * n + 20ull * ncand);
-        if (c->ltok.ensure(words * 4) && c->ltokoff.ensure(scan_words(ncand) * 8) &&
-            c->lntok.ensure(ncand * 4) && c->lcaps.ensure(ncand * 4) && c->lsplit.ensure(ncand * 4 + 8)) {
+        auto lane_bufs = [&]() {
+            return c->ltok.ensure(words * 4) && c->ltokoff.ensure(scan_words(ncand) * 8) &&
+                   c->lntok.ensure(ncand * 4) && c->lcaps.ensure(ncand * 4) && c->lsplit.ensure(ncand * 4 + 8);
+        };
+        // short of device memory: drop the scratch this call does not use (the deflate's token
+        // words and slots, path 5's token space and images, chain-repair scratch) and try again
+        // before the plan goes past the lane decoder
+        bool lanes_ok = lane_bufs();
+        if (!lanes_ok) {
+            for (DevBuf* b : {&c->dtok, &c->slots, &c->rtmp, &c->fbt, &c->fbimg, &c->fbwin, &c->fbopen, &c->fbk,
+                              &c->fbu, &c->fbJ, &c->fbJraw, &c->fbJsub})
+                b->release();
+            lanes_ok = lane_bufs();
+        }
+        if (lanes_ok) {
             plan[np][0] = 4, plan[np][1] = c->seg, np++;
             // (the workgroup decoder of the heavy route takes segments of <= 32 KiB)
             if (heavy_bytes && c->seg <= 32768 && ncand < 0xFFFFFFF0ull && c->lheavy.ensure((ncand + 2) * 4)) {
