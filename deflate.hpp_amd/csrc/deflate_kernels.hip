@@ -1235,10 +1235,26 @@ __global__ __launch_bounds__(DF_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 constexpr int EM_NW = 4;          // waves (segments) per 256-thread workgroup
 constexpr int EM_FLUSH = 256;     // staged whole words that trigger a flush to HBM
 constexpr int EM_STG = 576;       // staging words: EM_FLUSH + one block (256 x 36 bits) + slack
+// EmWave: the symbol counts share their LDS with the bit-staging window (1), and the emission
+// kernel asks for DMX_EM_OCC waves per SIMD (0: the compiler's choice)
+#ifndef DMX_EM_UNION
+#define DMX_EM_UNION 1
+#endif
+#ifndef DMX_EM_OCC
+#define DMX_EM_OCC 6
+#endif
 constexpr int EM_LIT = 288, EM_SYM = 320;  // lit/len symbols at [0, 288), distance at [288, 320)
 
 struct EmWave {
+#if DMX_EM_UNION
+    // the symbol counts die with the code build; the bit-staging window starts after it
+    union {
+        uint32_t freq[EM_SYM];
+        uint32_t stg[EM_STG];
+    };
+#else
     uint32_t freq[EM_SYM];
+#endif
     uint32_t code[EM_SYM];   // (len << 16) | bit-reversed code
     uint8_t len[EM_SYM];
     uint16_t rk[EM_SYM];     // per symbol slot: half-class | rank in it, then rank in its length;
@@ -1251,7 +1267,9 @@ struct EmWave {
     uint32_t kpre[2][20];    // per alphabet: members of the half-classes below k
     uint32_t start[2][16];   // per alphabet: first rank of code length l
     uint32_t next[2][16];    // per alphabet: first canonical code of length l
+#if !DMX_EM_UNION
     uint32_t stg[EM_STG];
+#endif
 };
 
 struct EmCodes {
@@ -1831,7 +1849,11 @@ __device__ void em_segment(const DeflateArgs& A, EmWave& W, uint64_t seg) {
 
 // RAW: level 1 (the input's bytes are the tokens) and level 0; else the front kernel's words
 template <int SEG, bool RAW>
-__global__ __launch_bounds__(64 * EM_NW) void k_deflate_emit(DeflateArgs A) {
+__global__ __launch_bounds__(64 * EM_NW)
+#if DMX_EM_OCC
+__attribute__((amdgpu_waves_per_eu(DMX_EM_OCC)))
+#endif
+void k_deflate_emit(DeflateArgs A) {
     __shared__ EmWave Ws[EM_NW];
     const uint64_t seg = (uint64_t)blockIdx.x * EM_NW + (threadIdx.x >> 6);
     if (seg >= A.nseg) return;
